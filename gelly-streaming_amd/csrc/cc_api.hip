@@ -1,0 +1,546 @@
+// cc_api.hip — the extern "C" boundary of libgsgpu.so (declared in include/gsgpu.h).
+// Host-side orchestration of one DisjointSet summary per handle: staging of host buffers,
+// kernel launches on the handle's stream, deferred device error reporting, instrumentation.
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "cc_kernels.hpp"
+
+namespace gsgpu {
+
+std::string& last_error() {
+    static thread_local std::string s;
+    return s;
+}
+
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    last_error() = buf;
+    return code;
+}
+
+bool is_device_pointer(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();   // pageable host memory is unknown to the runtime
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.isManaged;
+}
+
+static unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap_blocks) {
+    uint64_t b = (items + per_block - 1) / per_block;
+    if (b == 0) b = 1;
+    return (unsigned)(b < cap_blocks ? b : cap_blocks);
+}
+
+}  // namespace gsgpu
+
+using namespace gsgpu;
+
+struct gs_cc {
+    gs_cc_config cfg{};
+    uint32_t cap = 0;
+    int device = 0;
+    hipStream_t own = nullptr, stream = nullptr;
+    uint32_t* parent = nullptr;          // dense summary / label array
+    uint8_t* mark = nullptr;             // per-vertex export marks (GS_CC_TRACK_MARKS)
+    uint32_t* derr = nullptr;            // deferred device error flags
+    unsigned long long* dscratch = nullptr;  // reduction outputs (8 words)
+    unsigned long long* hscratch = nullptr;  // pinned mirror
+    void* stage = nullptr;               // host->device staging (2 * staging_edges ids)
+    size_t stage_bytes = 0;
+    void* tmp = nullptr;                 // emission temporaries
+    size_t tmp_bytes = 0;
+    bool compressed = true;
+    // instrumentation
+    bool timing = false;
+    struct Pend { int k; hipEvent_t a, b; };
+    std::vector<Pend> pending;
+    std::vector<hipEvent_t> pool;
+    double total_ms[GS_K_COUNT] = {};
+    uint64_t launches[GS_K_COUNT] = {};
+};
+
+namespace {
+
+int check(gs_cc_t* h) {
+    if (!h) return fail(GS_ERR_INVALID, "null handle");
+    return GS_OK;
+}
+
+int ensure_buf(void** p, size_t* have, size_t need) {
+    if (*have >= need) return GS_OK;
+    if (*p) { GS_HIP(hipFree(*p)); *p = nullptr; *have = 0; }
+    if (hipMalloc(p, need) != hipSuccess) { (void)hipGetLastError(); return fail(GS_ERR_NOMEM, "hipMalloc(%zu) failed", need); }
+    *have = need;
+    return GS_OK;
+}
+
+hipEvent_t get_event(gs_cc_t* h) {
+    if (!h->pool.empty()) { hipEvent_t e = h->pool.back(); h->pool.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+// brackets one kernel launch with events when timing is on
+struct KTimer {
+    gs_cc_t* h; int k; hipEvent_t a = nullptr;
+    KTimer(gs_cc_t* h_, int k_) : h(h_), k(k_) {
+        if (h->timing) { a = get_event(h); (void)hipEventRecord(a, h->stream); }
+    }
+    ~KTimer() {
+        if (!h->timing || !a) return;
+        hipEvent_t b = get_event(h);
+        (void)hipEventRecord(b, h->stream);
+        h->pending.push_back({k, a, b});
+    }
+};
+
+int resolve_timing(gs_cc_t* h) {
+    for (auto& p : h->pending) {
+        GS_HIP(hipEventSynchronize(p.b));
+        float ms = 0.f;
+        GS_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+        h->total_ms[p.k] += ms;
+        h->launches[p.k] += 1;
+        h->pool.push_back(p.a);
+        h->pool.push_back(p.b);
+    }
+    h->pending.clear();
+    return GS_OK;
+}
+
+int sync_and_check(gs_cc_t* h) {
+    uint32_t* hflag = reinterpret_cast<uint32_t*>(h->hscratch + 7);
+    GS_HIP(hipMemcpyAsync(hflag, h->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+    GS_HIP(hipStreamSynchronize(h->stream));
+    if (*hflag) {
+        *hflag = 0;
+        GS_HIP(hipMemsetAsync(h->derr, 0, sizeof(uint32_t), h->stream));
+        return fail(GS_ERR_RANGE, "a vertex id outside [0, %u) was folded; such edges were skipped", h->cap);
+    }
+    return GS_OK;
+}
+
+template <typename IdT, bool AOS>
+void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n) {
+    const unsigned grid = grid_for((n + kEdgesPerThread - 1) / kEdgesPerThread, kFoldThreads, 16384);
+    RangeCheck rc{h->cap, h->derr};
+    KTimer t(h, GS_K_FOLD);
+    if (h->mark)
+        hipLaunchKernelGGL((k_fold<IdT, AOS, true>), dim3(grid), dim3(kFoldThreads), 0, h->stream,
+                           (const IdT*)a, (const IdT*)b, n, h->parent, h->mark, rc);
+    else
+        hipLaunchKernelGGL((k_fold<IdT, AOS, false>), dim3(grid), dim3(kFoldThreads), 0, h->stream,
+                           (const IdT*)a, (const IdT*)b, n, h->parent, h->mark, rc);
+}
+
+int fold_impl(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, uint32_t id_bits) {
+    GS_TRY(check(h));
+    if (n == 0) return GS_OK;
+    if (!a || (!aos && !b)) return fail(GS_ERR_INVALID, "fold: null edge buffer");
+    DeviceGuard g(h->device);
+    const size_t esz = id_bits / 8;
+    const bool dev = is_device_pointer(a) && (aos || is_device_pointer(b));
+    h->compressed = false;
+    if (dev) {
+        if (id_bits == 32) { if (aos) launch_fold<uint32_t, true>(h, a, b, n); else launch_fold<uint32_t, false>(h, a, b, n); }
+        else { if (aos) launch_fold<int64_t, true>(h, a, b, n); else launch_fold<int64_t, false>(h, a, b, n); }
+        GS_HIP(hipGetLastError());
+        return GS_OK;
+    }
+    // host buffers: stage chunk by chunk (stream order protects the staging buffer)
+    const uint64_t chunk = h->cfg.staging_edges ? h->cfg.staging_edges : (1ull << 22);
+    GS_TRY(ensure_buf(&h->stage, &h->stage_bytes, (size_t)chunk * esz * 2));
+    for (uint64_t off = 0; off < n; off += chunk) {
+        const uint64_t m = (n - off < chunk) ? (n - off) : chunk;
+        char* s0 = static_cast<char*>(h->stage);
+        char* s1 = s0 + (size_t)chunk * esz;
+        if (aos) {
+            GS_HIP(hipMemcpyAsync(s0, static_cast<const char*>(a) + off * esz * 2, m * esz * 2, hipMemcpyHostToDevice, h->stream));
+        } else {
+            GS_HIP(hipMemcpyAsync(s0, static_cast<const char*>(a) + off * esz, m * esz, hipMemcpyHostToDevice, h->stream));
+            GS_HIP(hipMemcpyAsync(s1, static_cast<const char*>(b) + off * esz, m * esz, hipMemcpyHostToDevice, h->stream));
+        }
+        if (id_bits == 32) { if (aos) launch_fold<uint32_t, true>(h, s0, s1, m); else launch_fold<uint32_t, false>(h, s0, s1, m); }
+        else { if (aos) launch_fold<int64_t, true>(h, s0, s1, m); else launch_fold<int64_t, false>(h, s0, s1, m); }
+        GS_HIP(hipGetLastError());
+    }
+    return GS_OK;
+}
+
+int compress_impl(gs_cc_t* h) {
+    if (h->compressed) return GS_OK;
+    {
+        KTimer t(h, GS_K_COMPRESS);
+        hipLaunchKernelGGL(k_compress, dim3(grid_for((h->cap + 3) / 4, 256, 16384)), dim3(256), 0, h->stream,
+                           h->parent, h->cap);
+    }
+    GS_HIP(hipGetLastError());
+    h->compressed = true;
+    return GS_OK;
+}
+
+int stats_impl(gs_cc_t* h, bool checksum, uint64_t* nv, uint64_t* nc, uint64_t* sum) {
+    GS_HIP(hipMemsetAsync(h->dscratch, 0, 3 * sizeof(unsigned long long), h->stream));
+    const dim3 grid(grid_for(h->cap, 256, 4096));
+    if (checksum) hipLaunchKernelGGL(k_stats<true>, grid, dim3(256), 0, h->stream, h->parent, h->cap, h->dscratch);
+    else hipLaunchKernelGGL(k_stats<false>, grid, dim3(256), 0, h->stream, h->parent, h->cap, h->dscratch);
+    GS_HIP(hipGetLastError());
+    GS_HIP(hipMemcpyAsync(h->hscratch, h->dscratch, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
+    GS_TRY(sync_and_check(h));
+    if (nv) *nv = h->hscratch[0];
+    if (nc) *nc = h->hscratch[1];
+    if (sum) *sum = h->hscratch[2];
+    return GS_OK;
+}
+
+// copy n bytes of device data to dst (device or host)
+int copy_out(gs_cc_t* h, void* dst, const void* src, size_t n) {
+    GS_HIP(hipMemcpyAsync(dst, src, n, is_device_pointer(dst) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, h->stream));
+    return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_version(void) { return GSGPU_VERSION; }
+const char* gs_last_error(void) { return last_error().c_str(); }
+
+int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
+    if (!out || !cfg) return fail(GS_ERR_INVALID, "gs_cc_create: null argument");
+    *out = nullptr;
+    if (cfg->struct_size != sizeof(gs_cc_config))
+        return fail(GS_ERR_INVALID, "gs_cc_create: struct_size %u != %zu", cfg->struct_size, sizeof(gs_cc_config));
+    if (cfg->id_bits != 32 && cfg->id_bits != 64) return fail(GS_ERR_INVALID, "gs_cc_create: id_bits must be 32 or 64");
+    if (cfg->vertex_capacity == 0 || cfg->vertex_capacity > 0xFFFFFFFFull)
+        return fail(GS_ERR_INVALID, "gs_cc_create: vertex_capacity must be in [1, 2^32-1]");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        return fail(GS_ERR_HIP, "gs_cc_create: no HIP device available");
+    }
+    if (cfg->device < 0 || cfg->device >= ndev) return fail(GS_ERR_INVALID, "gs_cc_create: device %d of %d", cfg->device, ndev);
+    DeviceGuard g(cfg->device);
+    if (!g.ok) return fail(GS_ERR_HIP, "gs_cc_create: hipSetDevice(%d) failed", cfg->device);
+    gs_cc_t* h = new gs_cc_t();
+    h->cfg = *cfg;
+    h->cap = (uint32_t)cfg->vertex_capacity;
+    h->device = cfg->device;
+    auto bail = [&](int rc) { gs_cc_destroy(h); return rc; };
+    if (hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess) return bail(fail(GS_ERR_HIP, "hipStreamCreate failed"));
+    h->stream = h->own;
+    if (hipMalloc(&h->parent, (size_t)h->cap * sizeof(uint32_t)) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "parent[%u] allocation failed", h->cap)); }
+    if (cfg->flags & GS_CC_TRACK_MARKS) {
+        if (hipMalloc(&h->mark, ((size_t)h->cap + 15) & ~(size_t)15) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "mark allocation failed")); }
+    }
+    if (hipMalloc(&h->derr, 64) != hipSuccess || hipMalloc(&h->dscratch, 8 * sizeof(unsigned long long)) != hipSuccess ||
+        hipHostMalloc(&h->hscratch, 8 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return bail(fail(GS_ERR_NOMEM, "scratch allocation failed"));
+    }
+    std::memset(h->hscratch, 0, 8 * sizeof(unsigned long long));
+    if (hipMemsetAsync(h->derr, 0, 64, h->stream) != hipSuccess) return bail(fail(GS_ERR_HIP, "memset failed"));
+    int rc = gs_cc_reset(h);
+    if (rc != GS_OK) return bail(rc);
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(fail(GS_ERR_HIP, "stream sync failed"));
+    *out = h;
+    return GS_OK;
+}
+
+int gs_cc_destroy(gs_cc_t* h) {
+    if (!h) return GS_OK;
+    DeviceGuard g(h->device);
+    if (h->own) (void)hipStreamSynchronize(h->own);
+    if (h->stream && h->stream != h->own) (void)hipStreamSynchronize(h->stream);
+    for (auto& p : h->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+    for (auto e : h->pool) (void)hipEventDestroy(e);
+    if (h->parent) (void)hipFree(h->parent);
+    if (h->mark) (void)hipFree(h->mark);
+    if (h->derr) (void)hipFree(h->derr);
+    if (h->dscratch) (void)hipFree(h->dscratch);
+    if (h->hscratch) (void)hipHostFree(h->hscratch);
+    if (h->stage) (void)hipFree(h->stage);
+    if (h->tmp) (void)hipFree(h->tmp);
+    if (h->own) (void)hipStreamDestroy(h->own);
+    delete h;
+    return GS_OK;
+}
+
+int gs_cc_reset(gs_cc_t* h) {
+    GS_TRY(check(h));
+    DeviceGuard g(h->device);
+    GS_HIP(hipMemsetAsync(h->parent, 0xFF, (size_t)h->cap * sizeof(uint32_t), h->stream));
+    if (h->mark) GS_HIP(hipMemsetAsync(h->mark, 0, ((size_t)h->cap + 15) & ~(size_t)15, h->stream));
+    h->compressed = true;
+    return GS_OK;
+}
+
+int gs_cc_set_stream(gs_cc_t* h, void* s) {
+    GS_TRY(check(h));
+    h->stream = s ? static_cast<hipStream_t>(s) : h->own;
+    return GS_OK;
+}
+
+int gs_cc_get_stream(gs_cc_t* h, void** s) {
+    GS_TRY(check(h));
+    if (!s) return fail(GS_ERR_INVALID, "null out");
+    *s = h->stream;
+    return GS_OK;
+}
+
+int gs_cc_sync(gs_cc_t* h) {
+    GS_TRY(check(h));
+    DeviceGuard g(h->device);
+    return sync_and_check(h);
+}
+
+int gs_cc_fold(gs_cc_t* h, const void* src, const void* dst, uint64_t n) {
+    GS_TRY(check(h));
+    return fold_impl(h, src, dst, n, false, h->cfg.id_bits);
+}
+
+int gs_cc_fold_pairs(gs_cc_t* h, const void* pairs, uint64_t n) {
+    GS_TRY(check(h));
+    return fold_impl(h, pairs, nullptr, n, true, h->cfg.id_bits);
+}
+
+int gs_cc_fold_pairs32(gs_cc_t* h, const void* pairs, uint64_t n) {
+    GS_TRY(check(h));
+    return fold_impl(h, pairs, nullptr, n, true, 32);
+}
+
+int gs_cc_merge(gs_cc_t* into, gs_cc_t* from) {
+    GS_TRY(check(into));
+    GS_TRY(check(from));
+    if (into == from) return GS_OK;
+    if (into->device != from->device) return fail(GS_ERR_UNSUPPORTED, "gs_cc_merge: summaries on different devices");
+    if (from->cap > into->cap) return fail(GS_ERR_RANGE, "gs_cc_merge: source capacity %u exceeds target %u", from->cap, into->cap);
+    DeviceGuard g(into->device);
+    if (from->stream != into->stream) {
+        hipEvent_t e = get_event(into);
+        GS_HIP(hipEventRecord(e, from->stream));
+        GS_HIP(hipStreamWaitEvent(into->stream, e, 0));
+        into->pool.push_back(e);
+    }
+    into->compressed = false;
+    {
+        KTimer t(into, GS_K_MERGE);
+        const dim3 grid(grid_for(from->cap, 256, 16384));
+        if (into->mark) hipLaunchKernelGGL(k_merge_dense<true>, grid, dim3(256), 0, into->stream, from->parent, from->cap, into->parent, into->mark);
+        else hipLaunchKernelGGL(k_merge_dense<false>, grid, dim3(256), 0, into->stream, from->parent, from->cap, into->parent, into->mark);
+    }
+    GS_HIP(hipGetLastError());
+    if (from->stream != into->stream) {   // `from` must not be reused before the merge read it
+        hipEvent_t e = get_event(into);
+        GS_HIP(hipEventRecord(e, into->stream));
+        GS_HIP(hipStreamWaitEvent(from->stream, e, 0));
+        into->pool.push_back(e);
+    }
+    return GS_OK;
+}
+
+int gs_cc_combine(gs_cc_t* s1, gs_cc_t* s2, gs_cc_t** result) {
+    GS_TRY(check(s1));
+    GS_TRY(check(s2));
+    if (!result) return fail(GS_ERR_INVALID, "gs_cc_combine: null result");
+    uint64_t c1 = 0, c2 = 0;
+    GS_TRY(gs_cc_stats(s1, &c1, nullptr));
+    GS_TRY(gs_cc_stats(s2, &c2, nullptr));
+    if (c1 <= c2) { GS_TRY(gs_cc_merge(s2, s1)); *result = s2; }
+    else { GS_TRY(gs_cc_merge(s1, s2)); *result = s1; }
+    return GS_OK;
+}
+
+int gs_cc_close_window(gs_cc_t* h) {
+    GS_TRY(check(h));
+    DeviceGuard g(h->device);
+    return compress_impl(h);
+}
+
+int gs_cc_stats(gs_cc_t* h, uint64_t* nv, uint64_t* nc) {
+    GS_TRY(check(h));
+    DeviceGuard g(h->device);
+    return stats_impl(h, false, nv, nc, nullptr);
+}
+
+int gs_cc_checksum(gs_cc_t* h, uint64_t* sum, uint64_t* nv, uint64_t* nc) {
+    GS_TRY(check(h));
+    DeviceGuard g(h->device);
+    GS_TRY(compress_impl(h));
+    return stats_impl(h, true, nv, nc, sum);
+}
+
+int gs_cc_emit_dense(gs_cc_t* h, void* labels, uint64_t n) {
+    GS_TRY(check(h));
+    if (n && !labels) return fail(GS_ERR_INVALID, "gs_cc_emit_dense: null output");
+    DeviceGuard g(h->device);
+    GS_TRY(compress_impl(h));
+    const uint64_t m = n < h->cap ? n : h->cap;
+    const size_t esz = h->cfg.id_bits / 8;
+    if (h->cfg.id_bits == 32) {
+        GS_TRY(copy_out(h, labels, h->parent, m * 4));
+    } else if (is_device_pointer(labels)) {
+        hipLaunchKernelGGL(k_widen, dim3(grid_for(m, 256, 16384)), dim3(256), 0, h->stream, h->parent, (int64_t*)labels, m);
+        GS_HIP(hipGetLastError());
+    } else {
+        GS_TRY(ensure_buf(&h->tmp, &h->tmp_bytes, m * 8 + 8));
+        hipLaunchKernelGGL(k_widen, dim3(grid_for(m, 256, 16384)), dim3(256), 0, h->stream, h->parent, (int64_t*)h->tmp, m);
+        GS_HIP(hipGetLastError());
+        GS_TRY(copy_out(h, labels, h->tmp, m * 8));
+    }
+    if (n > m) {   // ids beyond the capacity are never in the summary: -1
+        char* tail = static_cast<char*>(labels) + m * esz;
+        if (is_device_pointer(labels)) GS_HIP(hipMemsetAsync(tail, 0xFF, (n - m) * esz, h->stream));
+        else { GS_TRY(sync_and_check(h)); std::memset(tail, 0xFF, (n - m) * esz); }
+    }
+    return sync_and_check(h);
+}
+
+int gs_cc_emit_pairs(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uint64_t* n_out) {
+    GS_TRY(check(h));
+    if (!n_out) return fail(GS_ERR_INVALID, "gs_cc_emit_pairs: null n_out");
+    if (cap && (!vertices || !labels)) return fail(GS_ERR_INVALID, "gs_cc_emit_pairs: null output");
+    DeviceGuard g(h->device);
+    GS_TRY(compress_impl(h));
+    const uint32_t ntiles = (uint32_t)((h->cap + kTile - 1) / kTile);
+    const size_t esz = h->cfg.id_bits / 8;
+    // layout of tmp: [tile counts u32 x ntiles][offsets u64 x ntiles+1][vertices][labels]
+    const size_t cnt_b = ((size_t)ntiles * 4 + 15) & ~(size_t)15;
+    const size_t off_b = ((size_t)(ntiles + 1) * 8 + 15) & ~(size_t)15;
+    GS_TRY(ensure_buf(&h->tmp, &h->tmp_bytes, cnt_b + off_b));
+    uint32_t* cnt = static_cast<uint32_t*>(h->tmp);
+    uint64_t* off = reinterpret_cast<uint64_t*>(static_cast<char*>(h->tmp) + cnt_b);
+    hipLaunchKernelGGL(k_tile_count, dim3(ntiles), dim3(kTileThreads), 0, h->stream, h->parent, h->cap, cnt);
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, h->stream, cnt, off, ntiles);
+    GS_HIP(hipGetLastError());
+    GS_HIP(hipMemcpyAsync(h->hscratch, off + ntiles, 8, hipMemcpyDeviceToHost, h->stream));
+    GS_TRY(sync_and_check(h));
+    const uint64_t total = h->hscratch[0];
+    *n_out = total;
+    const uint64_t w = total < cap ? total : cap;
+    if (w) {
+        const bool dev = is_device_pointer(vertices) && is_device_pointer(labels);
+        void* vo = vertices;
+        void* lo = labels;
+        if (!dev) {
+            GS_TRY(ensure_buf(&h->tmp, &h->tmp_bytes, cnt_b + off_b + 2 * w * esz));
+            cnt = static_cast<uint32_t*>(h->tmp);
+            off = reinterpret_cast<uint64_t*>(static_cast<char*>(h->tmp) + cnt_b);
+            // ensure_buf may have reallocated: recompute the offsets
+            hipLaunchKernelGGL(k_tile_count, dim3(ntiles), dim3(kTileThreads), 0, h->stream, h->parent, h->cap, cnt);
+            hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, h->stream, cnt, off, ntiles);
+            vo = static_cast<char*>(h->tmp) + cnt_b + off_b;
+            lo = static_cast<char*>(vo) + w * esz;
+        }
+        if (h->cfg.id_bits == 32)
+            hipLaunchKernelGGL(k_tile_scatter<uint32_t>, dim3(ntiles), dim3(kTileThreads), 0, h->stream, h->parent, h->cap, off,
+                               (uint32_t*)vo, (uint32_t*)lo, w);
+        else
+            hipLaunchKernelGGL(k_tile_scatter<int64_t>, dim3(ntiles), dim3(kTileThreads), 0, h->stream, h->parent, h->cap, off,
+                               (int64_t*)vo, (int64_t*)lo, w);
+        GS_HIP(hipGetLastError());
+        if (!dev) {
+            GS_HIP(hipMemcpyAsync(vertices, vo, w * esz, hipMemcpyDeviceToHost, h->stream));
+            GS_HIP(hipMemcpyAsync(labels, lo, w * esz, hipMemcpyDeviceToHost, h->stream));
+        }
+    }
+    GS_TRY(sync_and_check(h));
+    if (total > cap) return fail(GS_ERR_CAPACITY, "gs_cc_emit_pairs: %llu pairs, capacity %llu",
+                                 (unsigned long long)total, (unsigned long long)cap);
+    return GS_OK;
+}
+
+int gs_cc_find(gs_cc_t* h, const void* ids, void* roots, uint64_t n) {
+    GS_TRY(check(h));
+    if (n == 0) return GS_OK;
+    if (!ids || !roots) return fail(GS_ERR_INVALID, "gs_cc_find: null buffer");
+    DeviceGuard g(h->device);
+    const size_t esz = h->cfg.id_bits / 8;
+    const bool dev = is_device_pointer(ids) && is_device_pointer(roots);
+    const void* di = ids;
+    void* dr = roots;
+    if (!dev) {
+        GS_TRY(ensure_buf(&h->tmp, &h->tmp_bytes, 2 * n * esz));
+        di = h->tmp;
+        dr = static_cast<char*>(h->tmp) + n * esz;
+        GS_HIP(hipMemcpyAsync(const_cast<void*>(di), ids, n * esz, is_device_pointer(ids) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->stream));
+    }
+    const dim3 grid(grid_for(n, 256, 16384));
+    if (h->cfg.id_bits == 32)
+        hipLaunchKernelGGL(k_find<uint32_t>, grid, dim3(256), 0, h->stream, (const uint32_t*)di, (uint32_t*)dr, n, h->parent, h->cap);
+    else
+        hipLaunchKernelGGL(k_find<int64_t>, grid, dim3(256), 0, h->stream, (const int64_t*)di, (int64_t*)dr, n, h->parent, h->cap);
+    GS_HIP(hipGetLastError());
+    if (!dev) GS_TRY(copy_out(h, roots, dr, n * esz));
+    return sync_and_check(h);
+}
+
+int gs_cc_labels_device(gs_cc_t* h, const void** p) {
+    GS_TRY(check(h));
+    if (!p) return fail(GS_ERR_INVALID, "null out");
+    *p = h->parent;
+    return GS_OK;
+}
+
+int gs_cc_export_marks(gs_cc_t* h, void* pairs, uint64_t cap, uint64_t* n_out) {
+    GS_TRY(check(h));
+    if (!n_out) return fail(GS_ERR_INVALID, "gs_cc_export_marks: null n_out");
+    if (!h->mark) return fail(GS_ERR_UNSUPPORTED, "gs_cc_export_marks: handle created without GS_CC_TRACK_MARKS");
+    if (cap && !pairs) return fail(GS_ERR_INVALID, "gs_cc_export_marks: null output");
+    DeviceGuard g(h->device);
+    const bool dev = cap == 0 || is_device_pointer(pairs);
+    void* out = pairs;
+    if (!dev) {
+        GS_TRY(ensure_buf(&h->tmp, &h->tmp_bytes, cap * 8));
+        out = h->tmp;
+    }
+    GS_HIP(hipMemsetAsync(h->dscratch, 0, sizeof(unsigned long long), h->stream));
+    {
+        KTimer t(h, GS_K_EXPORT);
+        hipLaunchKernelGGL(k_export_marks, dim3(grid_for(h->cap, 256 * 16, 4096)), dim3(256), 0, h->stream,
+                           h->mark, h->parent, h->cap, (uint32_t*)out, cap, h->dscratch);
+    }
+    GS_HIP(hipGetLastError());
+    GS_HIP(hipMemcpyAsync(h->hscratch, h->dscratch, 8, hipMemcpyDeviceToHost, h->stream));
+    GS_TRY(sync_and_check(h));
+    const uint64_t total = h->hscratch[0];
+    *n_out = total < cap ? total : cap;
+    if (!dev && *n_out) {
+        GS_HIP(hipMemcpyAsync(pairs, out, *n_out * 8, hipMemcpyDeviceToHost, h->stream));
+        GS_TRY(sync_and_check(h));
+    }
+    if (total > cap) return fail(GS_ERR_CAPACITY, "gs_cc_export_marks: %llu marked, capacity %llu (rest kept)",
+                                 (unsigned long long)total, (unsigned long long)cap);
+    return GS_OK;
+}
+
+int gs_cc_timing(gs_cc_t* h, int enable) {
+    GS_TRY(check(h));
+    DeviceGuard g(h->device);
+    GS_TRY(resolve_timing(h));
+    h->timing = enable != 0;
+    for (int k = 0; k < GS_K_COUNT; ++k) { h->total_ms[k] = 0; h->launches[k] = 0; }
+    return GS_OK;
+}
+
+int gs_cc_kernel_time(gs_cc_t* h, int kernel, double* total_ms, uint64_t* launches) {
+    GS_TRY(check(h));
+    if (kernel < 0 || kernel >= GS_K_COUNT) return fail(GS_ERR_INVALID, "bad kernel id %d", kernel);
+    DeviceGuard g(h->device);
+    GS_TRY(resolve_timing(h));
+    if (total_ms) *total_ms = h->total_ms[kernel];
+    if (launches) *launches = h->launches[kernel];
+    return GS_OK;
+}
+
+}  // extern "C"

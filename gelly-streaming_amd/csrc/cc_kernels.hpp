@@ -1,0 +1,377 @@
+// cc_kernels.hpp — device code for streaming Connected Components on gfx950 (wave64).
+//
+// State: one dense uint32 parent[] per summary (HBM-resident, vertex_capacity words).
+//   parent[v] == kInvalid      v is not in the summary (DisjointSet.matches has no key v)
+//   parent[v] == v             v is a root
+//   parent[v] <  v             v hangs below parent[v]
+// Hooking always puts the LARGER root under the SMALLER one (atomicCAS on the larger root's
+// word), so parent[v] <= v holds for every seen v and every root is the minimum id of its tree:
+// after full compression parent[] *is* the canonical (min-id) label array the reference's
+// emissions canonicalise to. DisjointSet.java:92-118 decides by rank instead; its trees differ,
+// its components (and hence canonical labels) do not.
+//
+// Visibility: plain loads of parent[] may return a stale (older) word from this CU's L1. Every
+// older value of parent[x] is an ancestor of x (or x itself, or kInvalid), so a stale read can
+// only shorten a walk; every write that matters is an agent-scope atomicCAS, which sees the true
+// word and makes a failed hook retry from the true parent. Path-halving writes store an
+// ancestor into a non-root word, which is valid whatever order they land in.
+#pragma once
+
+#include "common.hpp"
+
+namespace gsgpu {
+
+// Root of x, given px = a parent[x] value already read (px != kInvalid). Walks with
+// intermediate pointer jumping (each visited word gets its grandparent) and stops at the first
+// word that is not strictly smaller than its index (a root, or a stale kInvalid read).
+__device__ __forceinline__ uint32_t find_root(uint32_t* __restrict__ parent, uint32_t x, uint32_t px) {
+    if (px == x) return x;
+    uint32_t prev = x, cur = px, next;
+    while (cur > (next = parent[cur])) {
+        parent[prev] = next;
+        prev = cur;
+        cur = next;
+    }
+    return cur;
+}
+
+// Read-only root walk (no writes) for find() on const state.
+__device__ __forceinline__ uint32_t find_root_ro(const uint32_t* __restrict__ parent, uint32_t x) {
+    uint32_t cur = x, next;
+    while (cur > (next = parent[cur])) cur = next;
+    return cur;
+}
+
+// First touch of v (makeSet, DisjointSet.java:53-56): kInvalid -> v. Returns v's parent word.
+__device__ __forceinline__ uint32_t make_set(uint32_t* __restrict__ parent, uint32_t v, uint32_t pv) {
+    if (pv != kInvalid) return pv;
+    const uint32_t old = atomicCAS(&parent[v], kInvalid, v);
+    return old == kInvalid ? v : old;
+}
+
+// union(u, v) given the parent words read by the caller. MARK: record hooked roots and
+// self-loop first touches in mark[] for the partial-summary export.
+template <bool MARK>
+__device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint8_t* __restrict__ mark,
+                                           uint32_t u, uint32_t v, uint32_t pu, uint32_t pv) {
+    if (u == v) {                                   // union(u,u): makeSet only
+        if (pu == kInvalid) {
+            const uint32_t old = atomicCAS(&parent[u], kInvalid, u);
+            if (MARK && old == kInvalid) mark[u] = 1;
+        }
+        return;
+    }
+    pu = make_set(parent, u, pu);
+    pv = make_set(parent, v, pv);
+    if (pu == pv) return;                           // common parent: already one component
+    uint32_t ru = find_root(parent, u, pu);
+    uint32_t rv = find_root(parent, v, pv);
+    while (ru != rv) {
+        const uint32_t hi = ru > rv ? ru : rv;
+        const uint32_t lo = ru > rv ? rv : ru;
+        const uint32_t old = atomicCAS(&parent[hi], hi, lo);
+        if (old == hi) {                            // hooked: hi is no longer a root
+            if (MARK) mark[hi] = 1;
+            return;
+        }
+        // hi was hooked meanwhile: continue from its true parent (old < hi, strictly
+        // decreasing, so the loop ends)
+        const uint32_t r = find_root(parent, old, parent[old]);
+        if (hi == ru) ru = r; else rv = r;
+    }
+}
+
+struct RangeCheck {
+    uint32_t cap;
+    uint32_t* err;
+};
+
+template <typename IdT>
+__device__ __forceinline__ bool id_ok(IdT x, uint32_t cap) {
+    return static_cast<uint64_t>(x) < static_cast<uint64_t>(cap) &&
+           !(sizeof(IdT) == 8 && static_cast<int64_t>(x) < 0);
+}
+
+constexpr int kFoldThreads = 256;
+constexpr int kEdgesPerThread = 4;
+
+// UpdateCC over a batch. Each thread takes 4 consecutive edges per pass: the 8 endpoint reads
+// are coalesced (nontemporal: the edge stream is read once and must not evict parent[] from
+// L2 / Infinity Cache), the 8 parent[] gathers are issued back to back before any dependent
+// step, then the 4 unions run.
+template <typename IdT, bool AOS, bool MARK>
+__global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a, const IdT* __restrict__ b,
+                                                       uint64_t n, uint32_t* __restrict__ parent,
+                                                       uint8_t* __restrict__ mark, RangeCheck rc) {
+    const uint64_t groups = (n + kEdgesPerThread - 1) / kEdgesPerThread;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += stride) {
+        const uint64_t e0 = g * kEdgesPerThread;
+        uint32_t u[kEdgesPerThread], v[kEdgesPerThread];
+        bool ok[kEdgesPerThread];
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < kEdgesPerThread; ++k) {
+            const uint64_t e = e0 + k;
+            IdT x = 0, y = 0;
+            if (e < n) {
+                if (AOS) {
+                    x = __builtin_nontemporal_load(&a[2 * e]);
+                    y = __builtin_nontemporal_load(&a[2 * e + 1]);
+                } else {
+                    x = __builtin_nontemporal_load(&a[e]);
+                    y = __builtin_nontemporal_load(&b[e]);
+                }
+            }
+            const bool in = e < n;
+            const bool good = in && id_ok<IdT>(x, rc.cap) && id_ok<IdT>(y, rc.cap);
+            bad |= in && !good;
+            ok[k] = good;
+            u[k] = good ? static_cast<uint32_t>(x) : 0u;
+            v[k] = good ? static_cast<uint32_t>(y) : 0u;
+        }
+        if (bad) atomicOr(rc.err, 1u);
+        uint32_t pu[kEdgesPerThread], pv[kEdgesPerThread];
+#pragma unroll
+        for (int k = 0; k < kEdgesPerThread; ++k) {
+            pu[k] = ok[k] ? parent[u[k]] : 0u;
+            pv[k] = ok[k] ? parent[v[k]] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kEdgesPerThread; ++k)
+            if (ok[k]) union_edge<MARK>(parent, mark, u[k], v[k], pu[k], pv[k]);
+    }
+}
+
+// DisjointSet.merge(other) with other given as a dense parent array: union(v, other[v]) for
+// every v in other (DisjointSet.java:127-131 iterates other.getMatches()).
+template <bool MARK>
+__global__ __launch_bounds__(256) void k_merge_dense(const uint32_t* __restrict__ other, uint32_t n_other,
+                                                     uint32_t* __restrict__ parent, uint8_t* __restrict__ mark) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n_other; v += stride) {
+        const uint32_t p = other[v];
+        if (p == kInvalid) continue;
+        union_edge<MARK>(parent, mark, v, p, parent[v], parent[p]);
+    }
+}
+
+// Merger emission: full compression. Afterwards parent[v] = root(v) = canonical label.
+__global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent, uint32_t n) {
+    const uint32_t stride = gridDim.x * blockDim.x * 4;
+    for (uint32_t base = (blockIdx.x * blockDim.x + threadIdx.x) * 4; base < n; base += stride) {
+        uint32_t p[4];
+        if (base + 4 <= n) {
+            const uint4 q = *reinterpret_cast<const uint4*>(parent + base);
+            p[0] = q.x; p[1] = q.y; p[2] = q.z; p[3] = q.w;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) p[k] = (base + k < n) ? parent[base + k] : kInvalid;
+        }
+        uint32_t gp[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t v = base + k;
+            gp[k] = (p[k] != kInvalid && p[k] != v) ? parent[p[k]] : p[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t v = base + k;
+            if (p[k] == kInvalid || p[k] == v || gp[k] == p[k]) continue;   // root / unseen / depth 1
+            parent[v] = find_root(parent, p[k], gp[k]);
+        }
+    }
+}
+
+// wave64 / block reductions
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+    return x;
+}
+
+// n_vertices, n_components (roots) and the emission checksum over a (compressed) parent array.
+template <bool CHECKSUM>
+__global__ __launch_bounds__(256) void k_stats(const uint32_t* __restrict__ parent, uint32_t n,
+                                               unsigned long long* __restrict__ out) {
+    unsigned long long seen = 0, roots = 0, h = 0;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += stride) {
+        const uint32_t p = parent[v];
+        if (p == kInvalid) continue;
+        ++seen;
+        roots += (p == v);
+        if (CHECKSUM) h += pair_mix(v, p);
+    }
+    __shared__ unsigned long long red[3][4];
+    seen = wave_sum(seen); roots = wave_sum(roots);
+    if (CHECKSUM) h = wave_sum(h);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) { red[0][wid] = seen; red[1][wid] = roots; red[2][wid] = h; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long s = 0, r = 0, c = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) { s += red[0][w]; r += red[1][w]; c += red[2][w]; }
+        atomicAdd(&out[0], s);
+        atomicAdd(&out[1], r);
+        if (CHECKSUM) atomicAdd(&out[2], c);
+    }
+}
+
+// DisjointSet.find for a batch of ids. Read-only walk (the label array is not modified).
+template <typename IdT>
+__global__ __launch_bounds__(256) void k_find(const IdT* __restrict__ ids, IdT* __restrict__ roots, uint64_t n,
+                                              const uint32_t* __restrict__ parent, uint32_t cap) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const IdT x = ids[i];
+        IdT r = static_cast<IdT>(-1);
+        if (id_ok<IdT>(x, cap)) {
+            const uint32_t p = parent[static_cast<uint32_t>(x)];
+            if (p != kInvalid) r = static_cast<IdT>(find_root_ro(parent, static_cast<uint32_t>(x)));
+        }
+        roots[i] = r;
+    }
+}
+
+// dense emission for 64-bit ids: labels[v] = parent[v] or -1
+__global__ __launch_bounds__(256) void k_widen(const uint32_t* __restrict__ parent, int64_t* __restrict__ out, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += stride) {
+        const uint32_t p = parent[v];
+        out[v] = p == kInvalid ? -1 : static_cast<int64_t>(p);
+    }
+}
+
+// ---- ordered compaction of (vertex, label) for emit_pairs: tile = 256 threads x 16 vertices
+constexpr int kTileThreads = 256;
+constexpr int kTilePerThread = 16;
+constexpr uint32_t kTile = kTileThreads * kTilePerThread;
+
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t* total) {
+    __shared__ uint32_t wsum[kTileThreads / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t incl = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kTileThreads / 64; ++w) {
+        if (w < wid) wbase += wsum[w];
+        tot += wsum[w];
+    }
+    __syncthreads();
+    *total = tot;
+    return wbase + incl - x;
+}
+
+__global__ __launch_bounds__(kTileThreads) void k_tile_count(const uint32_t* __restrict__ parent, uint32_t n,
+                                                             uint32_t* __restrict__ tile_count) {
+    const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kTilePerThread;
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kTilePerThread; ++k) {
+        const uint64_t v = base + k;
+        c += (v < n && parent[v] != kInvalid);
+    }
+    uint32_t tot;
+    (void)block_exclusive_scan(c, &tot);
+    if (threadIdx.x == 0) tile_count[blockIdx.x] = tot;
+}
+
+// exclusive scan of tile counts in one block (in place); offsets are uint64
+__global__ __launch_bounds__(1024) void k_tile_scan(const uint32_t* __restrict__ cnt, uint64_t* __restrict__ off,
+                                                    uint32_t ntiles) {
+    __shared__ unsigned long long part[1024];
+    const uint32_t per = (ntiles + blockDim.x - 1) / blockDim.x;
+    const uint32_t lo = threadIdx.x * per, hi = min(lo + per, ntiles);
+    unsigned long long s = 0;
+    for (uint32_t i = lo; i < hi; ++i) s += cnt[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long run = 0;
+        for (uint32_t t = 0; t < blockDim.x; ++t) { const unsigned long long x = part[t]; part[t] = run; run += x; }
+        off[ntiles] = run;
+    }
+    __syncthreads();
+    unsigned long long run = part[threadIdx.x];
+    for (uint32_t i = lo; i < hi; ++i) { off[i] = run; run += cnt[i]; }
+}
+
+template <typename IdT>
+__global__ __launch_bounds__(kTileThreads) void k_tile_scatter(const uint32_t* __restrict__ parent, uint32_t n,
+                                                               const uint64_t* __restrict__ off, IdT* __restrict__ vout,
+                                                               IdT* __restrict__ lout, uint64_t cap) {
+    const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kTilePerThread;
+    uint32_t p[kTilePerThread];
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kTilePerThread; ++k) {
+        const uint64_t v = base + k;
+        p[k] = (v < n) ? parent[v] : kInvalid;
+        c += (p[k] != kInvalid);
+    }
+    uint32_t tot;
+    uint64_t pos = off[blockIdx.x] + block_exclusive_scan(c, &tot);
+#pragma unroll
+    for (int k = 0; k < kTilePerThread; ++k) {
+        if (p[k] == kInvalid) continue;
+        if (pos < cap) { vout[pos] = static_cast<IdT>(base + k); lout[pos] = static_cast<IdT>(p[k]); }
+        ++pos;
+    }
+}
+
+// Partial-summary export: (v, parent[v]) for every marked v, mark cleared. Unordered append
+// with one atomic per wave (ballot + mbcnt).
+__global__ __launch_bounds__(256) void k_export_marks(uint8_t* __restrict__ mark, const uint32_t* __restrict__ parent,
+                                                      uint32_t n, uint32_t* __restrict__ pairs, uint64_t cap,
+                                                      unsigned long long* __restrict__ counter) {
+    const uint32_t stride = gridDim.x * blockDim.x * 16;
+    const int lane = threadIdx.x & 63;
+    for (uint32_t base0 = blockIdx.x * blockDim.x * 16; base0 < n; base0 += stride) {
+        const uint32_t base = base0 + threadIdx.x * 16;
+        uint8_t m[16];
+        if (base + 16 <= n) {
+            const uint4 q = *reinterpret_cast<const uint4*>(mark + base);
+            *reinterpret_cast<uint4*>(m) = q;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) m[k] = (base + k < n) ? mark[base + k] : 0;
+        }
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) cnt += (m[k] != 0);
+        // wave-aggregated reservation
+        unsigned long long incl = cnt;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const unsigned long long y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        const unsigned long long wtot = __shfl(incl, 63, 64);
+        unsigned long long wbase = 0;
+        if (lane == 0 && wtot) wbase = atomicAdd(counter, wtot);
+        wbase = __shfl(wbase, 0, 64);
+        if (cnt == 0) continue;
+        unsigned long long pos = wbase + incl - cnt;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (!m[k]) continue;
+            const uint32_t v = base + k;
+            if (pos < cap) {                      // overflowing marks stay for the next export
+                pairs[2 * pos] = v;
+                pairs[2 * pos + 1] = parent[v];
+                mark[v] = 0;
+            }
+            ++pos;
+        }
+    }
+}
+
+}  // namespace gsgpu

@@ -1,0 +1,156 @@
+"""Host-side mirror of the reference's streaming operator surface for Connected Components.
+
+Reference (paths relative to src/main/java/org/apache/flink/graph/streaming/):
+
+* ``SimpleEdgeStream.aggregate(summaryAggregation)`` -> ``summaryAggregation.run(edges)``
+  (SimpleEdgeStream.java:100-102, GraphStream.java:139-140)
+* ``SummaryBulkAggregation(updateFun, combineFun, initialVal, timeMillis, transientState)``
+  (SummaryBulkAggregation.java:57-64) and its dataflow ``run`` (:68-90): per-partition
+  tumbling-window fold from a fresh initial value, ``timeWindowAll`` reduce with the combine
+  function, then the parallelism-1 ``Merger`` (SummaryAggregation.java:106-119) that folds each
+  window result into the cumulative summary and emits it.
+* ``ConnectedComponents(long mergeWindowTime)`` (library/ConnectedComponents.java:52-54).
+
+Windows: the reference's are wall-clock / event-time tumbling windows. Here a stream carries
+either event timestamps (window = floor(ts / mergeWindowTime), Flink's tumbling window
+assignment with offset 0) or none, in which case ``window_edges`` cuts count-based windows
+(SURVEY.md §7 "Hard parts"). Partition p of a window is its contiguous slice
+[p*len/P, (p+1)*len/P), as in oracle/pipeline.c.
+
+Modes:
+* ``mode="fused"`` (default, the production path on one GPU): every window's edges, whatever
+  partition they belong to, are folded straight into the one cumulative device summary and the
+  window is closed (compressed) before its emission. The emitted canonical labels equal the
+  reference's, which do not depend on partitioning, merge order or rank tie-breaks (union-find
+  over the union of all edges so far).
+* ``mode="reference"``: the reference dataflow step by step on the device — one fresh partial
+  summary per partition per window, ``CombineCC`` in partition order, then the Merger's
+  ``CombineCC(windowResult, summary)``. Used by the parity tests of ``CombineCC``.
+"""
+from __future__ import annotations
+
+from typing import Iterator, List, Optional, Sequence
+
+import numpy as np
+
+from .summary import CombineCC, DisjointSet, UpdateCC
+
+
+class SimpleEdgeStream:
+    """An edge stream in arrival order: src[i] -> dst[i], optional event timestamps (ms)."""
+
+    def __init__(self, src, dst, timestamps: Optional[Sequence[int]] = None):
+        self.src = np.ascontiguousarray(np.asarray(src, dtype=np.int64))
+        self.dst = np.ascontiguousarray(np.asarray(dst, dtype=np.int64))
+        if self.src.shape != self.dst.shape:
+            raise ValueError("src/dst length mismatch")
+        self.timestamps = None if timestamps is None else np.asarray(timestamps, dtype=np.int64)
+        if self.timestamps is not None and self.timestamps.shape != self.src.shape:
+            raise ValueError("timestamps length mismatch")
+
+    def __len__(self) -> int:
+        return int(self.src.size)
+
+    def aggregate(self, summary_aggregation: "SummaryBulkAggregation") -> Iterator[DisjointSet]:
+        """GraphStream.aggregate (GraphStream.java:139-140)."""
+        return summary_aggregation.run(self)
+
+    def windows(self, time_millis: int, window_edges: Optional[int]) -> List[slice]:
+        n = len(self)
+        if n == 0:
+            return []
+        if self.timestamps is not None and not window_edges:
+            if np.any(np.diff(self.timestamps) < 0):
+                raise ValueError("timestamps must be ascending (AscendingTimestampExtractor)")
+            wid = self.timestamps // int(time_millis)
+            cuts = np.nonzero(np.diff(wid))[0] + 1
+            bounds = [0] + cuts.tolist() + [n]
+            return [slice(a, b) for a, b in zip(bounds[:-1], bounds[1:])]
+        w = int(window_edges) if window_edges else n
+        return [slice(a, min(a + w, n)) for a in range(0, n, w)]
+
+
+class SummaryBulkAggregation:
+    """Partitioned fold -> windowAll combine -> Merger (SummaryBulkAggregation.java:68-90)."""
+
+    def __init__(self, update_fun: UpdateCC, combine_fun: CombineCC, time_millis: int,
+                 transient_state: bool, *, vertex_capacity: Optional[int] = None, id_bits: int = 64,
+                 device: int = 0, parallelism: int = 1, window_edges: Optional[int] = None,
+                 mode: str = "fused"):
+        if mode not in ("fused", "reference"):
+            raise ValueError("mode must be 'fused' or 'reference'")
+        self.update_fun = update_fun
+        self.combine_fun = combine_fun
+        self.time_millis = int(time_millis)
+        self.transient_state = bool(transient_state)
+        self.vertex_capacity = vertex_capacity
+        self.id_bits = id_bits
+        self.device = device
+        self.parallelism = max(int(parallelism), 1)
+        self.window_edges = window_edges
+        self.mode = mode
+
+    def _capacity(self, stream: SimpleEdgeStream) -> int:
+        if self.vertex_capacity:
+            return int(self.vertex_capacity)
+        if len(stream) == 0:
+            return 1
+        return int(max(stream.src.max(), stream.dst.max())) + 1
+
+    def _new(self, cap: int) -> DisjointSet:
+        return DisjointSet(cap, id_bits=self.id_bits, device=self.device)
+
+    def run(self, stream: SimpleEdgeStream) -> Iterator[DisjointSet]:
+        cap = self._capacity(stream)
+        wins = stream.windows(self.time_millis, self.window_edges)
+        if self.mode == "fused":
+            yield from self._run_fused(stream, wins, cap)
+        else:
+            yield from self._run_reference(stream, wins, cap)
+
+    def _run_fused(self, stream, wins, cap) -> Iterator[DisjointSet]:
+        summary = self._new(cap)
+        try:
+            for w in wins:
+                if self.transient_state:
+                    summary.reset()
+                self.update_fun.fold_batch(summary, stream.src[w], stream.dst[w])
+                summary.close_window()
+                yield summary                      # Merger: collector.collect(summary)
+        finally:
+            summary.close()
+
+    def _run_reference(self, stream, wins, cap) -> Iterator[DisjointSet]:
+        P = self.parallelism
+        pool = [self._new(cap) for _ in range(P + 1)]
+        summary: Optional[DisjointSet] = None     # Merger.summary = initialVal (empty)
+        try:
+            for w in wins:
+                lo, ln = w.start, w.stop - w.start
+                free = [d for d in pool if d is not summary]
+                acc: Optional[DisjointSet] = None
+                for p in range(P):
+                    a, b = lo + (ln * p) // P, lo + (ln * (p + 1)) // P
+                    if a == b:
+                        continue                   # no element -> no window result
+                    part = free.pop()
+                    part.reset()                   # fresh copy of the initial value
+                    self.update_fun.fold_batch(part, stream.src[a:b], stream.dst[a:b])
+                    acc = part if acc is None else self.combine_fun.reduce(acc, part)
+                if summary is None or self.transient_state:
+                    summary = acc                  # reduce(s, empty) returns s
+                else:
+                    summary = self.combine_fun.reduce(acc, summary)
+                summary.close_window()
+                yield summary
+        finally:
+            for d in pool:
+                d.close()
+
+
+class ConnectedComponents(SummaryBulkAggregation):
+    """ConnectedComponents(long mergeWindowTime) (library/ConnectedComponents.java:52-54):
+    UpdateCC, CombineCC, a new DisjointSet as initial value, transientState = false."""
+
+    def __init__(self, mergeWindowTime: int, **kw):
+        super().__init__(UpdateCC(), CombineCC(), mergeWindowTime, False, **kw)

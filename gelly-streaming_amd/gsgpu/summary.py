@@ -1,0 +1,258 @@
+"""Device-backed ``DisjointSet`` summary and the ``UpdateCC`` / ``CombineCC`` functions.
+
+Mirrors the reference's hot-path types (paths relative to the reference's
+src/main/java/org/apache/flink/graph/streaming/):
+
+* ``DisjointSet``   — summaries/DisjointSet.java:25-150. One libgsgpu handle = one summary,
+  held as a dense uint32 parent array in HBM. ``union`` / ``find`` / ``merge`` / ``getMatches``
+  / ``toString`` keep the Java names and meaning; ``find`` returns ``None`` for unknown ids like
+  the Java method (:67-69). ``getMatches`` returns the canonical vertex -> root map (the roots
+  here are always the component minima, see csrc/cc_kernels.hpp).
+* ``UpdateCC``      — library/ConnectedComponents.java:83-85 (EdgesFold: ``ds.union(u, v)``),
+  with a batched form ``fold_batch`` that is what the streaming operator calls.
+* ``CombineCC``     — library/ConnectedComponents.java:116-125 (merge the smaller summary into
+  the larger, return the larger).
+
+Buffers: numpy arrays (host) or torch tensors (host or device) of the handle's id width.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from . import _abi
+from ._abi import GsCcConfig, call
+
+U64 = ctypes.c_uint64
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+def _buf(x, id_bits: int, name: str):
+    """(pointer, keepalive, length) for a 1-D id buffer of the handle's width."""
+    if _is_torch(x):
+        import torch
+        want = torch.int32 if id_bits == 32 else torch.int64
+        if x.dtype not in ((torch.int32, torch.uint32) if id_bits == 32 else (torch.int64,)):
+            raise TypeError("%s: torch dtype %s, expected %s" % (name, x.dtype, want))
+        if not x.is_contiguous():
+            raise ValueError("%s: tensor must be contiguous" % name)
+        return ctypes.c_void_p(x.data_ptr()), x, x.numel()
+    a = np.asarray(x)
+    if id_bits == 32:
+        if a.dtype not in (np.int32, np.uint32):
+            a = a.astype(np.int64)
+            if a.size and (a.min() < 0 or a.max() > 0xFFFFFFFE):
+                raise ValueError("%s: ids do not fit 32 bits" % name)
+            a = a.astype(np.uint32)
+    else:
+        a = a.astype(np.int64, copy=False)
+    a = np.ascontiguousarray(a)
+    return a.ctypes.data_as(ctypes.c_void_p), a, a.size
+
+
+def _stream_ptr(stream) -> Optional[int]:
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return int(stream.cuda_stream)        # torch.cuda.Stream
+
+
+class DisjointSet:
+    """GPU union-find summary (DisjointSet<K>), K = int32 or int64 vertex ids in [0, capacity)."""
+
+    def __init__(self, vertex_capacity: int, id_bits: int = 64, device: int = 0,
+                 track_marks: bool = False, stream=None, staging_edges: int = 0):
+        self.id_bits = int(id_bits)
+        self.capacity = int(vertex_capacity)
+        self.device = int(device)
+        cfg = GsCcConfig(ctypes.sizeof(GsCcConfig), self.id_bits, self.capacity, self.device,
+                         _abi.GS_CC_TRACK_MARKS if track_marks else 0, int(staging_edges))
+        h = ctypes.c_void_p()
+        call("gs_cc_create", ctypes.byref(h), ctypes.byref(cfg))
+        self._h = h
+        self.track_marks = bool(track_marks)
+        if stream is not None:
+            self.set_stream(stream)
+
+    # ---- lifetime ----
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        if self._h is None:
+            raise RuntimeError("DisjointSet is closed")
+        return self._h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None:
+            _abi.lib().gs_cc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - GC timing
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self) -> None:
+        """Back to ``new DisjointSet<K>()`` (the fold's initial value)."""
+        call("gs_cc_reset", self.handle)
+
+    def set_stream(self, stream) -> None:
+        call("gs_cc_set_stream", self.handle, _stream_ptr(stream))
+
+    def sync(self) -> None:
+        call("gs_cc_sync", self.handle)
+
+    # ---- DisjointSet.java API ----
+    def makeSet(self, e: int) -> None:
+        """makeSet (:53-56) for an id not yet in the summary (= union(e, e))."""
+        self.union(e, e)
+
+    def union(self, e1: int, e2: int) -> None:
+        """union (:92-118) of one pair."""
+        self.fold(np.array([e1]), np.array([e2]))
+
+    def find(self, e: int) -> Optional[int]:
+        """find (:66-80): root of e, or None if e is not in the summary."""
+        r = self.find_batch(np.array([e]))
+        return None if int(r[0]) < 0 else int(r[0])
+
+    def find_batch(self, ids) -> np.ndarray:
+        p, keep, n = _buf(ids, self.id_bits, "ids")
+        out = np.empty(n, dtype=np.uint32 if self.id_bits == 32 else np.int64)
+        call("gs_cc_find", self.handle, p, out.ctypes.data_as(ctypes.c_void_p), n)
+        return out.view(np.int32).astype(np.int64) if self.id_bits == 32 else out
+
+    def merge(self, other: "DisjointSet") -> None:
+        """merge (:127-131): union every (key, parent) of ``other`` into this summary."""
+        call("gs_cc_merge", self.handle, other.handle)
+
+    def getMatches(self) -> Dict[int, int]:
+        v, l = self.pairs()
+        return dict(zip(v.tolist(), l.tolist()))
+
+    def size(self) -> int:
+        """getMatches().size(): number of vertices in the summary."""
+        return self.stats()[0]
+
+    __len__ = size
+
+    def toString(self) -> str:
+        """``{root=[members...], ...}`` like DisjointSet.toString (:133-150); roots ascending,
+        members ascending (the Java HashMap order is unspecified)."""
+        v, l = self.pairs()
+        comps: Dict[int, List[int]] = {}
+        for a, b in zip(v.tolist(), l.tolist()):
+            comps.setdefault(b, []).append(a)
+        return "{" + ", ".join("%d=[%s]" % (r, ", ".join(map(str, m))) for r, m in sorted(comps.items())) + "}"
+
+    __str__ = toString
+
+    # ---- batched / streaming API ----
+    def fold(self, src, dst) -> None:
+        """UpdateCC over a batch: union(src[i], dst[i]) for every i."""
+        ps, ks, n = _buf(src, self.id_bits, "src")
+        pd, kd, m = _buf(dst, self.id_bits, "dst")
+        if n != m:
+            raise ValueError("src and dst lengths differ (%d, %d)" % (n, m))
+        call("gs_cc_fold", self.handle, ps, pd, n)
+
+    def fold_pairs(self, pairs, n: Optional[int] = None, id_bits: Optional[int] = None) -> None:
+        """union over interleaved (u, v) pairs; id_bits=32 folds exported partial summaries."""
+        bits = self.id_bits if id_bits is None else id_bits
+        p, keep, total = _buf(pairs, bits, "pairs")
+        cnt = total // 2 if n is None else int(n)
+        if cnt * 2 > total:
+            raise ValueError("pairs buffer holds %d pairs, %d requested" % (total // 2, cnt))
+        call("gs_cc_fold_pairs32" if bits == 32 else "gs_cc_fold_pairs", self.handle, p, cnt)
+
+    def close_window(self) -> None:
+        """Merger step: compress so every label is the canonical (min-id) root."""
+        call("gs_cc_close_window", self.handle)
+
+    def stats(self) -> Tuple[int, int]:
+        nv, nc = U64(), U64()
+        call("gs_cc_stats", self.handle, ctypes.byref(nv), ctypes.byref(nc))
+        return int(nv.value), int(nc.value)
+
+    def num_components(self) -> int:
+        return self.stats()[1]
+
+    def checksum(self) -> Tuple[int, int, int]:
+        s, nv, nc = U64(), U64(), U64()
+        call("gs_cc_checksum", self.handle, ctypes.byref(s), ctypes.byref(nv), ctypes.byref(nc))
+        return int(s.value), int(nv.value), int(nc.value)
+
+    def dense(self, n: Optional[int] = None, out=None):
+        """labels[v] for v < n (default capacity): canonical label or -1."""
+        n = self.capacity if n is None else int(n)
+        if out is None:
+            out = np.empty(n, dtype=np.int32 if self.id_bits == 32 else np.int64)
+        p, keep, m = _buf(out, self.id_bits, "labels")
+        call("gs_cc_emit_dense", self.handle, p, m)
+        return out
+
+    def pairs(self) -> Tuple[np.ndarray, np.ndarray]:
+        """(vertices, labels) of every vertex in the summary, sorted by vertex."""
+        cnt = U64()
+        nv = self.stats()[0]
+        dt = np.int32 if self.id_bits == 32 else np.int64
+        v = np.empty(max(nv, 1), dtype=dt)
+        l = np.empty(max(nv, 1), dtype=dt)
+        call("gs_cc_emit_pairs", self.handle, v.ctypes.data_as(ctypes.c_void_p),
+             l.ctypes.data_as(ctypes.c_void_p), nv, ctypes.byref(cnt))
+        return v[:cnt.value].astype(np.int64), l[:cnt.value].astype(np.int64)
+
+    def labels_device_ptr(self) -> int:
+        p = ctypes.c_void_p()
+        call("gs_cc_labels_device", self.handle, ctypes.byref(p))
+        return int(p.value or 0)
+
+    def export_marks(self, out, cap_pairs: Optional[int] = None) -> int:
+        """Write this window's partial-summary pairs (uint32 interleaved) into ``out``;
+        returns the number of pairs written."""
+        p, keep, total = _buf(out, 32, "out")
+        cap = total // 2 if cap_pairs is None else int(cap_pairs)
+        n = U64()
+        call("gs_cc_export_marks", self.handle, p, cap, ctypes.byref(n))
+        return int(n.value)
+
+    # ---- instrumentation ----
+    def timing(self, enable: bool) -> None:
+        call("gs_cc_timing", self.handle, 1 if enable else 0)
+
+    def kernel_time(self, kernel: int) -> Tuple[float, int]:
+        ms, n = ctypes.c_double(), U64()
+        call("gs_cc_kernel_time", self.handle, int(kernel), ctypes.byref(ms), ctypes.byref(n))
+        return float(ms.value), int(n.value)
+
+
+def combine_cc(s1: DisjointSet, s2: DisjointSet) -> DisjointSet:
+    """CombineCC.reduce (ConnectedComponents.java:116-125) on two device summaries."""
+    out = ctypes.c_void_p()
+    call("gs_cc_combine", s1.handle, s2.handle, ctypes.byref(out))
+    return s1 if out.value == s1.handle.value else s2
+
+
+class UpdateCC:
+    """EdgesFold<K, NullValue, DisjointSet<K>> (ConnectedComponents.java:70-86)."""
+
+    def foldEdges(self, ds: DisjointSet, vertex: int, vertex2: int, edgeValue=None) -> DisjointSet:
+        ds.union(vertex, vertex2)
+        return ds
+
+    def fold_batch(self, ds: DisjointSet, src, dst) -> DisjointSet:
+        ds.fold(src, dst)
+        return ds
+
+
+class CombineCC:
+    """ReduceFunction<DisjointSet<K>> (ConnectedComponents.java:95-126)."""
+
+    def reduce(self, s1: DisjointSet, s2: DisjointSet) -> DisjointSet:
+        return combine_cc(s1, s2)

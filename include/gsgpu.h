@@ -1,0 +1,142 @@
+/*
+ * gsgpu.h — C ABI of libgsgpu.so: MI355X (gfx950) streaming Connected Components for the
+ * Gelly Streaming `ConnectedComponents` SummaryBulkAggregation hot path.
+ *
+ * Reference interfaces replaced (paths relative to the reference's
+ * src/main/java/org/apache/flink/graph/streaming/):
+ *
+ *   gs_cc_create / gs_cc_reset   new DisjointSet<K>() as the fold's initial value
+ *                                (library/ConnectedComponents.java:52-54, summaries/DisjointSet.java:31-34)
+ *   gs_cc_fold / gs_cc_fold_pairs  EdgesFold.foldEdges -> UpdateCC: ds.union(u, v) per edge
+ *                                (EdgesFold.java:47, library/ConnectedComponents.java:83-85,
+ *                                 summaries/DisjointSet.java:92-118, SummaryBulkAggregation.java:121-123)
+ *   gs_cc_merge                  DisjointSet.merge(other)  (summaries/DisjointSet.java:127-131)
+ *   gs_cc_combine                CombineCC.reduce(s1, s2): merge the smaller summary into the larger
+ *                                (library/ConnectedComponents.java:116-125)
+ *   gs_cc_close_window           the Merger step that emits the cumulative summary per window
+ *                                (SummaryAggregation.java:106-119; transientState=false)
+ *   gs_cc_find                   DisjointSet.find (summaries/DisjointSet.java:66-80; -1 = null)
+ *   gs_cc_stats                  getMatches().size() and the number of components
+ *                                (summaries/DisjointSet.java:44-46)
+ *   gs_cc_emit_dense / _pairs    the emitted summary as canonical (vertex, min-id) labels:
+ *                                what getMatches()+find() give FlattenSet
+ *                                (example/ConnectedComponentsExample.java:143-156) and toString
+ *                                groups by (summaries/DisjointSet.java:133-150), canonicalised
+ *   gs_cc_export_marks           the partial summary that crosses the windowAll / tree exchange
+ *                                (SummaryBulkAggregation.java:81, SummaryTreeReduce.java:95-123)
+ *
+ * Conventions: every function returns 0 (GS_OK) or a negative GS_ERR_* code; the message of the
+ * last failure on the calling thread is gs_last_error(). No C++ exception crosses the ABI.
+ * Buffers passed in may be host (pageable or pinned) or device pointers; the caller keeps
+ * ownership of them, the library owns all device state of a handle. One handle per subtask
+ * thread; calls on one handle must be serialised by the caller; different handles may be used
+ * concurrently. All work of a handle is ordered on its HIP stream (gs_cc_set_stream).
+ */
+#ifndef GSGPU_H
+#define GSGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSGPU_VERSION 1
+
+enum {
+    GS_OK = 0,
+    GS_ERR_INVALID = -1,      /* bad argument                                           */
+    GS_ERR_HIP = -2,          /* HIP runtime failure                                    */
+    GS_ERR_RANGE = -3,        /* a vertex id outside [0, vertex_capacity)               */
+    GS_ERR_NOMEM = -4,        /* device allocation failed                               */
+    GS_ERR_STATE = -5,        /* call not valid in the handle's current state           */
+    GS_ERR_UNSUPPORTED = -6,  /* feature not built / not enabled on this handle         */
+    GS_ERR_CAPACITY = -7      /* output buffer too small                                */
+};
+
+/* gs_cc_config.flags */
+enum {
+    GS_CC_TRACK_MARKS = 1u << 0  /* keep per-vertex marks of this window's hooks, needed by
+                                    gs_cc_export_marks (multi-GPU / multi-handle merge)    */
+};
+
+typedef struct gs_cc gs_cc_t;
+
+typedef struct gs_cc_config {
+    uint32_t struct_size;       /* sizeof(gs_cc_config)                                    */
+    uint32_t id_bits;           /* 32 (int/uint32 ids) or 64 (long ids, the reference's K=Long) */
+    uint64_t vertex_capacity;   /* ids must lie in [0, vertex_capacity); <= 2^32 - 1       */
+    int32_t  device;            /* HIP device ordinal                                      */
+    uint32_t flags;             /* GS_CC_*                                                 */
+    uint64_t staging_edges;     /* staging size for host-pointer folds (0 = 2^22)          */
+} gs_cc_config;
+
+/* ---- lifetime ---- */
+int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg);
+int gs_cc_destroy(gs_cc_t* h);
+int gs_cc_reset(gs_cc_t* h);                        /* back to an empty DisjointSet          */
+int gs_cc_set_stream(gs_cc_t* h, void* hip_stream); /* NULL = the handle's own stream        */
+int gs_cc_get_stream(gs_cc_t* h, void** hip_stream);
+int gs_cc_sync(gs_cc_t* h);                         /* wait for the handle's stream; reports
+                                                       deferred device errors (GS_ERR_RANGE) */
+
+/* ---- UpdateCC / DisjointSet.union over a batch ----
+ * src/dst: n ids each (id_bits wide). pairs: n interleaved (src, dst) ids. Duplicates and
+ * self-loops are allowed: union(u,u) makes u a singleton (DisjointSet.java:94-105). */
+int gs_cc_fold(gs_cc_t* h, const void* src, const void* dst, uint64_t n);
+int gs_cc_fold_pairs(gs_cc_t* h, const void* pairs, uint64_t n);
+
+/* ---- DisjointSet.merge / CombineCC ---- (both handles on one device) */
+int gs_cc_merge(gs_cc_t* into, gs_cc_t* from);
+/* CombineCC.reduce(s1, s2): if |s1| <= |s2| then s2.merge(s1), *result = s2; else s1.merge(s2),
+ * *result = s1 (sizes = getMatches().size()). */
+int gs_cc_combine(gs_cc_t* s1, gs_cc_t* s2, gs_cc_t** result);
+
+/* ---- Merger / emission ----
+ * close_window fully compresses the summary: afterwards every seen vertex's label is the
+ * minimum vertex id of its component, resident on the device (gs_cc_labels_device). */
+int gs_cc_close_window(gs_cc_t* h);
+int gs_cc_stats(gs_cc_t* h, uint64_t* n_vertices, uint64_t* n_components);
+/* labels[v] for v < n: canonical label of v, or -1 if v is not in the summary.
+ * Output element width = id_bits. Implies close_window. */
+int gs_cc_emit_dense(gs_cc_t* h, void* labels, uint64_t n);
+/* (vertex, label) pairs of every vertex in the summary, sorted by vertex.
+ * Writes min(cap, |V|) pairs, *n_out = |V|; GS_ERR_CAPACITY if cap < |V|. Implies close_window. */
+int gs_cc_emit_pairs(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uint64_t* n_out);
+/* Order-independent checksum of the canonical emission (definition shared with oracle/:
+ * sum over seen v of splitmix64(v ^ splitmix64(label ^ 0xD1B54A32D192ED03))). Implies close_window. */
+int gs_cc_checksum(gs_cc_t* h, uint64_t* checksum, uint64_t* n_vertices, uint64_t* n_components);
+/* DisjointSet.find for n ids: roots[i] = current root of ids[i], -1 if unknown (null).
+ * The root is the canonical label (roots are always component minima). */
+int gs_cc_find(gs_cc_t* h, const void* ids, void* roots, uint64_t n);
+/* device pointer to the uint32 label/parent array (length vertex_capacity, 0xFFFFFFFF = unseen). */
+int gs_cc_labels_device(gs_cc_t* h, const void** dev_ptr);
+
+/* ---- partial-summary exchange (windowAll / tree merge) ----
+ * Requires GS_CC_TRACK_MARKS. Writes the (vertex, parent) pairs (uint32, interleaved) of every
+ * vertex whose root status changed in this handle since the last export / close_window, and
+ * clears those marks. Folding these pairs into another summary (gs_cc_fold_pairs, 32-bit ids
+ * regardless of id_bits via gs_cc_fold_pairs32) transfers all connectivity this handle gained. */
+int gs_cc_export_marks(gs_cc_t* h, void* pairs, uint64_t cap, uint64_t* n_out);
+int gs_cc_fold_pairs32(gs_cc_t* h, const void* pairs, uint64_t n);
+
+/* ---- instrumentation ----
+ * kernel ids: 0 fold, 1 compress (close_window), 2 merge, 3 export. */
+enum { GS_K_FOLD = 0, GS_K_COMPRESS = 1, GS_K_MERGE = 2, GS_K_EXPORT = 3, GS_K_COUNT = 4 };
+int gs_cc_timing(gs_cc_t* h, int enable);
+int gs_cc_kernel_time(gs_cc_t* h, int kernel, double* total_ms, uint64_t* launches);
+
+/* ---- synthetic streams on the device (definition: oracle/gen.c header) ----
+ * Write ids [first, first+n) of the stream into src/dst (device pointers, id_bits wide). */
+int gs_gen_rmat(void* src, void* dst, uint32_t id_bits, uint64_t first, uint64_t n, int scale,
+                uint64_t seed, uint32_t ta, uint32_t tb, uint32_t tc, int scramble, void* hip_stream);
+int gs_gen_er(void* src, void* dst, uint32_t id_bits, uint64_t first, uint64_t n, uint64_t nv,
+              uint64_t seed, void* hip_stream);
+
+const char* gs_last_error(void);
+int gs_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSGPU_H */

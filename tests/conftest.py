@@ -1,0 +1,28 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "gelly-streaming_amd"), os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD Instinct MI355X (HIP device); run with -m gpu")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _oracle_built():
+    lib = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+    if not os.path.exists(lib):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle")], stdout=subprocess.DEVNULL)
+    yield
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from pyoracle import coracle
+    return coracle()

@@ -1,0 +1,346 @@
+"""GPU parity: the HIP path (libgsgpu.so via its C ABI) against the oracle and golden fixtures.
+
+Bar: bit-exact canonical (min-id) labels for every window emission (integer path, no tolerance).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import gsgpu
+from gsgpu import DisjointSet, SimpleEdgeStream, ConnectedComponents, GsError, combine_cc
+from gsgpu import _abi
+from pyoracle import EMIT_CHECKSUM, EMIT_DENSE, dense_checksum
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _kats():
+    with open(os.path.join(GOLD, "reference_kats.json")) as f:
+        return json.load(f)
+
+
+def _streams():
+    with open(os.path.join(GOLD, "streams_index.json")) as f:
+        idx = json.load(f)
+    z = np.load(os.path.join(GOLD, "streams.npz"))
+    return [dict(c, **{k: z["%s__%s" % (c["name"], k)] for k in ("src", "dst", "labels", "checksums")})
+            for c in idx]
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch
+
+
+def _parse(ds: DisjointSet):
+    """ConnectedComponentsTest.parser (example/test/ConnectedComponentsTest.java:65-81)."""
+    r = ds.toString()
+    out = []
+    for g in r.split("="):
+        if "[" in g:
+            out.append(g.split("]")[0][1:])
+    return sorted(out)
+
+
+# ---------------- reference known-answer tests ----------------
+@pytest.mark.parametrize("bits", [32, 64])
+def test_disjointset_kat(bits):
+    k = _kats()["DisjointSetTest"]
+    ds = DisjointSet(256, id_bits=bits)
+    for a, b in k["setup_unions"]:
+        ds.union(a, b)
+    assert ds.size() == k["expect_matches_size"]
+    r0, r1 = ds.find(0), ds.find(1)
+    assert r0 != r1
+    for i in range(10):
+        assert ds.find(i) == (r0 if i % 2 == 0 else r1)
+    assert ds.find(77) is None
+    ds2 = DisjointSet(256, id_bits=bits)
+    for a, b in k["merge_unions"]:
+        ds2.union(a, b)
+    ds2.merge(ds)
+    assert ds2.size() == k["expect_merged_size"]
+    v, l = ds2.pairs()
+    assert len(set(l.tolist())) == k["expect_merged_roots"]
+
+
+@pytest.mark.parametrize("mode", ["fused", "reference"])
+def test_connected_components_kat(mode):
+    k = _kats()["ConnectedComponentsTest"]
+    e = np.array(k["edges"])
+    stream = SimpleEdgeStream(e[:, 0], e[:, 1])
+    last = None
+    for ds in stream.aggregate(ConnectedComponents(5, window_edges=2, mode=mode, parallelism=2)):
+        last = _parse(ds)
+    assert last == k["expect_final_components"]
+
+
+def test_example_sample_stream_event_time():
+    k = _kats()["ConnectedComponentsExample"]
+    stream = SimpleEdgeStream(k["src"], k["dst"], k["timestamps"])
+    emissions = []
+    for ds in stream.aggregate(ConnectedComponents(k["merge_window_ms"])):
+        emissions.append(ds.getMatches())
+    assert len(emissions) == len(k["event_time_windows"])
+    for em, w in zip(emissions, k["event_time_windows"]):
+        assert len(em) == w["n_vertices"]
+        assert all(lab == (1 if v % 2 else 2) for v, lab in em.items())
+    assert len(emissions[-1]) == k["expect_final_vertices"]
+
+
+# ---------------- golden seeded streams, per-window emissions ----------------
+@pytest.mark.parametrize("bits", [32, 64])
+@pytest.mark.parametrize("mode", ["fused", "reference"])
+@pytest.mark.parametrize("case", _streams(), ids=lambda c: c["name"])
+def test_streams_golden(case, mode, bits):
+    stream = SimpleEdgeStream(case["src"], case["dst"])
+    cc = ConnectedComponents(1000, window_edges=case["window_edges"], parallelism=case["partitions"],
+                             mode=mode, id_bits=bits, vertex_capacity=case["cap"])
+    w = 0
+    for ds in stream.aggregate(cc):
+        lab = ds.dense().astype(np.int64)
+        np.testing.assert_array_equal(lab, case["labels"][w], err_msg="window %d" % w)
+        assert ds.checksum()[0] == int(case["checksums"][w])
+        w += 1
+    assert w == case["labels"].shape[0]
+
+
+# ---------------- larger random streams vs the C oracle ----------------
+@pytest.mark.parametrize("gen,scale,n,W", [("rmat", 16, 1 << 20, 1 << 16), ("er", 17, 1 << 19, 100003),
+                                           ("rmat", 12, 300000, 4096)])
+def test_random_streams_vs_oracle(oracle, torch_cuda, gen, scale, n, W):
+    torch = torch_cuda
+    cap = 1 << scale
+    if gen == "rmat":
+        s, d = oracle.gen_rmat(0, n, scale, 17)
+    else:
+        s, d = oracle.gen_er(0, n, cap, 5)
+    want = oracle.run(s, d, W, partitions=4, threads=4, emit=EMIT_CHECKSUM, label_cap=cap, want_final=True)
+    ds = DisjointSet(cap, id_bits=32)
+    ts = torch.from_numpy(s.astype(np.int32)).cuda()
+    td = torch.from_numpy(d.astype(np.int32)).cuda()
+    for w, lo in enumerate(range(0, n, W)):
+        ds.fold(ts[lo:lo + W], td[lo:lo + W])
+        ds.close_window()
+        h, nv, nc = ds.checksum()
+        assert h == int(want["checksums"][w]), "window %d" % w
+    np.testing.assert_array_equal(ds.dense().astype(np.int64), want["final"])
+    assert ds.stats() == (want["final_vertices"], want["final_components"])
+
+
+def test_host_and_device_buffers_agree(oracle, torch_cuda):
+    torch = torch_cuda
+    s, d = oracle.gen_rmat(0, 200000, 14, 4)
+    a = DisjointSet(1 << 14, id_bits=64, staging_edges=4096)   # host int64, staged in chunks
+    a.fold(s, d)
+    b = DisjointSet(1 << 14, id_bits=64)
+    b.fold(torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda())
+    np.testing.assert_array_equal(a.dense(), b.dense())
+    out = torch.empty(1 << 14, dtype=torch.int64, device="cuda")
+    b.dense(out=out)
+    np.testing.assert_array_equal(out.cpu().numpy(), a.dense())
+
+
+def test_combine_cc_semantics():
+    a = DisjointSet(64, id_bits=32)
+    b = DisjointSet(64, id_bits=32)
+    a.union(1, 2)
+    for i in range(5):
+        b.union(10 + i, 11 + i)
+    r = combine_cc(a, b)
+    assert r is b and b.size() == 8
+    c = DisjointSet(64, id_bits=32)
+    c.union(2, 10)
+    r = combine_cc(b, c)
+    assert r is b
+    assert b.find(15) == 1 and b.find(11) == 1 and b.find(2) == 1
+
+
+# ---------------- edge cases ----------------
+def test_empty_and_noop_calls():
+    ds = DisjointSet(16, id_bits=32)
+    ds.fold(np.array([], dtype=np.int32), np.array([], dtype=np.int32))
+    ds.close_window()
+    assert ds.stats() == (0, 0)
+    assert ds.pairs()[0].size == 0
+    assert (ds.dense() == -1).all()
+    assert ds.checksum() == (0, 0, 0)
+
+
+def test_out_of_range_ids_raise_and_are_skipped():
+    ds = DisjointSet(100, id_bits=64)
+    ds.fold(np.array([1, 5, -3]), np.array([2, 100, 4]))
+    with pytest.raises(GsError) as ei:
+        ds.sync()
+    assert ei.value.code == _abi.GS_ERR_RANGE
+    assert ds.getMatches() == {1: 1, 2: 1}
+    ds32 = DisjointSet(100, id_bits=32)
+    with pytest.raises(GsError):
+        ds32.fold(np.array([0xFFFFFFFF], dtype=np.uint32), np.array([1], dtype=np.uint32))
+        ds32.sync()
+
+
+def test_self_loops_and_duplicates():
+    ds = DisjointSet(32, id_bits=32)
+    ds.fold(np.array([3, 3, 4, 4, 9]), np.array([3, 3, 9, 9, 4]))
+    assert ds.getMatches() == {3: 3, 4: 4, 9: 4}
+    assert ds.stats() == (3, 2)
+
+
+def test_max_capacity_id_and_find_batch():
+    cap = (1 << 20) + 3
+    ds = DisjointSet(cap, id_bits=64)
+    ds.fold(np.array([cap - 1, 7]), np.array([0, cap - 2]))
+    r = ds.find_batch(np.array([cap - 1, cap - 2, 0, 7, 5, cap, -1]))
+    assert r.tolist() == [0, 7, 0, 7, -1, -1, -1]
+
+
+def test_emit_pairs_sorted_and_capacity_error(torch_cuda):
+    ds = DisjointSet(5000, id_bits=32)
+    rng = np.random.default_rng(1)
+    s, d = rng.integers(0, 5000, 3000), rng.integers(0, 5000, 3000)
+    ds.fold(s, d)
+    v, l = ds.pairs()
+    assert (np.diff(v) > 0).all()
+    dense = ds.dense()
+    np.testing.assert_array_equal(dense[v], l)
+    assert (dense >= 0).sum() == v.size
+    import ctypes
+    n = ctypes.c_uint64()
+    small = np.empty(4, dtype=np.int32)
+    rc = _abi.lib().gs_cc_emit_pairs(ds.handle, small.ctypes.data_as(ctypes.c_void_p),
+                                     small.ctypes.data_as(ctypes.c_void_p), 2, ctypes.byref(n))
+    assert rc == _abi.GS_ERR_CAPACITY and n.value == v.size
+
+
+def test_reset_and_transient_state():
+    ds = DisjointSet(64, id_bits=32)
+    ds.union(1, 2)
+    ds.reset()
+    assert ds.stats() == (0, 0)
+    ds.union(3, 4)
+    assert ds.getMatches() == {3: 3, 4: 3}
+
+
+# ---------------- device generators vs the host definition ----------------
+@pytest.mark.parametrize("bits", [32, 64])
+def test_device_generators_match_oracle(oracle, torch_cuda, bits):
+    torch = torch_cuda
+    from gsgpu import gen
+    dt = torch.int32 if bits == 32 else torch.int64
+    for first, n, scale, seed, scr in [(0, 100000, 20, 1, True), (1 << 30, 4096, 26, 1, True),
+                                       (77, 5000, 12, 9, False)]:
+        s = torch.empty(n, dtype=dt, device="cuda")
+        d = torch.empty(n, dtype=dt, device="cuda")
+        gen.rmat(s, d, first, scale, seed, scramble=scr)
+        torch.cuda.synchronize()
+        ws, wd = oracle.gen_rmat(first, n, scale, seed, scramble=scr)
+        np.testing.assert_array_equal(s.cpu().numpy().astype(np.int64), ws)
+        np.testing.assert_array_equal(d.cpu().numpy().astype(np.int64), wd)
+    s = torch.empty(50000, dtype=dt, device="cuda")
+    d = torch.empty(50000, dtype=dt, device="cuda")
+    gen.erdos_renyi(s, d, 123, 1 << 24, 2)
+    torch.cuda.synchronize()
+    ws, wd = oracle.gen_er(123, 50000, 1 << 24, 2)
+    np.testing.assert_array_equal(s.cpu().numpy().astype(np.int64), ws)
+    np.testing.assert_array_equal(d.cpu().numpy().astype(np.int64), wd)
+
+
+# ---------------- partial-summary exchange (multi-GPU tree protocol, one process) ----------------
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_tree_exchange_single_process(oracle, torch_cuda, world):
+    """Every 'rank' is a handle on this GPU; the tree rounds of gsgpu/tree.py are replayed with
+    device buffers handed across directly (what RCCL send/recv does between GPUs)."""
+    torch = torch_cuda
+    from gsgpu.tree import tree_schedule
+    scale, n, W = 13, 200000, 20000
+    cap = 1 << scale
+    s, d = oracle.gen_rmat(0, n, scale, 8)
+    s = np.concatenate([s, [cap - 1, cap - 2]]); d = np.concatenate([d, [cap - 1, cap - 2]])
+    n = s.size
+    want = oracle.run(s, d, W, partitions=world, emit=EMIT_DENSE, label_cap=cap)["labels"]
+    ranks = [DisjointSet(cap, id_bits=32, track_marks=(r != 0)) for r in range(world)]
+    buf = torch.empty(2 * cap, dtype=torch.int32, device="cuda")
+    scheds = [tree_schedule(r, world) for r in range(world)]
+    ts = torch.from_numpy(s.astype(np.int32)).cuda()
+    td = torch.from_numpy(d.astype(np.int32)).cuda()
+    for w, lo in enumerate(range(0, n, W)):
+        ln = min(W, n - lo)
+        for r in range(world):
+            a, b = lo + (ln * r) // world, lo + (ln * (r + 1)) // world
+            ranks[r].fold(ts[a:b], td[a:b])
+        done = set()
+        for i in range(len(scheds[0])):
+            for r in range(world):
+                if r in done:
+                    continue
+                role, peer = scheds[r][i]
+                if role == "send":
+                    m = ranks[r].export_marks(buf)
+                    ranks[peer].fold_pairs(buf, m, id_bits=32)
+                    done.add(r)
+        ranks[0].close_window()
+        np.testing.assert_array_equal(ranks[0].dense().astype(np.int64), want[w], err_msg="window %d" % w)
+
+
+# ---------------- full-size properties (independent torch checker) ----------------
+def _torch_min_labels(torch, src, dst, V):
+    """Independent min-label CC on the GPU with torch ops (hook-to-min + pointer jumping)."""
+    lab = torch.arange(V, dtype=torch.int64, device="cuda")
+    s = src.long(); d = dst.long()
+    while True:
+        ls, ld = lab[s], lab[d]
+        m = torch.minimum(ls, ld)
+        new = lab.clone()
+        new.scatter_reduce_(0, ls, m, reduce="amin")
+        new.scatter_reduce_(0, ld, m, reduce="amin")
+        while True:                                   # pointer jumping to the fixpoint
+            j = new[new]
+            if torch.equal(j, new):
+                break
+            new = j
+        if torch.equal(new, lab):
+            break
+        lab = new
+    seen = torch.zeros(V, dtype=torch.bool, device="cuda")
+    seen[s] = True
+    seen[d] = True
+    return torch.where(seen, lab, torch.full_like(lab, -1))
+
+
+@pytest.mark.parametrize("scale,ef,W", [(22, 16, 1 << 22), (24, 16, 1 << 24)])
+def test_full_size_rmat_properties(torch_cuda, scale, ef, W):
+    torch = torch_cuda
+    from gsgpu import gen
+    V, E = 1 << scale, ef << scale
+    s = torch.empty(E, dtype=torch.int32, device="cuda")
+    d = torch.empty(E, dtype=torch.int32, device="cuda")
+    gen.rmat(s, d, 0, scale, 1)
+    ds = DisjointSet(V, id_bits=32)
+    ds.set_stream(torch.cuda.current_stream())
+    sums = []
+    for lo in range(0, E, W):
+        ds.fold(s[lo:lo + W], d[lo:lo + W])
+        ds.close_window()
+        sums.append(ds.checksum())
+    lab = torch.empty(V, dtype=torch.int32, device="cuda")
+    ds.dense(out=lab)
+    lab = lab.long()
+    seenmask = lab >= 0
+    v = torch.arange(V, device="cuda")
+    # min-id labels: label <= vertex, label is its own label (idempotent), edges agree
+    assert bool((lab[seenmask] <= v[seenmask]).all())
+    assert bool((lab[lab[seenmask]] == lab[seenmask]).all())
+    assert bool((lab[s.long()] == lab[d.long()]).all())
+    want = _torch_min_labels(torch, s, d, V)
+    assert torch.equal(lab, want)
+    # checksum of the final emission recomputed from the dense labels
+    assert sums[-1][0] == dense_checksum(lab.cpu().numpy())[0]
+    # number of vertices is monotone over the windows (cumulative summary)
+    assert all(a[1] <= b[1] for a, b in zip(sums, sums[1:]))

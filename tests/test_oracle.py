@@ -1,0 +1,193 @@
+"""CPU: pin the oracle (C restatement + Python twin) against the reference's golden vectors."""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+from pyoracle import (EMIT_CHECKSUM, EMIT_DENSE, PyDisjointSet, canonical_to_dense, dense_checksum,
+                      py_cc_stream)
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _kats():
+    with open(os.path.join(GOLD, "reference_kats.json")) as f:
+        return json.load(f)
+
+
+def _streams():
+    with open(os.path.join(GOLD, "streams_index.json")) as f:
+        idx = json.load(f)
+    z = np.load(os.path.join(GOLD, "streams.npz"))   # allow_pickle=False (default)
+    return [dict(c, **{k: z["%s__%s" % (c["name"], k)] for k in ("src", "dst", "labels", "checksums")})
+            for c in idx]
+
+
+# ---- DisjointSetTest (util/DisjointSetTest.java:37-78) ----
+def test_disjointset_kat_python_twin():
+    k = _kats()["DisjointSetTest"]
+    ds = PyDisjointSet()
+    for a, b in k["setup_unions"]:
+        ds.union(a, b)
+    assert len(ds.getMatches()) == k["expect_matches_size"]
+    r0, r1 = ds.find(0), ds.find(1)
+    assert r0 != r1
+    for i in range(10):
+        assert ds.find(i) == (r0 if i % 2 == 0 else r1)
+    ds2 = PyDisjointSet()
+    for a, b in k["merge_unions"]:
+        ds2.union(a, b)
+    ds2.merge(ds)
+    assert len(ds2.getMatches()) == k["expect_merged_size"]
+    assert len({ds2.find(e) for e in ds2.getMatches()}) == k["expect_merged_roots"]
+    assert ds2.find(12345) is None                         # find() of an unknown id is null
+
+
+def test_disjointset_kat_c_oracle(oracle):
+    L = oracle.L
+    k = _kats()["DisjointSetTest"]
+    ds = L.gso_ds_new()
+    for a, b in k["setup_unions"]:
+        L.gso_ds_union(ds, a, b)
+    assert L.gso_ds_size(ds) == k["expect_matches_size"]
+    r = ctypes.c_int64()
+    roots = []
+    for i in range(10):
+        assert L.gso_ds_find(ds, i, ctypes.byref(r)) == 1
+        roots.append(r.value)
+    assert roots[0] != roots[1]
+    assert all(roots[i] == roots[i % 2] for i in range(10))
+    ds2 = L.gso_ds_new()
+    for a, b in k["merge_unions"]:
+        L.gso_ds_union(ds2, a, b)
+    L.gso_ds_merge(ds2, ds)
+    assert L.gso_ds_size(ds2) == k["expect_merged_size"]
+    rs = set()
+    for i in range(L.gso_ds_size(ds2)):
+        L.gso_ds_find(ds2, L.gso_ds_key_at(ds2, i), ctypes.byref(r))
+        rs.add(r.value)
+    assert len(rs) == k["expect_merged_roots"]
+    assert L.gso_ds_find(ds2, 999, ctypes.byref(r)) == 0
+    L.gso_ds_free(ds)
+    L.gso_ds_free(ds2)
+
+
+def test_combine_cc_merges_smaller_into_larger(oracle):
+    L = oracle.L
+    a, b = L.gso_ds_new(), L.gso_ds_new()
+    L.gso_ds_union(a, 1, 2)
+    for i in range(5):
+        L.gso_ds_union(b, 10 + i, 11 + i)
+    assert L.gso_combine(a, b) == b          # |a| = 2 <= |b| = 6 -> b.merge(a), return b
+    assert L.gso_ds_size(b) == 8
+    c = L.gso_ds_new()
+    L.gso_ds_union(c, 100, 101)
+    assert L.gso_combine(b, c) == b          # |b| = 8 > |c| = 2 -> b.merge(c), return b
+    assert L.gso_ds_size(b) == 10
+    for d in (a, b, c):
+        L.gso_ds_free(d)
+
+
+# ---- ConnectedComponentsTest (example/test/ConnectedComponentsTest.java:41,54-63) ----
+def _components(labels: np.ndarray):
+    comps = {}
+    for v in np.nonzero(labels >= 0)[0].tolist():
+        comps.setdefault(int(labels[v]), []).append(v)
+    return sorted(", ".join(map(str, sorted(m))) for m in comps.values())
+
+
+def test_connected_components_kat(oracle):
+    k = _kats()["ConnectedComponentsTest"]
+    e = np.array(k["edges"], dtype=np.int64)
+    r = oracle.run(e[:, 0], e[:, 1], 0, partitions=1, emit=EMIT_DENSE, label_cap=16, want_final=True)
+    assert _components(r["final"]) == k["expect_final_components"]
+    # partition count does not change the result
+    r4 = oracle.run(e[:, 0], e[:, 1], 2, partitions=4, emit=EMIT_DENSE, label_cap=16, want_final=True)
+    assert _components(r4["final"]) == k["expect_final_components"]
+
+
+def test_example_sample_stream(oracle):
+    k = _kats()["ConnectedComponentsExample"]
+    src = np.array(k["src"])
+    dst = np.array(k["dst"])
+    r = oracle.run(src, dst, 0, emit=EMIT_DENSE, label_cap=128, want_final=True)
+    lab = r["final"]
+    seen = np.nonzero(lab >= 0)[0]
+    assert seen.size == k["expect_final_vertices"]
+    assert all(lab[v] == (1 if v % 2 else 2) for v in seen)
+    # event-time windows: cumulative emissions after each window
+    for w in k["event_time_windows"]:
+        a, b = w["edges"]
+        rr = oracle.run(src[:b], dst[:b], 0, emit=EMIT_DENSE, label_cap=128, want_final=True)
+        assert int((rr["final"] >= 0).sum()) == w["n_vertices"]
+
+
+# ---- seeded streams: per-window emissions ----
+@pytest.mark.parametrize("case", _streams(), ids=lambda c: c["name"])
+def test_streams_golden_c_oracle(oracle, case):
+    r = oracle.run(case["src"], case["dst"], case["window_edges"], partitions=case["partitions"],
+                   threads=2, emit=EMIT_DENSE, label_cap=case["cap"])
+    assert r["windows"] == case["labels"].shape[0]
+    np.testing.assert_array_equal(r["labels"], case["labels"])
+    np.testing.assert_array_equal(r["checksums"], case["checksums"])
+    for w in range(r["windows"]):
+        assert dense_checksum(case["labels"][w])[0] == int(case["checksums"][w])
+
+
+@pytest.mark.parametrize("case", _streams()[:4], ids=lambda c: c["name"])
+def test_streams_golden_python_twin(case):
+    emis = py_cc_stream(case["src"].tolist(), case["dst"].tolist(), case["window_edges"], case["partitions"])
+    for w, c in enumerate(emis):
+        np.testing.assert_array_equal(canonical_to_dense(c, case["cap"]), case["labels"][w])
+
+
+@pytest.mark.parametrize("P,W", [(1, 1000), (3, 777), (8, 4096), (5, 0)])
+def test_partition_and_window_invariance_of_final_labels(oracle, P, W):
+    s, d = oracle.gen_rmat(0, 20000, 12, 3)
+    base = oracle.run(s, d, 0, partitions=1, emit=EMIT_CHECKSUM, label_cap=4096, want_final=True)
+    r = oracle.run(s, d, W, partitions=P, threads=4, emit=EMIT_CHECKSUM, label_cap=4096, want_final=True)
+    np.testing.assert_array_equal(base["final"], r["final"])
+    assert r["final_vertices"] == base["final_vertices"]
+
+
+def test_checksum_definition_c_matches_numpy(oracle):
+    lab = np.array([-1, 0, 0, 3, -1, 3, 0], dtype=np.int64)
+    want = 0
+    for v, l in enumerate(lab.tolist()):
+        if l >= 0:
+            want = (want + oracle.L.gso_pair_mix(v, l)) & ((1 << 64) - 1)
+    assert dense_checksum(lab)[0] == want
+
+
+# ---- generators ----
+def test_generators_golden(oracle):
+    with open(os.path.join(GOLD, "generators.json")) as f:
+        g = json.load(f)
+    s, d = oracle.gen_rmat(0, 64, 20, 1)
+    assert [s.tolist(), d.tolist()] == g["rmat_s20_seed1_first0"]
+    s, d = oracle.gen_rmat(1 << 20, 64, 26, 1)
+    assert [s.tolist(), d.tolist()] == g["rmat_s26_seed1_first1M"]
+    s, d = oracle.gen_er(0, 64, 1 << 24, 2)
+    assert [s.tolist(), d.tolist()] == g["er_n2^24_seed2_first0"]
+    s, d = oracle.gen_rmat(5, 64, 12, 9, scramble=False)
+    assert [s.tolist(), d.tolist()] == g["rmat_s12_seed9_first5_noscramble"]
+
+
+def test_generator_is_counter_based(oracle):
+    s, d = oracle.gen_rmat(0, 1000, 16, 5)
+    s2, d2 = oracle.gen_rmat(400, 600, 16, 5)
+    np.testing.assert_array_equal(s[400:], s2)
+    np.testing.assert_array_equal(d[400:], d2)
+    assert s.min() >= 0 and s.max() < (1 << 16)
+
+
+def test_rmat_scramble_is_bijection(oracle):
+    # scrambled ids of the unscrambled stream's distinct ids stay distinct
+    s, d = oracle.gen_rmat(0, 50000, 10, 11, scramble=False)
+    s2, d2 = oracle.gen_rmat(0, 50000, 10, 11, scramble=True)
+    pairs = {}
+    for a, b in zip(np.concatenate([s, d]).tolist(), np.concatenate([s2, d2]).tolist()):
+        assert pairs.setdefault(a, b) == b
+    assert len(set(pairs.values())) == len(pairs)
