@@ -98,8 +98,12 @@ def main():
             else:
                 ds.close_window()
 
+    log = lambda m: print("[bench rank %d] %s" % (rank, m), file=sys.stderr, flush=True)
+    log("inputs ready: %d edges/rank, %d windows of %d" % (E_rank, nwin, W_rank))
     for _ in range(a.warmup):
         step()
+    torch.cuda.synchronize()
+    log("warmup done")
     ds.timing(True)
     if world > 1:
         dist.barrier()
@@ -179,6 +183,7 @@ def main():
         if verify is not None:
             line["verify"] = verify
         if not a.no_cpu_baseline and world == 1:
+            log("timed region done (%.1f ms/step); cpu baseline..." % (elapsed / a.steps * 1e3))
             line["cpu_baseline"] = cpu_baseline(a, src, dst, W_rank)
         print(json.dumps(line), flush=True)
     ds.close()

@@ -21,11 +21,14 @@
 
 namespace gsgpu {
 
-// Root of x, given px = a parent[x] value already read (px != kInvalid). Walks with
-// intermediate pointer jumping (each visited word gets its grandparent) and stops at the first
-// word that is not strictly smaller than its index (a root, or a stale kInvalid read).
+// Root of x, given px = a parent[x] value already read. Walks with intermediate pointer jumping
+// (each visited word gets its grandparent) and stops at the first word that is not strictly
+// smaller than its index: a root, or a stale kInvalid read from L1 of a vertex another CU has
+// just initialised (treated as a root; a hook on it is then decided by the CAS, which sees the
+// true word). A non-root's parent is always < its index, so px >= x covers both cases and no
+// walk ever indexes parent[kInvalid].
 __device__ __forceinline__ uint32_t find_root(uint32_t* __restrict__ parent, uint32_t x, uint32_t px) {
-    if (px == x) return x;
+    if (px >= x) return x;
     uint32_t prev = x, cur = px, next;
     while (cur > (next = parent[cur])) {
         parent[prev] = next;

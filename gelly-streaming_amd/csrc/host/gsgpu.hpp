@@ -1,0 +1,232 @@
+// gsgpu.hpp — C++ host mirror of the reference's Connected Components operator surface, over the
+// C ABI of libgsgpu.so (include/gsgpu.h). Header-only; no HIP types appear here.
+//
+// Reference types mirrored (paths relative to src/main/java/org/apache/flink/graph/streaming/):
+//   DisjointSet<K>                 summaries/DisjointSet.java:25-150
+//   UpdateCC / CombineCC           library/ConnectedComponents.java:70-126
+//   SummaryBulkAggregation         SummaryBulkAggregation.java:46-131 (+ Merger, SummaryAggregation.java:94-136)
+//   ConnectedComponents(long)      library/ConnectedComponents.java:44-55
+//   SimpleEdgeStream::aggregate    SimpleEdgeStream.java:100-102
+// Errors: the Java UDFs throw Exception; here a failing ABI call throws gelly::streaming::GsError
+// carrying the GS_ERR_* code and gs_last_error() text.
+#pragma once
+
+#include <algorithm>
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <optional>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+#include "gsgpu.h"
+
+namespace gelly {
+namespace streaming {
+
+class GsError : public std::runtime_error {
+public:
+    GsError(int code, const std::string& where)
+        : std::runtime_error(where + " failed (" + std::to_string(code) + "): " + gs_last_error()), code_(code) {}
+    int code() const { return code_; }
+
+private:
+    int code_;
+};
+
+inline void check(int rc, const char* where) {
+    if (rc != GS_OK) throw GsError(rc, where);
+}
+
+// DisjointSet<K> on the device. K = int32_t or int64_t ids in [0, capacity).
+template <typename K>
+class DisjointSet {
+    static_assert(std::is_same<K, int32_t>::value || std::is_same<K, int64_t>::value, "K must be int32_t or int64_t");
+
+public:
+    explicit DisjointSet(uint64_t capacity, int device = 0, uint32_t flags = 0) : cap_(capacity) {
+        gs_cc_config cfg{};
+        cfg.struct_size = sizeof(gs_cc_config);
+        cfg.id_bits = sizeof(K) * 8;
+        cfg.vertex_capacity = capacity;
+        cfg.device = device;
+        cfg.flags = flags;
+        check(gs_cc_create(&h_, &cfg), "gs_cc_create");
+    }
+    ~DisjointSet() { gs_cc_destroy(h_); }
+    DisjointSet(const DisjointSet&) = delete;
+    DisjointSet& operator=(const DisjointSet&) = delete;
+    DisjointSet(DisjointSet&& o) noexcept : h_(o.h_), cap_(o.cap_) { o.h_ = nullptr; }
+
+    gs_cc_t* handle() const { return h_; }
+    uint64_t capacity() const { return cap_; }
+
+    void reset() { check(gs_cc_reset(h_), "gs_cc_reset"); }
+
+    // makeSet (:53-56) for an id not yet present
+    void makeSet(K e) { union_(e, e); }
+
+    // union (:92-118); `union` is a C++ keyword
+    void union_(K e1, K e2) { fold(&e1, &e2, 1); }
+
+    // find (:66-80): root, or nullopt for an unknown id (Java null)
+    std::optional<K> find(K e) {
+        K r = -1;
+        check(gs_cc_find(h_, &e, &r, 1), "gs_cc_find");
+        if (r < 0) return std::nullopt;
+        return r;
+    }
+
+    // merge (:127-131)
+    void merge(DisjointSet& other) { check(gs_cc_merge(h_, other.h_), "gs_cc_merge"); }
+
+    // getMatches().size()
+    uint64_t size() {
+        uint64_t nv = 0, nc = 0;
+        check(gs_cc_stats(h_, &nv, &nc), "gs_cc_stats");
+        return nv;
+    }
+    uint64_t numComponents() {
+        uint64_t nv = 0, nc = 0;
+        check(gs_cc_stats(h_, &nv, &nc), "gs_cc_stats");
+        return nc;
+    }
+
+    // getMatches() (:44-46) as the canonical vertex -> root map (roots are component minima)
+    std::map<K, K> getMatches() {
+        std::vector<K> v, l;
+        pairs(v, l);
+        std::map<K, K> m;
+        for (size_t i = 0; i < v.size(); ++i) m.emplace(v[i], l[i]);
+        return m;
+    }
+
+    // sorted (vertex, label) emission
+    void pairs(std::vector<K>& v, std::vector<K>& l) {
+        uint64_t n = size(), got = 0;
+        v.resize(n);
+        l.resize(n);
+        check(gs_cc_emit_pairs(h_, v.data(), l.data(), n, &got), "gs_cc_emit_pairs");
+        v.resize(got);
+        l.resize(got);
+    }
+
+    // toString (:133-150): {root=[members...], ...}, roots and members ascending
+    std::string toString() {
+        std::vector<K> v, l;
+        pairs(v, l);
+        std::map<K, std::vector<K>> comps;
+        for (size_t i = 0; i < v.size(); ++i) comps[l[i]].push_back(v[i]);
+        std::ostringstream os;
+        os << "{";
+        bool first = true;
+        for (auto& kv : comps) {
+            if (!first) os << ", ";
+            first = false;
+            os << kv.first << "=[";
+            for (size_t i = 0; i < kv.second.size(); ++i) os << (i ? ", " : "") << kv.second[i];
+            os << "]";
+        }
+        os << "}";
+        return os.str();
+    }
+
+    // batched UpdateCC: host or device buffers
+    void fold(const K* src, const K* dst, uint64_t n) { check(gs_cc_fold(h_, src, dst, n), "gs_cc_fold"); }
+    void closeWindow() { check(gs_cc_close_window(h_), "gs_cc_close_window"); }
+    void sync() { check(gs_cc_sync(h_), "gs_cc_sync"); }
+
+private:
+    gs_cc_t* h_ = nullptr;
+    uint64_t cap_ = 0;
+};
+
+// EdgesFold<K, NullValue, DisjointSet<K>> (ConnectedComponents.java:70-86)
+template <typename K>
+struct UpdateCC {
+    DisjointSet<K>& foldEdges(DisjointSet<K>& ds, K vertex, K vertex2) {
+        ds.union_(vertex, vertex2);
+        return ds;
+    }
+    DisjointSet<K>& foldBatch(DisjointSet<K>& ds, const K* src, const K* dst, uint64_t n) {
+        ds.fold(src, dst, n);
+        return ds;
+    }
+};
+
+// ReduceFunction<DisjointSet<K>> (ConnectedComponents.java:95-126)
+template <typename K>
+struct CombineCC {
+    DisjointSet<K>* reduce(DisjointSet<K>* s1, DisjointSet<K>* s2) {
+        gs_cc_t* out = nullptr;
+        check(gs_cc_combine(s1->handle(), s2->handle(), &out), "gs_cc_combine");
+        return out == s1->handle() ? s1 : s2;
+    }
+};
+
+// An edge stream in arrival order with optional event timestamps (ms).
+template <typename K>
+struct SimpleEdgeStream {
+    std::vector<K> src, dst;
+    std::vector<int64_t> timestamps;   // empty => no event time
+
+    // [begin, end) edge ranges of the windows: event-time tumbling windows of `millis`
+    // (window = ts / millis) or, without timestamps, count windows of `window_edges`
+    std::vector<std::pair<size_t, size_t>> windows(int64_t millis, uint64_t window_edges) const {
+        std::vector<std::pair<size_t, size_t>> w;
+        const size_t n = src.size();
+        if (n == 0) return w;
+        if (!timestamps.empty() && window_edges == 0) {
+            size_t a = 0;
+            for (size_t i = 1; i <= n; ++i)
+                if (i == n || timestamps[i] / millis != timestamps[i - 1] / millis) { w.emplace_back(a, i); a = i; }
+            return w;
+        }
+        const uint64_t W = window_edges ? window_edges : n;
+        for (size_t a = 0; a < n; a += W) w.emplace_back(a, std::min<size_t>(a + W, n));
+        return w;
+    }
+};
+
+// SummaryBulkAggregation specialised to ConnectedComponents: every window's edges are folded into
+// the cumulative device summary, the window is closed (compressed), and the Merger emits the
+// summary (transientState == false keeps it across windows). Canonical labels equal the
+// reference's whatever the partitioning (see gsgpu/aggregation.py, mode "fused").
+template <typename K>
+class ConnectedComponents {
+public:
+    explicit ConnectedComponents(long mergeWindowTime, uint64_t vertex_capacity = 0, int device = 0,
+                                 uint64_t window_edges = 0)
+        : millis_(mergeWindowTime), cap_(vertex_capacity), device_(device), window_edges_(window_edges) {}
+
+    // SummaryAggregation.run -> one emission per window
+    void run(const SimpleEdgeStream<K>& s, const std::function<void(DisjointSet<K>&)>& emit) {
+        uint64_t cap = cap_;
+        if (!cap) {
+            K mx = 0;
+            for (K x : s.src) mx = std::max(mx, x);
+            for (K x : s.dst) mx = std::max(mx, x);
+            cap = (uint64_t)mx + 1;
+        }
+        DisjointSet<K> summary(cap, device_);
+        UpdateCC<K> update;
+        for (auto& w : s.windows(millis_, window_edges_)) {
+            update.foldBatch(summary, s.src.data() + w.first, s.dst.data() + w.first, w.second - w.first);
+            summary.closeWindow();
+            emit(summary);
+        }
+    }
+
+private:
+    long millis_;
+    uint64_t cap_;
+    int device_;
+    uint64_t window_edges_;
+};
+
+}  // namespace streaming
+}  // namespace gelly

@@ -344,3 +344,38 @@ def test_full_size_rmat_properties(torch_cuda, scale, ef, W):
     assert sums[-1][0] == dense_checksum(lab.cpu().numpy())[0]
     # number of vertices is monotone over the windows (cumulative summary)
     assert all(a[1] <= b[1] for a, b in zip(sums, sums[1:]))
+
+
+# ---------------- C++ host mirror: ConnectedComponentsExample port ----------------
+def _example_bin():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return os.path.join(root, "gelly-streaming_amd", "gsgpu", "lib", "cc_example")
+
+
+def _parse_pairs(out: str):
+    import re
+    return [(int(a), int(b)) for a, b in re.findall(r"^\((-?\d+),(-?\d+)\)$", out, re.M)]
+
+
+def test_cc_example_builtin_stream():
+    import subprocess
+    out = subprocess.check_output([_example_bin()], timeout=120).decode()
+    pairs = _parse_pairs(out)
+    assert pairs, out
+    assert all(r == (1 if v % 2 else 2) for v, r in pairs)
+    assert {v for v, _ in pairs} == set(range(1, 103))
+
+
+def test_cc_example_file_input(tmp_path):
+    import subprocess
+    k = _kats()["ConnectedComponentsTest"]
+    f = tmp_path / "edges.txt"
+    f.write_text("".join("%d %d\n" % (a, b) for a, b in k["edges"]))
+    out = subprocess.check_output([_example_bin(), str(f), "2", "1"], timeout=120).decode()
+    last = {}
+    for v, r in _parse_pairs(out):
+        last[v] = r
+    comps = {}
+    for v, r in last.items():
+        comps.setdefault(r, []).append(v)
+    assert sorted(", ".join(map(str, sorted(m))) for m in comps.values()) == k["expect_final_components"]
