@@ -160,6 +160,9 @@ __global__ __launch_bounds__(256) void k_merge_dense(const uint32_t* __restrict_
 }
 
 // Merger emission: full compression. Afterwards parent[v] = root(v) = canonical label.
+// Only v's own thread writes parent[v] here, and it walks read-only: a path-halving store
+// from another thread's walk could land after v's thread stored the root and put back an
+// intermediate ancestor (a valid forest, but not the fully compressed emission).
 __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent, uint32_t n) {
     const uint32_t stride = gridDim.x * blockDim.x * 4;
     for (uint32_t base = (blockIdx.x * blockDim.x + threadIdx.x) * 4; base < n; base += stride) {
@@ -181,7 +184,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
         for (int k = 0; k < 4; ++k) {
             const uint32_t v = base + k;
             if (p[k] == kInvalid || p[k] == v || gp[k] == p[k]) continue;   // root / unseen / depth 1
-            parent[v] = find_root(parent, p[k], gp[k]);
+            parent[v] = find_root_ro(parent, gp[k]);
         }
     }
 }
