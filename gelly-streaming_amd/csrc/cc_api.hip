@@ -34,6 +34,8 @@ bool is_device_pointer(const void* p) {
     return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.isManaged;
 }
 
+static size_t mark_bytes(uint32_t cap) { return (((size_t)cap + 31) / 32) * 4; }
+
 static unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap_blocks) {
     uint64_t b = (items + per_block - 1) / per_block;
     if (b == 0) b = 1;
@@ -50,7 +52,7 @@ struct gs_cc {
     int device = 0;
     hipStream_t own = nullptr, stream = nullptr;
     uint32_t* parent = nullptr;          // dense summary / label array
-    uint8_t* mark = nullptr;             // per-vertex export marks (GS_CC_TRACK_MARKS)
+    uint32_t* mark = nullptr;            // export mark bitmap, 1 bit per vertex (GS_CC_TRACK_MARKS)
     uint32_t* derr = nullptr;            // deferred device error flags
     unsigned long long* dscratch = nullptr;  // reduction outputs (8 words)
     unsigned long long* hscratch = nullptr;  // pinned mirror
@@ -241,7 +243,7 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
     h->stream = h->own;
     if (hipMalloc(&h->parent, (size_t)h->cap * sizeof(uint32_t)) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "parent[%u] allocation failed", h->cap)); }
     if (cfg->flags & GS_CC_TRACK_MARKS) {
-        if (hipMalloc(&h->mark, ((size_t)h->cap + 15) & ~(size_t)15) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "mark allocation failed")); }
+        if (hipMalloc(&h->mark, mark_bytes(h->cap)) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "mark allocation failed")); }
     }
     if (hipMalloc(&h->derr, 64) != hipSuccess || hipMalloc(&h->dscratch, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&h->hscratch, 8 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
@@ -280,14 +282,14 @@ int gs_cc_reset(gs_cc_t* h) {
     GS_TRY(check(h));
     DeviceGuard g(h->device);
     GS_HIP(hipMemsetAsync(h->parent, 0xFF, (size_t)h->cap * sizeof(uint32_t), h->stream));
-    if (h->mark) GS_HIP(hipMemsetAsync(h->mark, 0, ((size_t)h->cap + 15) & ~(size_t)15, h->stream));
+    if (h->mark) GS_HIP(hipMemsetAsync(h->mark, 0, mark_bytes(h->cap), h->stream));
     h->compressed = true;
     return GS_OK;
 }
 
 int gs_cc_set_stream(gs_cc_t* h, void* s) {
     GS_TRY(check(h));
-    h->stream = s ? static_cast<hipStream_t>(s) : h->own;
+    h->stream = static_cast<hipStream_t>(s);     // NULL = the HIP null stream, like any HIP API
     return GS_OK;
 }
 
@@ -507,7 +509,7 @@ int gs_cc_export_marks(gs_cc_t* h, void* pairs, uint64_t cap, uint64_t* n_out) {
     GS_HIP(hipMemsetAsync(h->dscratch, 0, sizeof(unsigned long long), h->stream));
     {
         KTimer t(h, GS_K_EXPORT);
-        hipLaunchKernelGGL(k_export_marks, dim3(grid_for(h->cap, 256 * 16, 4096)), dim3(256), 0, h->stream,
+        hipLaunchKernelGGL(k_export_marks, dim3(grid_for((h->cap + 31) / 32, 256, 4096)), dim3(256), 0, h->stream,
                            h->mark, h->parent, h->cap, (uint32_t*)out, cap, h->dscratch);
     }
     GS_HIP(hipGetLastError());

@@ -10,11 +10,16 @@
 // emissions canonicalise to. DisjointSet.java:92-118 decides by rank instead; its trees differ,
 // its components (and hence canonical labels) do not.
 //
-// Visibility: plain loads of parent[] may return a stale (older) word from this CU's L1. Every
-// older value of parent[x] is an ancestor of x (or x itself, or kInvalid), so a stale read can
-// only shorten a walk; every write that matters is an agent-scope atomicCAS, which sees the true
-// word and makes a failed hook retry from the true parent. Path-halving writes store an
-// ancestor into a non-root word, which is valid whatever order they land in.
+// Visibility (8 XCDs, per-XCD L2s not coherent with each other, per-CU L1s never refreshed by
+// other CUs' stores): plain loads of parent[] may return a stale (older) word. Every older value
+// of parent[x] is an ancestor of x (or x itself, or kInvalid), so a stale read can only shorten a
+// walk. EVERY store to parent[] / mark[] inside a launch where other workgroups also write is a
+// device-scope atomic, executed at the memory side: hooks are atomicCAS (a failed hook retries
+// from the true parent), path halving is a no-return atomicMin (parents only ever decrease), marks
+// are atomicOr. A plain store would sit in the writer's XCD L2 as a dirty line and, written back
+// later, could overwrite a hook that another XCD made meanwhile on the same line; at RMAT-22 scale
+// that lost unions (tests/test_gpu_parity.py::test_full_size_rmat_properties). Plain stores are
+// used only where one workgroup owns every word of the line it writes (k_compress, k_export).
 #pragma once
 
 #include "common.hpp"
@@ -31,11 +36,15 @@ __device__ __forceinline__ uint32_t find_root(uint32_t* __restrict__ parent, uin
     if (px >= x) return x;
     uint32_t prev = x, cur = px, next;
     while (cur > (next = parent[cur])) {
-        parent[prev] = next;
+        __hip_atomic_fetch_min(&parent[prev], next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         prev = cur;
         cur = next;
     }
     return cur;
+}
+
+__device__ __forceinline__ void set_mark(uint32_t* __restrict__ mark, uint32_t v) {
+    __hip_atomic_fetch_or(&mark[v >> 5], 1u << (v & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Read-only root walk (no writes) for find() on const state.
@@ -55,12 +64,12 @@ __device__ __forceinline__ uint32_t make_set(uint32_t* __restrict__ parent, uint
 // union(u, v) given the parent words read by the caller. MARK: record hooked roots and
 // self-loop first touches in mark[] for the partial-summary export.
 template <bool MARK>
-__device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint8_t* __restrict__ mark,
+__device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32_t* __restrict__ mark,
                                            uint32_t u, uint32_t v, uint32_t pu, uint32_t pv) {
     if (u == v) {                                   // union(u,u): makeSet only
         if (pu == kInvalid) {
             const uint32_t old = atomicCAS(&parent[u], kInvalid, u);
-            if (MARK && old == kInvalid) mark[u] = 1;
+            if (MARK && old == kInvalid) set_mark(mark, u);
         }
         return;
     }
@@ -74,7 +83,7 @@ __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint8_
         const uint32_t lo = ru > rv ? rv : ru;
         const uint32_t old = atomicCAS(&parent[hi], hi, lo);
         if (old == hi) {                            // hooked: hi is no longer a root
-            if (MARK) mark[hi] = 1;
+            if (MARK) set_mark(mark, hi);
             return;
         }
         // hi was hooked meanwhile: continue from its true parent (old < hi, strictly
@@ -105,7 +114,7 @@ constexpr int kEdgesPerThread = 4;
 template <typename IdT, bool AOS, bool MARK>
 __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a, const IdT* __restrict__ b,
                                                        uint64_t n, uint32_t* __restrict__ parent,
-                                                       uint8_t* __restrict__ mark, RangeCheck rc) {
+                                                       uint32_t* __restrict__ mark, RangeCheck rc) {
     const uint64_t groups = (n + kEdgesPerThread - 1) / kEdgesPerThread;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += stride) {
@@ -150,7 +159,7 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
 // every v in other (DisjointSet.java:127-131 iterates other.getMatches()).
 template <bool MARK>
 __global__ __launch_bounds__(256) void k_merge_dense(const uint32_t* __restrict__ other, uint32_t n_other,
-                                                     uint32_t* __restrict__ parent, uint8_t* __restrict__ mark) {
+                                                     uint32_t* __restrict__ parent, uint32_t* __restrict__ mark) {
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n_other; v += stride) {
         const uint32_t p = other[v];
@@ -333,27 +342,19 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_scatter(const uint32_t* _
     }
 }
 
-// Partial-summary export: (v, parent[v]) for every marked v, mark cleared. Unordered append
-// with one atomic per wave (ballot + mbcnt).
-__global__ __launch_bounds__(256) void k_export_marks(uint8_t* __restrict__ mark, const uint32_t* __restrict__ parent,
+// Partial-summary export: (v, parent[v]) for every marked v (bitmap, 32 vertices per word),
+// marks cleared. Unordered append with one atomic per wave (prefix sum over the wave). Each word
+// is owned by one thread, so its plain clear cannot race with another workgroup's store.
+__global__ __launch_bounds__(256) void k_export_marks(uint32_t* __restrict__ mark, const uint32_t* __restrict__ parent,
                                                       uint32_t n, uint32_t* __restrict__ pairs, uint64_t cap,
                                                       unsigned long long* __restrict__ counter) {
-    const uint32_t stride = gridDim.x * blockDim.x * 16;
+    const uint32_t nwords = (n + 31) >> 5;
+    const uint32_t stride = gridDim.x * blockDim.x;
     const int lane = threadIdx.x & 63;
-    for (uint32_t base0 = blockIdx.x * blockDim.x * 16; base0 < n; base0 += stride) {
-        const uint32_t base = base0 + threadIdx.x * 16;
-        uint8_t m[16];
-        if (base + 16 <= n) {
-            const uint4 q = *reinterpret_cast<const uint4*>(mark + base);
-            *reinterpret_cast<uint4*>(m) = q;
-        } else {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) m[k] = (base + k < n) ? mark[base + k] : 0;
-        }
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) cnt += (m[k] != 0);
-        // wave-aggregated reservation
+    for (uint32_t w0 = blockIdx.x * blockDim.x; w0 < nwords; w0 += stride) {
+        const uint32_t w = w0 + threadIdx.x;
+        uint32_t m = (w < nwords) ? mark[w] : 0u;
+        const uint32_t cnt = __popc(m);
         unsigned long long incl = cnt;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
@@ -366,17 +367,20 @@ __global__ __launch_bounds__(256) void k_export_marks(uint8_t* __restrict__ mark
         wbase = __shfl(wbase, 0, 64);
         if (cnt == 0) continue;
         unsigned long long pos = wbase + incl - cnt;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            if (!m[k]) continue;
-            const uint32_t v = base + k;
-            if (pos < cap) {                      // overflowing marks stay for the next export
+        uint32_t keep = 0;
+        while (m) {
+            const int b = __ffs(m) - 1;
+            m &= m - 1;
+            const uint32_t v = (w << 5) + b;
+            if (pos < cap) {
                 pairs[2 * pos] = v;
                 pairs[2 * pos + 1] = parent[v];
-                mark[v] = 0;
+            } else {
+                keep |= 1u << b;                // overflowing marks stay for the next export
             }
             ++pos;
         }
+        mark[w] = keep;
     }
 }
 

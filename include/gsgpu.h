@@ -75,7 +75,10 @@ typedef struct gs_cc_config {
 int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg);
 int gs_cc_destroy(gs_cc_t* h);
 int gs_cc_reset(gs_cc_t* h);                        /* back to an empty DisjointSet          */
-int gs_cc_set_stream(gs_cc_t* h, void* hip_stream); /* NULL = the handle's own stream        */
+/* Orders all later work of the handle on hip_stream (NULL = the HIP null stream). A new handle
+ * runs on a non-blocking stream of its own; set the caller's stream before folding device buffers
+ * the caller produced on it. */
+int gs_cc_set_stream(gs_cc_t* h, void* hip_stream);
 int gs_cc_get_stream(gs_cc_t* h, void** hip_stream);
 int gs_cc_sync(gs_cc_t* h);                         /* wait for the handle's stream; reports
                                                        deferred device errors (GS_ERR_RANGE) */
@@ -114,8 +117,8 @@ int gs_cc_labels_device(gs_cc_t* h, const void** dev_ptr);
 
 /* ---- partial-summary exchange (windowAll / tree merge) ----
  * Requires GS_CC_TRACK_MARKS. Writes the (vertex, parent) pairs (uint32, interleaved) of every
- * vertex whose root status changed in this handle since the last export / close_window, and
- * clears those marks. Folding these pairs into another summary (gs_cc_fold_pairs, 32-bit ids
+ * vertex whose root status changed in this handle since the last export (roots it hooked,
+ * singletons made by self-loops), and clears those marks. Folding these pairs into another summary (gs_cc_fold_pairs, 32-bit ids
  * regardless of id_bits via gs_cc_fold_pairs32) transfers all connectivity this handle gained. */
 int gs_cc_export_marks(gs_cc_t* h, void* pairs, uint64_t cap, uint64_t* n_out);
 int gs_cc_fold_pairs32(gs_cc_t* h, const void* pairs, uint64_t n);
