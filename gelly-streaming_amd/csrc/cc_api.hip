@@ -2,6 +2,7 @@
 // Host-side orchestration of one DisjointSet summary per handle: staging of host buffers,
 // kernel launches on the handle's stream, deferred device error reporting, instrumentation.
 #include <cstring>
+#include <type_traits>
 #include <mutex>
 #include <vector>
 
@@ -53,7 +54,8 @@ struct gs_cc {
     hipStream_t own = nullptr, stream = nullptr;
     uint32_t* parent = nullptr;          // dense summary / label array
     uint32_t* mark = nullptr;            // export mark bitmap, 1 bit per vertex (GS_CC_TRACK_MARKS)
-    uint32_t* derr = nullptr;            // deferred device error flags
+    uint32_t* gbits = nullptr;           // giant-component filter bitmap (1 bit per vertex)
+    uint32_t* derr = nullptr;            // deferred device error flags; derr[1] = giant root
     unsigned long long* dscratch = nullptr;  // reduction outputs (8 words)
     unsigned long long* hscratch = nullptr;  // pinned mirror
     void* stage = nullptr;               // host->device staging (2 * staging_edges ids)
@@ -135,14 +137,16 @@ int sync_and_check(gs_cc_t* h) {
 template <typename IdT, bool AOS>
 void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n) {
     const unsigned grid = grid_for((n + kEdgesPerThread - 1) / kEdgesPerThread, kFoldThreads, 16384);
-    RangeCheck rc{h->cap, h->derr};
+    FoldArgs f{n, h->parent, h->mark, h->gbits, h->derr + 1, RangeCheck{h->cap, h->derr}};
+    const bool vec = std::is_same<IdT, uint32_t>::value && !AOS &&
+                     ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
     KTimer t(h, GS_K_FOLD);
-    if (h->mark)
-        hipLaunchKernelGGL((k_fold<IdT, AOS, true>), dim3(grid), dim3(kFoldThreads), 0, h->stream,
-                           (const IdT*)a, (const IdT*)b, n, h->parent, h->mark, rc);
-    else
-        hipLaunchKernelGGL((k_fold<IdT, AOS, false>), dim3(grid), dim3(kFoldThreads), 0, h->stream,
-                           (const IdT*)a, (const IdT*)b, n, h->parent, h->mark, rc);
+#define GS_LAUNCH_FOLD(MARKV, VECV)                                                                   \
+    hipLaunchKernelGGL((k_fold<IdT, AOS, MARKV, VECV>), dim3(grid), dim3(kFoldThreads), 0, h->stream, \
+                       (const IdT*)a, (const IdT*)b, f)
+    if (h->mark) { if (vec) GS_LAUNCH_FOLD(true, true); else GS_LAUNCH_FOLD(true, false); }
+    else { if (vec) GS_LAUNCH_FOLD(false, true); else GS_LAUNCH_FOLD(false, false); }
+#undef GS_LAUNCH_FOLD
 }
 
 int fold_impl(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, uint32_t id_bits) {
@@ -183,8 +187,9 @@ int compress_impl(gs_cc_t* h) {
     if (h->compressed) return GS_OK;
     {
         KTimer t(h, GS_K_COMPRESS);
-        hipLaunchKernelGGL(k_compress, dim3(grid_for((h->cap + 3) / 4, 256, 16384)), dim3(256), 0, h->stream,
-                           h->parent, h->cap);
+        hipLaunchKernelGGL(k_pick_giant, dim3(1), dim3(256), 0, h->stream, h->parent, h->cap, h->derr + 1);
+        hipLaunchKernelGGL(k_compress, dim3(grid_for(h->cap, 1024, 16384)), dim3(256), 0, h->stream,
+                           h->parent, h->cap, h->gbits, h->derr + 1);
     }
     GS_HIP(hipGetLastError());
     h->compressed = true;
@@ -245,13 +250,13 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
     if (cfg->flags & GS_CC_TRACK_MARKS) {
         if (hipMalloc(&h->mark, mark_bytes(h->cap)) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "mark allocation failed")); }
     }
-    if (hipMalloc(&h->derr, 64) != hipSuccess || hipMalloc(&h->dscratch, 8 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc(&h->gbits, mark_bytes(h->cap)) != hipSuccess || hipMalloc(&h->derr, 64) != hipSuccess || hipMalloc(&h->dscratch, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&h->hscratch, 8 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         return bail(fail(GS_ERR_NOMEM, "scratch allocation failed"));
     }
     std::memset(h->hscratch, 0, 8 * sizeof(unsigned long long));
-    if (hipMemsetAsync(h->derr, 0, 64, h->stream) != hipSuccess) return bail(fail(GS_ERR_HIP, "memset failed"));
+    if (hipMemsetAsync(h->derr, 0, 4, h->stream) != hipSuccess) return bail(fail(GS_ERR_HIP, "memset failed"));
     int rc = gs_cc_reset(h);
     if (rc != GS_OK) return bail(rc);
     if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(fail(GS_ERR_HIP, "stream sync failed"));
@@ -269,6 +274,7 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->parent) (void)hipFree(h->parent);
     if (h->mark) (void)hipFree(h->mark);
     if (h->derr) (void)hipFree(h->derr);
+    if (h->gbits) (void)hipFree(h->gbits);
     if (h->dscratch) (void)hipFree(h->dscratch);
     if (h->hscratch) (void)hipHostFree(h->hscratch);
     if (h->stage) (void)hipFree(h->stage);
@@ -283,6 +289,8 @@ int gs_cc_reset(gs_cc_t* h) {
     DeviceGuard g(h->device);
     GS_HIP(hipMemsetAsync(h->parent, 0xFF, (size_t)h->cap * sizeof(uint32_t), h->stream));
     if (h->mark) GS_HIP(hipMemsetAsync(h->mark, 0, mark_bytes(h->cap), h->stream));
+    GS_HIP(hipMemsetAsync(h->gbits, 0, mark_bytes(h->cap), h->stream));
+    GS_HIP(hipMemsetAsync(h->derr + 1, 0xFF, 4, h->stream));       // no giant root yet
     h->compressed = true;
     return GS_OK;
 }

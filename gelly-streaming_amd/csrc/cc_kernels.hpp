@@ -93,6 +93,8 @@ __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32
     }
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 struct RangeCheck {
     uint32_t cap;
     uint32_t* err;
@@ -107,14 +109,29 @@ __device__ __forceinline__ bool id_ok(IdT x, uint32_t cap) {
 constexpr int kFoldThreads = 256;
 constexpr int kEdgesPerThread = 4;
 
-// UpdateCC over a batch. Each thread takes 4 consecutive edges per pass: the 8 endpoint reads
-// are coalesced (nontemporal: the edge stream is read once and must not evict parent[] from
-// L2 / Infinity Cache), the 8 parent[] gathers are issued back to back before any dependent
-// step, then the 4 unions run.
-template <typename IdT, bool AOS, bool MARK>
+// Giant-component filter (Afforest's "skip the largest component", made streaming): after every
+// close_window, gbits[v] = 1 iff v's canonical label == *giant, a root picked by sampling
+// (k_pick_giant). Components only ever merge until reset, so two set bits always mean "already
+// one component" and the edge needs no parent[] access at all. The bitmap is V/8 bytes (8 MiB at
+// 2^26 vertices: L2 / Infinity-Cache resident) where parent[] is V*4 bytes (HBM-bound gathers).
+struct FoldArgs {
+    uint64_t n;
+    uint32_t* parent;
+    uint32_t* mark;
+    const uint32_t* gbits;
+    const uint32_t* giant;
+    RangeCheck rc;
+};
+
+// UpdateCC over a batch. Each thread takes 4 consecutive edges per pass: endpoint reads are
+// coalesced and nontemporal (the edge stream is read once and must not evict parent[] / gbits
+// from L2 / Infinity Cache), 16 B per lane when VEC; the filter and parent[] gathers of the 4
+// edges are issued back to back before any dependent step; then the unions run.
+template <typename IdT, bool AOS, bool MARK, bool VEC>
 __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a, const IdT* __restrict__ b,
-                                                       uint64_t n, uint32_t* __restrict__ parent,
-                                                       uint32_t* __restrict__ mark, RangeCheck rc) {
+                                                       FoldArgs f) {
+    const uint64_t n = f.n;
+    const bool filt = *f.giant != kInvalid;          // wave-uniform
     const uint64_t groups = (n + kEdgesPerThread - 1) / kEdgesPerThread;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += stride) {
@@ -122,36 +139,63 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
         uint32_t u[kEdgesPerThread], v[kEdgesPerThread];
         bool ok[kEdgesPerThread];
         bool bad = false;
+        if (VEC && e0 + kEdgesPerThread <= n) {
+            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a) + g);
+            const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b) + g);
+            u[0] = x.x; u[1] = x.y; u[2] = x.z; u[3] = x.w;
+            v[0] = y.x; v[1] = y.y; v[2] = y.z; v[3] = y.w;
+#pragma unroll
+            for (int k = 0; k < kEdgesPerThread; ++k) {
+                ok[k] = u[k] < f.rc.cap && v[k] < f.rc.cap;
+                bad |= !ok[k];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kEdgesPerThread; ++k) {
+                const uint64_t e = e0 + k;
+                IdT x = 0, y = 0;
+                if (e < n) {
+                    if (AOS) {
+                        x = __builtin_nontemporal_load(&a[2 * e]);
+                        y = __builtin_nontemporal_load(&a[2 * e + 1]);
+                    } else {
+                        x = __builtin_nontemporal_load(&a[e]);
+                        y = __builtin_nontemporal_load(&b[e]);
+                    }
+                }
+                const bool in = e < n;
+                const bool good = in && id_ok<IdT>(x, f.rc.cap) && id_ok<IdT>(y, f.rc.cap);
+                bad |= in && !good;
+                ok[k] = good;
+                u[k] = static_cast<uint32_t>(x);
+                v[k] = static_cast<uint32_t>(y);
+            }
+        }
+        if (bad) atomicOr(f.rc.err, 1u);
 #pragma unroll
         for (int k = 0; k < kEdgesPerThread; ++k) {
-            const uint64_t e = e0 + k;
-            IdT x = 0, y = 0;
-            if (e < n) {
-                if (AOS) {
-                    x = __builtin_nontemporal_load(&a[2 * e]);
-                    y = __builtin_nontemporal_load(&a[2 * e + 1]);
-                } else {
-                    x = __builtin_nontemporal_load(&a[e]);
-                    y = __builtin_nontemporal_load(&b[e]);
-                }
-            }
-            const bool in = e < n;
-            const bool good = in && id_ok<IdT>(x, rc.cap) && id_ok<IdT>(y, rc.cap);
-            bad |= in && !good;
-            ok[k] = good;
-            u[k] = good ? static_cast<uint32_t>(x) : 0u;
-            v[k] = good ? static_cast<uint32_t>(y) : 0u;
+            if (!ok[k]) { u[k] = 0; v[k] = 0; }
         }
-        if (bad) atomicOr(rc.err, 1u);
+        if (filt) {
+            uint32_t wu[kEdgesPerThread], wv[kEdgesPerThread];
+#pragma unroll
+            for (int k = 0; k < kEdgesPerThread; ++k) {
+                wu[k] = f.gbits[u[k] >> 5];
+                wv[k] = f.gbits[v[k] >> 5];
+            }
+#pragma unroll
+            for (int k = 0; k < kEdgesPerThread; ++k)
+                ok[k] = ok[k] && !((wu[k] >> (u[k] & 31)) & (wv[k] >> (v[k] & 31)) & 1u);
+        }
         uint32_t pu[kEdgesPerThread], pv[kEdgesPerThread];
 #pragma unroll
         for (int k = 0; k < kEdgesPerThread; ++k) {
-            pu[k] = ok[k] ? parent[u[k]] : 0u;
-            pv[k] = ok[k] ? parent[v[k]] : 0u;
+            pu[k] = ok[k] ? f.parent[u[k]] : 0u;
+            pv[k] = ok[k] ? f.parent[v[k]] : 0u;
         }
 #pragma unroll
         for (int k = 0; k < kEdgesPerThread; ++k)
-            if (ok[k]) union_edge<MARK>(parent, mark, u[k], v[k], pu[k], pv[k]);
+            if (ok[k]) union_edge<MARK>(f.parent, f.mark, u[k], v[k], pu[k], pv[k]);
     }
 }
 
@@ -168,20 +212,74 @@ __global__ __launch_bounds__(256) void k_merge_dense(const uint32_t* __restrict_
     }
 }
 
-// Merger emission: full compression. Afterwards parent[v] = root(v) = canonical label.
-// Only v's own thread writes parent[v] here, and it walks read-only: a path-halving store
-// from another thread's walk could land after v's thread stored the root and put back an
-// intermediate ancestor (a valid forest, but not the fully compressed emission).
-__global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent, uint32_t n) {
-    const uint32_t stride = gridDim.x * blockDim.x * 4;
-    for (uint32_t base = (blockIdx.x * blockDim.x + threadIdx.x) * 4; base < n; base += stride) {
+// Pick the giant component's root for the filter: labels (read-only root walks) of 1024 sampled
+// vertex ids, counted in an LDS hash table; the most frequent label wins if it holds at least a
+// quarter of the seen samples (else no filter: *giant = kInvalid). One workgroup.
+constexpr int kPickSamples = 1024;
+constexpr int kPickSlots = 2048;
+__global__ __launch_bounds__(256) void k_pick_giant(const uint32_t* __restrict__ parent, uint32_t n,
+                                                    uint32_t* __restrict__ giant) {
+    __shared__ uint32_t keys[kPickSlots];
+    __shared__ uint32_t cnt[kPickSlots];
+    __shared__ unsigned long long best[4];
+    __shared__ uint32_t seen_total;
+    for (int i = threadIdx.x; i < kPickSlots; i += blockDim.x) { keys[i] = kInvalid; cnt[i] = 0; }
+    if (threadIdx.x == 0) seen_total = 0;
+    __syncthreads();
+    uint32_t seen = 0;
+    for (int i = threadIdx.x; i < kPickSamples; i += blockDim.x) {
+        const uint32_t pos = (uint32_t)(splitmix64(0x5EED0000ull + i) % n);
+        if (parent[pos] == kInvalid) continue;
+        const uint32_t lab = find_root_ro(parent, pos);
+        ++seen;
+        uint32_t h = (lab * 2654435761u) & (kPickSlots - 1);
+        for (;;) {
+            const uint32_t old = atomicCAS(&keys[h], kInvalid, lab);
+            if (old == kInvalid || old == lab) { atomicAdd(&cnt[h], 1u); break; }
+            h = (h + 1) & (kPickSlots - 1);
+        }
+    }
+    atomicAdd(&seen_total, seen);
+    __syncthreads();
+    unsigned long long mine = 0;                 // (count << 32) | key, max-reduced
+    for (int i = threadIdx.x; i < kPickSlots; i += blockDim.x)
+        if (cnt[i]) {
+            const unsigned long long c = ((unsigned long long)cnt[i] << 32) | keys[i];
+            mine = c > mine ? c : mine;
+        }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_down(mine, off, 64);
+        mine = o > mine ? o : mine;
+    }
+    if ((threadIdx.x & 63) == 0) best[threadIdx.x >> 6] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long b = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) b = best[w] > b ? best[w] : b;
+        const uint32_t c = (uint32_t)(b >> 32);
+        *giant = (c >= 16 && 4 * c >= seen_total) ? (uint32_t)b : kInvalid;
+    }
+}
+
+// Merger emission: full compression. Afterwards parent[v] = root(v) = canonical label, and
+// gbits is rebuilt for the current giant root. Only v's own thread writes parent[v], walking
+// read-only: a path-halving store from another thread's walk could land after v's thread
+// stored the root and put back an intermediate ancestor. A workgroup covers 1024 consecutive
+// vertices (4 KiB of parent[], 128 B of gbits), so every line it stores to is its own.
+__global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent, uint32_t n,
+                                                  uint32_t* __restrict__ gbits, const uint32_t* __restrict__ giant) {
+    const uint32_t g = *giant;
+    const int lane = threadIdx.x & 63;
+    for (uint64_t blk = (uint64_t)blockIdx.x * 1024; blk < n; blk += (uint64_t)gridDim.x * 1024) {
+        const uint32_t base = (uint32_t)blk + threadIdx.x * 4;
         uint32_t p[4];
-        if (base + 4 <= n) {
+        if ((uint64_t)base + 4 <= n) {
             const uint4 q = *reinterpret_cast<const uint4*>(parent + base);
             p[0] = q.x; p[1] = q.y; p[2] = q.z; p[3] = q.w;
         } else {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) p[k] = (base + k < n) ? parent[base + k] : kInvalid;
+            for (int k = 0; k < 4; ++k) p[k] = ((uint64_t)base + k < n) ? parent[base + k] : kInvalid;
         }
         uint32_t gp[4];
 #pragma unroll
@@ -189,12 +287,22 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
             const uint32_t v = base + k;
             gp[k] = (p[k] != kInvalid && p[k] != v) ? parent[p[k]] : p[k];
         }
+        uint32_t nib = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t v = base + k;
-            if (p[k] == kInvalid || p[k] == v || gp[k] == p[k]) continue;   // root / unseen / depth 1
-            parent[v] = find_root_ro(parent, gp[k]);
+            uint32_t lab = p[k];
+            if (p[k] != kInvalid && p[k] != v && gp[k] != p[k]) {   // depth >= 2: walk, store the root
+                lab = find_root_ro(parent, gp[k]);
+                parent[v] = lab;
+            }
+            nib |= (lab == g && lab != kInvalid) ? (1u << k) : 0u;
         }
+        uint32_t word = nib << (4 * (lane & 7));
+        word |= __shfl_xor(word, 1, 64);
+        word |= __shfl_xor(word, 2, 64);
+        word |= __shfl_xor(word, 4, 64);
+        if ((lane & 7) == 0 && base < n) gbits[base >> 5] = word;
     }
 }
 
