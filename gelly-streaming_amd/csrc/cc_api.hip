@@ -1,6 +1,7 @@
 // cc_api.hip — the extern "C" boundary of libgsgpu.so (declared in include/gsgpu.h).
 // Host-side orchestration of one DisjointSet summary per handle: staging of host buffers,
 // kernel launches on the handle's stream, deferred device error reporting, instrumentation.
+#include <algorithm>
 #include <cstring>
 #include <type_traits>
 #include <mutex>
@@ -63,6 +64,7 @@ struct gs_cc {
     void* tmp = nullptr;                 // emission temporaries
     size_t tmp_bytes = 0;
     bool compressed = true;
+    uint64_t edges_since_reset = 0;      // drives the young-forest launch split (fold_impl)
     // instrumentation
     bool timing = false;
     struct Pend { int k; hipEvent_t a, b; };
@@ -149,6 +151,42 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n) {
 #undef GS_LAUNCH_FOLD
 }
 
+// Young-forest launch split: while fewer than capacity/4 edges have been folded since reset,
+// the forest is being built (most edges hook) and concurrent hooks on the same few roots
+// (RMAT hubs) serialise on failed CAS retries; launches of at most kYoungChunk edges cut the
+// edges in flight and let later edges see earlier unions (RMAT-26 window 1: 6.4 -> 2.0 ms,
+// tools/exp_chunks.py). Once mature, a batch is one launch (steady windows are filter-bound).
+constexpr uint64_t kYoungChunk = 1ull << 18;
+
+template <typename IdT, bool AOS>
+void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, size_t esz) {
+    const uint64_t young_limit = h->cap / 4;
+    uint64_t off = 0;
+    while (off < n) {
+        uint64_t m = n - off;
+        if (h->edges_since_reset < young_limit) {
+            const uint64_t left = young_limit - h->edges_since_reset;
+            m = std::min(m, std::max<uint64_t>(std::min(kYoungChunk, left), 1));
+        }
+        const size_t stride = AOS ? 2 * esz : esz;
+        launch_fold<IdT, AOS>(h, a + off * stride, b ? b + off * esz : nullptr, m);
+        h->edges_since_reset += m;
+        off += m;
+    }
+}
+
+void launch_fold_any(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, uint32_t id_bits) {
+    const char* ca = static_cast<const char*>(a);
+    const char* cb = static_cast<const char*>(b);
+    if (id_bits == 32) {
+        if (aos) launch_fold_split<uint32_t, true>(h, ca, nullptr, n, 4);
+        else launch_fold_split<uint32_t, false>(h, ca, cb, n, 4);
+    } else {
+        if (aos) launch_fold_split<int64_t, true>(h, ca, nullptr, n, 8);
+        else launch_fold_split<int64_t, false>(h, ca, cb, n, 8);
+    }
+}
+
 int fold_impl(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, uint32_t id_bits) {
     GS_TRY(check(h));
     if (n == 0) return GS_OK;
@@ -158,8 +196,7 @@ int fold_impl(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, ui
     const bool dev = is_device_pointer(a) && (aos || is_device_pointer(b));
     h->compressed = false;
     if (dev) {
-        if (id_bits == 32) { if (aos) launch_fold<uint32_t, true>(h, a, b, n); else launch_fold<uint32_t, false>(h, a, b, n); }
-        else { if (aos) launch_fold<int64_t, true>(h, a, b, n); else launch_fold<int64_t, false>(h, a, b, n); }
+        launch_fold_any(h, a, b, n, aos, id_bits);
         GS_HIP(hipGetLastError());
         return GS_OK;
     }
@@ -176,8 +213,7 @@ int fold_impl(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, ui
             GS_HIP(hipMemcpyAsync(s0, static_cast<const char*>(a) + off * esz, m * esz, hipMemcpyHostToDevice, h->stream));
             GS_HIP(hipMemcpyAsync(s1, static_cast<const char*>(b) + off * esz, m * esz, hipMemcpyHostToDevice, h->stream));
         }
-        if (id_bits == 32) { if (aos) launch_fold<uint32_t, true>(h, s0, s1, m); else launch_fold<uint32_t, false>(h, s0, s1, m); }
-        else { if (aos) launch_fold<int64_t, true>(h, s0, s1, m); else launch_fold<int64_t, false>(h, s0, s1, m); }
+        launch_fold_any(h, s0, s1, m, aos, id_bits);
         GS_HIP(hipGetLastError());
     }
     return GS_OK;
@@ -292,6 +328,7 @@ int gs_cc_reset(gs_cc_t* h) {
     GS_HIP(hipMemsetAsync(h->gbits, 0, mark_bytes(h->cap), h->stream));
     GS_HIP(hipMemsetAsync(h->derr + 1, 0xFF, 4, h->stream));       // no giant root yet
     h->compressed = true;
+    h->edges_since_reset = 0;
     return GS_OK;
 }
 

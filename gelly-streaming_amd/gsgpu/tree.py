@@ -81,7 +81,7 @@ class TreeMerge:
                     dist.recv(self.buf[: 2 * n], self._grank(peer), group=self.group)
                     self.summary.fold_pairs(self.buf, n, id_bits=32)
                 self.bytes_recv += 8 * n
-        if self.rank == 0:
-            self.summary.close_window()
-            return True
-        return False
+        # every rank closes its window: rank 0's close is the Merger's emission; on the other
+        # ranks it keeps their own giant-component filter current for their next fold
+        self.summary.close_window()
+        return self.rank == 0
