@@ -1,0 +1,70 @@
+"""Fold rocprofv3 --pmc CSVs (tools/pmc_traffic.sh) into per-window HBM traffic of k_fold.
+
+Correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE
+reports half the bytes of wide (16 B/lane) coalesced streaming reads, so the streaming edge read
+is doubled; the random 4-B gathers of this kernel are an uncalibrated width, reported raw beside.
+Output: profiles/fold_traffic.json-shaped dict (bench.py reads hbm_bytes_per_window from it).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def load(passdir):
+    files = glob.glob(os.path.join(passdir, "**", "*counter_collection.csv"), recursive=True)
+    vals = defaultdict(lambda: defaultdict(float))    # kernel -> counter -> sum over dispatches
+    calls = defaultdict(set)
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            vals[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            calls[k].add(r.get("Dispatch_Id", r.get("Correlation_Id")))
+    return vals, calls
+
+
+def main():
+    root = sys.argv[1]
+    agg = defaultdict(dict)
+    ncalls = {}
+    for p in sorted(glob.glob(os.path.join(root, "p*"))):
+        if not os.path.isdir(p):
+            continue
+        v, c = load(p)
+        for k in v:
+            agg[k].update(v[k])
+            ncalls[k] = len(c[k])
+    comp = [k for k in agg if "k_compress" in k]
+    windows = ncalls[comp[0]] if comp else 1
+    fold = [k for k in agg if "k_fold" in k]
+    out = {"windows": windows, "kernels": {}}
+    for k in agg:
+        out["kernels"][k] = dict(agg[k], dispatches=ncalls.get(k))
+    fetch = sum(agg[k].get("FETCH_SIZE", 0.0) for k in fold) * 1024
+    write = sum(agg[k].get("WRITE_SIZE", 0.0) for k in fold) * 1024
+    hit = sum(agg[k].get("TCC_HIT_sum", 0.0) for k in fold)
+    miss = sum(agg[k].get("TCC_MISS_sum", 0.0) for k in fold)
+    out["fold"] = {
+        "fetch_bytes_raw_per_window": fetch / windows,
+        "write_bytes_per_window": write / windows,
+        "l2_hit_rate": hit / (hit + miss) if hit + miss else None,
+        "atomic_requests_per_window": sum(agg[k].get("TCC_EA0_ATOMIC_sum", 0.0) for k in fold) / windows,
+    }
+    try:
+        b = json.load(open(os.path.join(root, "..", "bench.json")))
+        out["window_edges"] = b["config"]["window_edges_per_gpu"]
+        out["scale"] = b["config"]["scale"]
+    except Exception:
+        pass
+    # streaming edge read (8 B/edge, 16 B/lane loads) is under-reported 2x: add it back once
+    edge_bytes = 8 * out.get("window_edges", 0)
+    out["hbm_bytes_per_window"] = out["fold"]["fetch_bytes_raw_per_window"] + edge_bytes / 2 + out["fold"]["write_bytes_per_window"]
+    out["note"] = ("hbm_bytes_per_window = FETCH_SIZE*1024 + half the 8 B/edge stream (gfx950 reports wide "
+                   "streaming reads at 1/2) + WRITE_SIZE*1024, per window fold; gathers uncalibrated")
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
