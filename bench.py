@@ -48,7 +48,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-windows", type=int, default=2,
                     help="cpu_baseline sample: this many windows of the same stream")
-    ap.add_argument("--verify", action="store_true", help="check final labels with an independent torch CC")
+    ap.add_argument("--verify", action="store_true", help="check final labels with an independent torch CC "
+                    "(multi-rank: rank 0 regenerates the whole global stream; small scales only)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (production); gloo = host-staged, for testing the "
+                         "multi-rank path with several ranks on one GPU")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "fold_traffic.json"),
                     help="PMC-derived HBM bytes per fold launch (written by profiles/pmc_traffic.py)")
     return ap.parse_args()
@@ -59,10 +63,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1)          # more ranks than GPUs only in the gloo test mode
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     if a.gpus != world and rank == 0:
         print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (a.gpus, world), file=sys.stderr)
 
@@ -125,8 +134,14 @@ def main():
         elapsed = float(t.item())
 
     verify = None
-    if a.verify and rank == 0 and world == 1:
-        verify = verify_labels(ds, src, dst, V)
+    if a.verify and rank == 0:
+        if world == 1:
+            verify = verify_labels(ds, src, dst, V)
+        else:                                   # the union of every rank's slices
+            gs = torch.empty(E_rank * world, dtype=torch.int32, device=dev)
+            gd = torch.empty(E_rank * world, dtype=torch.int32, device=dev)
+            gen.rmat(gs, gd, 0, a.scale, a.seed)
+            verify = verify_labels(ds, gs, gd, V)
 
     if rank == 0:
         total_edges = a.steps * E_rank * world
@@ -200,6 +215,30 @@ def _pow2(x: int) -> str:
     return str(x)
 
 
+def torch_min_labels(src, dst, V):
+    """Independent min-label CC with torch ops (hook labels to the min, pointer-jump to the fixpoint)."""
+    lab = torch.arange(V, dtype=torch.int64, device=src.device)
+    s, d = src.long(), dst.long()
+    while True:
+        ls, ld = lab[s], lab[d]
+        m = torch.minimum(ls, ld)
+        new = lab.clone()
+        new.scatter_reduce_(0, ls, m, reduce="amin")
+        new.scatter_reduce_(0, ld, m, reduce="amin")
+        while True:
+            j = new[new]
+            if torch.equal(j, new):
+                break
+            new = j
+        if torch.equal(new, lab):
+            break
+        lab = new
+    seen = torch.zeros(V, dtype=torch.bool, device=src.device)
+    seen[s] = True
+    seen[d] = True
+    return torch.where(seen, lab, torch.full_like(lab, -1))
+
+
 def verify_labels(ds, src, dst, V):
     lab = torch.empty(V, dtype=torch.int32, device=src.device)
     ds.dense(out=lab)
@@ -209,7 +248,8 @@ def verify_labels(ds, src, dst, V):
     seen = lab >= 0
     v = torch.arange(V, device=src.device)
     ok_min = bool((lab[seen] <= v[seen]).all()) and bool((lab[lab[seen]] == lab[seen]).all())
-    return {"edges_consistent": ok_edges, "labels_minimal_idempotent": ok_min}
+    ok_exact = bool(torch.equal(lab, torch_min_labels(src, dst, V)))
+    return {"edges_consistent": ok_edges, "labels_minimal_idempotent": ok_min, "equals_torch_cc": ok_exact}
 
 
 def cpu_baseline(a, src, dst, W):

@@ -55,30 +55,56 @@ class TreeMerge:
         needs_buf = any(r != "idle" for r, _ in self.schedule)
         self.buf = torch.empty(2 * self.cap if needs_buf else 2, dtype=torch.int32, device=device)
         self.cnt = torch.zeros(1, dtype=torch.int64, device=device)
+        # gloo moves host tensors only: stage device buffers through pinned host copies (tests
+        # of the multi-rank path on one GPU); nccl (RCCL) sends device memory directly
+        self.stage = (dist.get_backend(group) == "gloo" and torch.device(device).type == "cuda")
+        if self.stage:
+            self.hbuf = torch.empty(self.buf.numel(), dtype=torch.int32).pin_memory()
+            self.hcnt = torch.zeros(1, dtype=torch.int64)
         self.bytes_sent = 0
         self.bytes_recv = 0
 
     def _grank(self, r: int) -> int:
         return r if self.group is None else dist.get_global_rank(self.group, r)
 
+    def _send(self, n: int, dst: int) -> None:
+        if self.stage:
+            self.hcnt.fill_(n)
+            dist.send(self.hcnt, dst, group=self.group)
+            if n:
+                self.hbuf[: 2 * n].copy_(self.buf[: 2 * n])
+                dist.send(self.hbuf[: 2 * n], dst, group=self.group)
+            return
+        self.cnt.fill_(n)
+        dist.send(self.cnt, dst, group=self.group)
+        if n:
+            dist.send(self.buf[: 2 * n], dst, group=self.group)
+
+    def _recv(self, src: int) -> int:
+        c = self.hcnt if self.stage else self.cnt
+        dist.recv(c, src, group=self.group)
+        n = int(c.item())
+        if n > self.cap:
+            raise RuntimeError("partial summary of %d pairs exceeds capacity %d" % (n, self.cap))
+        if n:
+            if self.stage:
+                dist.recv(self.hbuf[: 2 * n], src, group=self.group)
+                self.buf[: 2 * n].copy_(self.hbuf[: 2 * n])
+            else:
+                dist.recv(self.buf[: 2 * n], src, group=self.group)
+        return n
+
     def merge_window(self) -> bool:
         """Exchange this window's partial summaries; returns True on rank 0 (which emitted)."""
         for role, peer in self.schedule:
             if role == "send":
                 n = self.summary.export_marks(self.buf, self.cap)
-                self.cnt.fill_(n)
-                dist.send(self.cnt, self._grank(peer), group=self.group)
-                if n:
-                    dist.send(self.buf[: 2 * n], self._grank(peer), group=self.group)
+                self._send(n, self._grank(peer))
                 self.bytes_sent += 8 * n
                 break                                   # a sender is done for this window
             if role == "recv":
-                dist.recv(self.cnt, self._grank(peer), group=self.group)
-                n = int(self.cnt.item())
+                n = self._recv(self._grank(peer))
                 if n:
-                    if n > self.cap:
-                        raise RuntimeError("partial summary of %d pairs exceeds capacity %d" % (n, self.cap))
-                    dist.recv(self.buf[: 2 * n], self._grank(peer), group=self.group)
                     self.summary.fold_pairs(self.buf, n, id_bits=32)
                 self.bytes_recv += 8 * n
         # every rank closes its window: rank 0's close is the Merger's emission; on the other

@@ -379,3 +379,18 @@ def test_cc_example_file_input(tmp_path):
     for v, r in last.items():
         comps.setdefault(r, []).append(v)
     assert sorted(", ".join(map(str, sorted(m))) for m in comps.values()) == k["expect_final_components"]
+
+
+# ---------------- bench.py multi-rank path (2 ranks on one GPU, gloo-staged exchange) ----------------
+def test_bench_two_ranks_one_gpu_verified():
+    import subprocess, sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "1", "--warmup", "1", "--scale", "16", "--edge-factor", "16",
+           "--window-log2", "16", "--dist-backend", "gloo", "--verify"]
+    out = subprocess.check_output(cmd, env=env, timeout=240).decode()
+    line = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["verify"] == {"edges_consistent": True, "labels_minimal_idempotent": True, "equals_torch_cc": True}
