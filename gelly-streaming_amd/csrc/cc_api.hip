@@ -56,6 +56,7 @@ struct gs_cc {
     uint32_t* parent = nullptr;          // dense summary / label array
     uint32_t* mark = nullptr;            // export mark bitmap, 1 bit per vertex (GS_CC_TRACK_MARKS)
     uint32_t* gbits = nullptr;           // giant-component filter bitmap (1 bit per vertex)
+    uint32_t* sbits = nullptr;           // seen bitmap (1 bit per vertex), set on first touch
     uint32_t* derr = nullptr;            // deferred device error flags; derr[1] = giant root
     unsigned long long* dscratch = nullptr;  // reduction outputs (8 words)
     unsigned long long* hscratch = nullptr;  // pinned mirror
@@ -139,7 +140,7 @@ int sync_and_check(gs_cc_t* h) {
 template <typename IdT, bool AOS>
 void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n) {
     const unsigned grid = grid_for((n + kEdgesPerThread - 1) / kEdgesPerThread, kFoldThreads, 16384);
-    FoldArgs f{n, h->parent, h->mark, h->gbits, h->derr + 1, RangeCheck{h->cap, h->derr}};
+    FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, h->derr + 1, RangeCheck{h->cap, h->derr}};
     const bool vec = std::is_same<IdT, uint32_t>::value && !AOS &&
                      ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
     KTimer t(h, GS_K_FOLD);
@@ -225,7 +226,7 @@ int compress_impl(gs_cc_t* h) {
         KTimer t(h, GS_K_COMPRESS);
         hipLaunchKernelGGL(k_pick_giant, dim3(1), dim3(256), 0, h->stream, h->parent, h->cap, h->derr + 1);
         hipLaunchKernelGGL(k_compress, dim3(grid_for(h->cap, 1024, 16384)), dim3(256), 0, h->stream,
-                           h->parent, h->cap, h->gbits, h->derr + 1);
+                           h->parent, h->cap, h->gbits, h->sbits, h->derr + 1);
     }
     GS_HIP(hipGetLastError());
     h->compressed = true;
@@ -286,7 +287,8 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
     if (cfg->flags & GS_CC_TRACK_MARKS) {
         if (hipMalloc(&h->mark, mark_bytes(h->cap)) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "mark allocation failed")); }
     }
-    if (hipMalloc(&h->gbits, mark_bytes(h->cap)) != hipSuccess || hipMalloc(&h->derr, 64) != hipSuccess || hipMalloc(&h->dscratch, 8 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc(&h->gbits, mark_bytes(h->cap)) != hipSuccess || hipMalloc(&h->sbits, mark_bytes(h->cap)) != hipSuccess ||
+        hipMalloc(&h->derr, 64) != hipSuccess || hipMalloc(&h->dscratch, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&h->hscratch, 8 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         return bail(fail(GS_ERR_NOMEM, "scratch allocation failed"));
@@ -311,6 +313,7 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->mark) (void)hipFree(h->mark);
     if (h->derr) (void)hipFree(h->derr);
     if (h->gbits) (void)hipFree(h->gbits);
+    if (h->sbits) (void)hipFree(h->sbits);
     if (h->dscratch) (void)hipFree(h->dscratch);
     if (h->hscratch) (void)hipHostFree(h->hscratch);
     if (h->stage) (void)hipFree(h->stage);
@@ -326,7 +329,9 @@ int gs_cc_reset(gs_cc_t* h) {
     GS_HIP(hipMemsetAsync(h->parent, 0xFF, (size_t)h->cap * sizeof(uint32_t), h->stream));
     if (h->mark) GS_HIP(hipMemsetAsync(h->mark, 0, mark_bytes(h->cap), h->stream));
     GS_HIP(hipMemsetAsync(h->gbits, 0, mark_bytes(h->cap), h->stream));
+    GS_HIP(hipMemsetAsync(h->sbits, 0, mark_bytes(h->cap), h->stream));
     GS_HIP(hipMemsetAsync(h->derr + 1, 0xFF, 4, h->stream));       // no giant root yet
+    GS_HIP(hipMemsetAsync(h->derr + 2, 0, 4, h->stream));          // next close: full
     h->compressed = true;
     h->edges_since_reset = 0;
     return GS_OK;
@@ -383,8 +388,8 @@ int gs_cc_merge(gs_cc_t* into, gs_cc_t* from) {
     {
         KTimer t(into, GS_K_MERGE);
         const dim3 grid(grid_for(from->cap, 256, 16384));
-        if (into->mark) hipLaunchKernelGGL(k_merge_dense<true>, grid, dim3(256), 0, into->stream, from->parent, from->cap, into->parent, into->mark);
-        else hipLaunchKernelGGL(k_merge_dense<false>, grid, dim3(256), 0, into->stream, from->parent, from->cap, into->parent, into->mark);
+        if (into->mark) hipLaunchKernelGGL(k_merge_dense<true>, grid, dim3(256), 0, into->stream, from->parent, from->cap, into->parent, into->mark, into->sbits);
+        else hipLaunchKernelGGL(k_merge_dense<false>, grid, dim3(256), 0, into->stream, from->parent, from->cap, into->parent, into->mark, into->sbits);
     }
     GS_HIP(hipGetLastError());
     if (from->stream != into->stream) {   // `from` must not be reused before the merge read it

@@ -54,27 +54,35 @@ __device__ __forceinline__ uint32_t find_root_ro(const uint32_t* __restrict__ pa
     return cur;
 }
 
-// First touch of v (makeSet, DisjointSet.java:53-56): kInvalid -> v. Returns v's parent word.
-__device__ __forceinline__ uint32_t make_set(uint32_t* __restrict__ parent, uint32_t v, uint32_t pv) {
+// First touch of v (makeSet, DisjointSet.java:53-56): kInvalid -> v, and v's bit in the seen
+// bitmap (read by the incremental close). Returns v's parent word.
+__device__ __forceinline__ uint32_t make_set(uint32_t* __restrict__ parent, uint32_t* __restrict__ sbits,
+                                             uint32_t v, uint32_t pv) {
     if (pv != kInvalid) return pv;
     const uint32_t old = atomicCAS(&parent[v], kInvalid, v);
-    return old == kInvalid ? v : old;
+    if (old != kInvalid) return old;
+    set_mark(sbits, v);
+    return v;
 }
 
 // union(u, v) given the parent words read by the caller. MARK: record hooked roots and
 // self-loop first touches in mark[] for the partial-summary export.
 template <bool MARK>
 __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32_t* __restrict__ mark,
+                                           uint32_t* __restrict__ sbits,
                                            uint32_t u, uint32_t v, uint32_t pu, uint32_t pv) {
     if (u == v) {                                   // union(u,u): makeSet only
         if (pu == kInvalid) {
             const uint32_t old = atomicCAS(&parent[u], kInvalid, u);
-            if (MARK && old == kInvalid) set_mark(mark, u);
+            if (old == kInvalid) {
+                set_mark(sbits, u);
+                if (MARK) set_mark(mark, u);
+            }
         }
         return;
     }
-    pu = make_set(parent, u, pu);
-    pv = make_set(parent, v, pv);
+    pu = make_set(parent, sbits, u, pu);
+    pv = make_set(parent, sbits, v, pv);
     if (pu == pv) return;                           // common parent: already one component
     uint32_t ru = find_root(parent, u, pu);
     uint32_t rv = find_root(parent, v, pv);
@@ -118,6 +126,7 @@ struct FoldArgs {
     uint64_t n;
     uint32_t* parent;
     uint32_t* mark;
+    uint32_t* sbits;
     const uint32_t* gbits;
     const uint32_t* giant;
     RangeCheck rc;
@@ -195,7 +204,7 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
         }
 #pragma unroll
         for (int k = 0; k < kEdgesPerThread; ++k)
-            if (ok[k]) union_edge<MARK>(f.parent, f.mark, u[k], v[k], pu[k], pv[k]);
+            if (ok[k]) union_edge<MARK>(f.parent, f.mark, f.sbits, u[k], v[k], pu[k], pv[k]);
     }
 }
 
@@ -203,12 +212,13 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
 // every v in other (DisjointSet.java:127-131 iterates other.getMatches()).
 template <bool MARK>
 __global__ __launch_bounds__(256) void k_merge_dense(const uint32_t* __restrict__ other, uint32_t n_other,
-                                                     uint32_t* __restrict__ parent, uint32_t* __restrict__ mark) {
+                                                     uint32_t* __restrict__ parent, uint32_t* __restrict__ mark,
+                                                     uint32_t* __restrict__ sbits) {
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n_other; v += stride) {
         const uint32_t p = other[v];
         if (p == kInvalid) continue;
-        union_edge<MARK>(parent, mark, v, p, parent[v], parent[p]);
+        union_edge<MARK>(parent, mark, sbits, v, p, parent[v], parent[p]);
     }
 }
 
@@ -217,6 +227,9 @@ __global__ __launch_bounds__(256) void k_merge_dense(const uint32_t* __restrict_
 // quarter of the seen samples (else no filter: *giant = kInvalid). One workgroup.
 constexpr int kPickSamples = 1024;
 constexpr int kPickSlots = 2048;
+// state[0] = giant root (kInvalid: none), state[1] = 1 iff the next close may be incremental:
+// the picked root equals the root the last close built gbits for (so it was not hooked: roots
+// only ever become non-roots, and the pick returns roots).
 __global__ __launch_bounds__(256) void k_pick_giant(const uint32_t* __restrict__ parent, uint32_t n,
                                                     uint32_t* __restrict__ giant) {
     __shared__ uint32_t keys[kPickSlots];
@@ -258,7 +271,9 @@ __global__ __launch_bounds__(256) void k_pick_giant(const uint32_t* __restrict__
         unsigned long long b = 0;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) b = best[w] > b ? best[w] : b;
         const uint32_t c = (uint32_t)(b >> 32);
-        *giant = (c >= 16 && 4 * c >= seen_total) ? (uint32_t)b : kInvalid;
+        const uint32_t g = (c >= 16 && 4 * c >= seen_total) ? (uint32_t)b : kInvalid;
+        giant[1] = (g != kInvalid && g == giant[0]) ? 1u : 0u;
+        giant[0] = g;
     }
 }
 
@@ -267,11 +282,45 @@ __global__ __launch_bounds__(256) void k_pick_giant(const uint32_t* __restrict__
 // read-only: a path-halving store from another thread's walk could land after v's thread
 // stored the root and put back an intermediate ancestor. A workgroup covers 1024 consecutive
 // vertices (4 KiB of parent[], 128 B of gbits), so every line it stores to is its own.
+//
+// Incremental mode (state[1] == 1, the giant root g is unchanged since the last close): every
+// vertex with its gbit set is a depth-1 child of g and stays so (g was never hooked, and a walk
+// through g's children never writes), so only seen vertices outside the giant (sbits & ~gbits)
+// are relabelled; the per-window cost drops from a 4-B read per vertex to two bitmap words per
+// 32 vertices plus the stragglers. The 32 vertices of a bitmap word are one thread's, as are
+// their 128 B of parent[].
 __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent, uint32_t n,
-                                                  uint32_t* __restrict__ gbits, const uint32_t* __restrict__ giant) {
-    const uint32_t g = *giant;
+                                                  uint32_t* __restrict__ gbits, const uint32_t* __restrict__ sbits,
+                                                  const uint32_t* __restrict__ giant) {
+    const uint32_t g = giant[0];
+    const bool incremental = giant[1] != 0;
     const int lane = threadIdx.x & 63;
     for (uint64_t blk = (uint64_t)blockIdx.x * 1024; blk < n; blk += (uint64_t)gridDim.x * 1024) {
+        if (incremental) {
+            if (threadIdx.x < 32) {
+                const uint32_t w = (uint32_t)(blk >> 5) + threadIdx.x;
+                if ((uint64_t)w * 32 >= n) continue;
+                uint32_t cand = sbits[w] & ~gbits[w];
+                uint32_t add = 0;
+                while (cand) {
+                    const int b = __ffs(cand) - 1;
+                    cand &= cand - 1;
+                    const uint32_t v = (w << 5) + b;
+                    const uint32_t p = parent[v];
+                    uint32_t lab = p;
+                    if (p != v) {
+                        const uint32_t gp = parent[p];
+                        if (gp != p) {
+                            lab = find_root_ro(parent, gp);
+                            parent[v] = lab;
+                        }
+                    }
+                    add |= (lab == g) ? (1u << b) : 0u;
+                }
+                if (add) gbits[w] |= add;
+            }
+            continue;
+        }
         const uint32_t base = (uint32_t)blk + threadIdx.x * 4;
         uint32_t p[4];
         if ((uint64_t)base + 4 <= n) {
