@@ -2,6 +2,7 @@
 // Host-side orchestration of one DisjointSet summary per handle: staging of host buffers,
 // kernel launches on the handle's stream, deferred device error reporting, instrumentation.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <mutex>
@@ -137,18 +138,29 @@ int sync_and_check(gs_cc_t* h) {
     return GS_OK;
 }
 
+// edges per thread of the fold (4 or 8; GSGPU_FOLD_EPT for experiments, read once)
+static int fold_ept() {
+    static const int ept = [] {
+        const char* e = getenv("GSGPU_FOLD_EPT");
+        return (e && atoi(e) == 8) ? 8 : 4;
+    }();
+    return ept;
+}
+
 template <typename IdT, bool AOS>
 void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n) {
-    const unsigned grid = grid_for((n + kEdgesPerThread - 1) / kEdgesPerThread, kFoldThreads, 16384);
+    const int ept = fold_ept();
+    const unsigned grid = grid_for((n + ept - 1) / ept, kFoldThreads, 16384);
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, h->derr + 1, RangeCheck{h->cap, h->derr}};
     const bool vec = std::is_same<IdT, uint32_t>::value && !AOS &&
                      ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
     KTimer t(h, GS_K_FOLD);
-#define GS_LAUNCH_FOLD(MARKV, VECV)                                                                   \
-    hipLaunchKernelGGL((k_fold<IdT, AOS, MARKV, VECV>), dim3(grid), dim3(kFoldThreads), 0, h->stream, \
+#define GS_LAUNCH_FOLD(MARKV, VECV, EPTV)                                                                    \
+    hipLaunchKernelGGL((k_fold<IdT, AOS, MARKV, VECV, EPTV>), dim3(grid), dim3(kFoldThreads), 0, h->stream, \
                        (const IdT*)a, (const IdT*)b, f)
-    if (h->mark) { if (vec) GS_LAUNCH_FOLD(true, true); else GS_LAUNCH_FOLD(true, false); }
-    else { if (vec) GS_LAUNCH_FOLD(false, true); else GS_LAUNCH_FOLD(false, false); }
+    if (vec && ept == 8) { if (h->mark) GS_LAUNCH_FOLD(true, true, 8); else GS_LAUNCH_FOLD(false, true, 8); }
+    else if (h->mark) { if (vec) GS_LAUNCH_FOLD(true, true, 4); else GS_LAUNCH_FOLD(true, false, 4); }
+    else { if (vec) GS_LAUNCH_FOLD(false, true, 4); else GS_LAUNCH_FOLD(false, false, 4); }
 #undef GS_LAUNCH_FOLD
 }
 
@@ -224,7 +236,7 @@ int compress_impl(gs_cc_t* h) {
     if (h->compressed) return GS_OK;
     {
         KTimer t(h, GS_K_COMPRESS);
-        hipLaunchKernelGGL(k_pick_giant, dim3(1), dim3(256), 0, h->stream, h->parent, h->cap, h->derr + 1);
+        hipLaunchKernelGGL(k_pick_giant, dim3(1), dim3(1024), 0, h->stream, h->parent, h->cap, h->derr + 1);
         hipLaunchKernelGGL(k_compress, dim3(grid_for(h->cap, 1024, 16384)), dim3(256), 0, h->stream,
                            h->parent, h->cap, h->gbits, h->sbits, h->derr + 1);
     }

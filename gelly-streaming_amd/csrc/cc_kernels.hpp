@@ -115,7 +115,7 @@ __device__ __forceinline__ bool id_ok(IdT x, uint32_t cap) {
 }
 
 constexpr int kFoldThreads = 256;
-constexpr int kEdgesPerThread = 4;
+constexpr int kEdgesPerThread = 4;          // default; k_fold takes EPT as a template parameter
 
 // Giant-component filter (Afforest's "skip the largest component", made streaming): after every
 // close_window, gbits[v] = 1 iff v's canonical label == *giant, a root picked by sampling
@@ -136,31 +136,34 @@ struct FoldArgs {
 // coalesced and nontemporal (the edge stream is read once and must not evict parent[] / gbits
 // from L2 / Infinity Cache), 16 B per lane when VEC; the filter and parent[] gathers of the 4
 // edges are issued back to back before any dependent step; then the unions run.
-template <typename IdT, bool AOS, bool MARK, bool VEC>
+template <typename IdT, bool AOS, bool MARK, bool VEC, int EPT = kEdgesPerThread>
 __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a, const IdT* __restrict__ b,
                                                        FoldArgs f) {
     const uint64_t n = f.n;
     const bool filt = *f.giant != kInvalid;          // wave-uniform
-    const uint64_t groups = (n + kEdgesPerThread - 1) / kEdgesPerThread;
+    const uint64_t groups = (n + EPT - 1) / EPT;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += stride) {
-        const uint64_t e0 = g * kEdgesPerThread;
-        uint32_t u[kEdgesPerThread], v[kEdgesPerThread];
-        bool ok[kEdgesPerThread];
+        const uint64_t e0 = g * EPT;
+        uint32_t u[EPT], v[EPT];
+        bool ok[EPT];
         bool bad = false;
-        if (VEC && e0 + kEdgesPerThread <= n) {
-            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a) + g);
-            const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b) + g);
-            u[0] = x.x; u[1] = x.y; u[2] = x.z; u[3] = x.w;
-            v[0] = y.x; v[1] = y.y; v[2] = y.z; v[3] = y.w;
+        if (VEC && e0 + EPT <= n) {
 #pragma unroll
-            for (int k = 0; k < kEdgesPerThread; ++k) {
+            for (int q = 0; q < EPT / 4; ++q) {
+                const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a) + g * (EPT / 4) + q);
+                const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b) + g * (EPT / 4) + q);
+                u[4 * q + 0] = x.x; u[4 * q + 1] = x.y; u[4 * q + 2] = x.z; u[4 * q + 3] = x.w;
+                v[4 * q + 0] = y.x; v[4 * q + 1] = y.y; v[4 * q + 2] = y.z; v[4 * q + 3] = y.w;
+            }
+#pragma unroll
+            for (int k = 0; k < EPT; ++k) {
                 ok[k] = u[k] < f.rc.cap && v[k] < f.rc.cap;
                 bad |= !ok[k];
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < kEdgesPerThread; ++k) {
+            for (int k = 0; k < EPT; ++k) {
                 const uint64_t e = e0 + k;
                 IdT x = 0, y = 0;
                 if (e < n) {
@@ -182,28 +185,28 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
         }
         if (bad) atomicOr(f.rc.err, 1u);
 #pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k) {
+        for (int k = 0; k < EPT; ++k) {
             if (!ok[k]) { u[k] = 0; v[k] = 0; }
         }
         if (filt) {
-            uint32_t wu[kEdgesPerThread], wv[kEdgesPerThread];
+            uint32_t wu[EPT], wv[EPT];
 #pragma unroll
-            for (int k = 0; k < kEdgesPerThread; ++k) {
+            for (int k = 0; k < EPT; ++k) {
                 wu[k] = f.gbits[u[k] >> 5];
                 wv[k] = f.gbits[v[k] >> 5];
             }
 #pragma unroll
-            for (int k = 0; k < kEdgesPerThread; ++k)
+            for (int k = 0; k < EPT; ++k)
                 ok[k] = ok[k] && !((wu[k] >> (u[k] & 31)) & (wv[k] >> (v[k] & 31)) & 1u);
         }
-        uint32_t pu[kEdgesPerThread], pv[kEdgesPerThread];
+        uint32_t pu[EPT], pv[EPT];
 #pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k) {
+        for (int k = 0; k < EPT; ++k) {
             pu[k] = ok[k] ? f.parent[u[k]] : 0u;
             pv[k] = ok[k] ? f.parent[v[k]] : 0u;
         }
 #pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k)
+        for (int k = 0; k < EPT; ++k)
             if (ok[k]) union_edge<MARK>(f.parent, f.mark, f.sbits, u[k], v[k], pu[k], pv[k]);
     }
 }
@@ -230,11 +233,11 @@ constexpr int kPickSlots = 2048;
 // state[0] = giant root (kInvalid: none), state[1] = 1 iff the next close may be incremental:
 // the picked root equals the root the last close built gbits for (so it was not hooked: roots
 // only ever become non-roots, and the pick returns roots).
-__global__ __launch_bounds__(256) void k_pick_giant(const uint32_t* __restrict__ parent, uint32_t n,
+__global__ __launch_bounds__(1024) void k_pick_giant(const uint32_t* __restrict__ parent, uint32_t n,
                                                     uint32_t* __restrict__ giant) {
     __shared__ uint32_t keys[kPickSlots];
     __shared__ uint32_t cnt[kPickSlots];
-    __shared__ unsigned long long best[4];
+    __shared__ unsigned long long best[16];
     __shared__ uint32_t seen_total;
     for (int i = threadIdx.x; i < kPickSlots; i += blockDim.x) { keys[i] = kInvalid; cnt[i] = 0; }
     if (threadIdx.x == 0) seen_total = 0;
@@ -295,32 +298,31 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
     const uint32_t g = giant[0];
     const bool incremental = giant[1] != 0;
     const int lane = threadIdx.x & 63;
-    for (uint64_t blk = (uint64_t)blockIdx.x * 1024; blk < n; blk += (uint64_t)gridDim.x * 1024) {
-        if (incremental) {
-            if (threadIdx.x < 32) {
-                const uint32_t w = (uint32_t)(blk >> 5) + threadIdx.x;
-                if ((uint64_t)w * 32 >= n) continue;
-                uint32_t cand = sbits[w] & ~gbits[w];
-                uint32_t add = 0;
-                while (cand) {
-                    const int b = __ffs(cand) - 1;
-                    cand &= cand - 1;
-                    const uint32_t v = (w << 5) + b;
-                    const uint32_t p = parent[v];
-                    uint32_t lab = p;
-                    if (p != v) {
-                        const uint32_t gp = parent[p];
-                        if (gp != p) {
-                            lab = find_root_ro(parent, gp);
-                            parent[v] = lab;
-                        }
+    if (incremental) {                               // one bitmap word (32 vertices) per thread
+        const uint32_t nwords = (uint32_t)((n + 31) >> 5);
+        for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += gridDim.x * blockDim.x) {
+            uint32_t cand = sbits[w] & ~gbits[w];
+            uint32_t add = 0;
+            while (cand) {
+                const int b = __ffs(cand) - 1;
+                cand &= cand - 1;
+                const uint32_t v = (w << 5) + b;
+                const uint32_t p = parent[v];
+                uint32_t lab = p;
+                if (p != v) {
+                    const uint32_t gp = parent[p];
+                    if (gp != p) {
+                        lab = find_root_ro(parent, gp);
+                        parent[v] = lab;
                     }
-                    add |= (lab == g) ? (1u << b) : 0u;
                 }
-                if (add) gbits[w] |= add;
+                add |= (lab == g) ? (1u << b) : 0u;
             }
-            continue;
+            if (add) gbits[w] |= add;
         }
+        return;
+    }
+    for (uint64_t blk = (uint64_t)blockIdx.x * 1024; blk < n; blk += (uint64_t)gridDim.x * 1024) {
         const uint32_t base = (uint32_t)blk + threadIdx.x * 4;
         uint32_t p[4];
         if ((uint64_t)base + 4 <= n) {
