@@ -67,6 +67,7 @@ struct gs_cc {
     size_t tmp_bytes = 0;
     bool compressed = true;
     uint64_t edges_since_reset = 0;      // drives the young-forest launch split (fold_impl)
+    unsigned long long* dstats = nullptr;    // GSGPU_FOLD_STATS=1: per-window fold counters
     // instrumentation
     bool timing = false;
     struct Pend { int k; hipEvent_t a, b; };
@@ -147,20 +148,30 @@ static int fold_ept() {
     return ept;
 }
 
+static bool fold_stats_on() {
+    static const bool on = [] { const char* e = getenv("GSGPU_FOLD_STATS"); return e && atoi(e) != 0; }();
+    return on;
+}
+
 template <typename IdT, bool AOS>
 void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n) {
     const int ept = fold_ept();
     const unsigned grid = grid_for((n + ept - 1) / ept, kFoldThreads, 16384);
-    FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, h->derr + 1, RangeCheck{h->cap, h->derr}};
+    if (fold_stats_on() && !h->dstats) {
+        (void)hipMalloc(&h->dstats, 8 * sizeof(unsigned long long));
+        (void)hipMemsetAsync(h->dstats, 0, 8 * sizeof(unsigned long long), h->stream);
+    }
+    FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, h->derr + 1, RangeCheck{h->cap, h->derr}, h->dstats};
     const bool vec = std::is_same<IdT, uint32_t>::value && !AOS &&
                      ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
     KTimer t(h, GS_K_FOLD);
-#define GS_LAUNCH_FOLD(MARKV, VECV, EPTV)                                                                    \
-    hipLaunchKernelGGL((k_fold<IdT, AOS, MARKV, VECV, EPTV>), dim3(grid), dim3(kFoldThreads), 0, h->stream, \
+#define GS_LAUNCH_FOLD(MARKV, VECV, EPTV, STV)                                                                    \
+    hipLaunchKernelGGL((k_fold<IdT, AOS, MARKV, VECV, EPTV, STV>), dim3(grid), dim3(kFoldThreads), 0, h->stream, \
                        (const IdT*)a, (const IdT*)b, f)
-    if (vec && ept == 8) { if (h->mark) GS_LAUNCH_FOLD(true, true, 8); else GS_LAUNCH_FOLD(false, true, 8); }
-    else if (h->mark) { if (vec) GS_LAUNCH_FOLD(true, true, 4); else GS_LAUNCH_FOLD(true, false, 4); }
-    else { if (vec) GS_LAUNCH_FOLD(false, true, 4); else GS_LAUNCH_FOLD(false, false, 4); }
+    if (h->dstats) { if (h->mark) GS_LAUNCH_FOLD(true, false, 4, true); else GS_LAUNCH_FOLD(false, false, 4, true); }
+    else if (vec && ept == 8) { if (h->mark) GS_LAUNCH_FOLD(true, true, 8, false); else GS_LAUNCH_FOLD(false, true, 8, false); }
+    else if (h->mark) { if (vec) GS_LAUNCH_FOLD(true, true, 4, false); else GS_LAUNCH_FOLD(true, false, 4, false); }
+    else { if (vec) GS_LAUNCH_FOLD(false, true, 4, false); else GS_LAUNCH_FOLD(false, false, 4, false); }
 #undef GS_LAUNCH_FOLD
 }
 
@@ -232,7 +243,18 @@ int fold_impl(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, ui
     return GS_OK;
 }
 
+void report_fold_stats(gs_cc_t* h) {
+    if (!h->dstats) return;
+    unsigned long long c[8];
+    if (hipMemcpyAsync(c, h->dstats, sizeof(c), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+        hipStreamSynchronize(h->stream) != hipSuccess) return;
+    fprintf(stderr, "[gsgpu fold-stats] valid=%llu unfiltered=%llu early=%llu hooks=%llu casfail=%llu inits=%llu\n",
+            c[0], c[1], c[2], c[3], c[4], c[5]);
+    (void)hipMemsetAsync(h->dstats, 0, sizeof(c), h->stream);
+}
+
 int compress_impl(gs_cc_t* h) {
+    report_fold_stats(h);
     if (h->compressed) return GS_OK;
     {
         KTimer t(h, GS_K_COMPRESS);
@@ -326,6 +348,7 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->derr) (void)hipFree(h->derr);
     if (h->gbits) (void)hipFree(h->gbits);
     if (h->sbits) (void)hipFree(h->sbits);
+    if (h->dstats) (void)hipFree(h->dstats);
     if (h->dscratch) (void)hipFree(h->dscratch);
     if (h->hscratch) (void)hipHostFree(h->hscratch);
     if (h->stage) (void)hipFree(h->stage);

@@ -67,10 +67,16 @@ __device__ __forceinline__ uint32_t make_set(uint32_t* __restrict__ parent, uint
 
 // union(u, v) given the parent words read by the caller. MARK: record hooked roots and
 // self-loop first touches in mark[] for the partial-summary export.
-template <bool MARK>
+// per-thread diagnostic counters (GSGPU_FOLD_STATS=1 builds the STATS variant of k_fold)
+struct FoldStats {
+    uint32_t early = 0, hooks = 0, casfail = 0, inits = 0;
+};
+
+template <bool MARK, bool STATS = false>
 __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32_t* __restrict__ mark,
                                            uint32_t* __restrict__ sbits,
-                                           uint32_t u, uint32_t v, uint32_t pu, uint32_t pv) {
+                                           uint32_t u, uint32_t v, uint32_t pu, uint32_t pv,
+                                           FoldStats* st = nullptr) {
     if (u == v) {                                   // union(u,u): makeSet only
         if (pu == kInvalid) {
             const uint32_t old = atomicCAS(&parent[u], kInvalid, u);
@@ -81,9 +87,13 @@ __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32
         }
         return;
     }
+    if (STATS) st->inits += (pu == kInvalid) + (pv == kInvalid);
     pu = make_set(parent, sbits, u, pu);
     pv = make_set(parent, sbits, v, pv);
-    if (pu == pv) return;                           // common parent: already one component
+    if (pu == pv) {                                 // common parent: already one component
+        if (STATS) ++st->early;
+        return;
+    }
     uint32_t ru = find_root(parent, u, pu);
     uint32_t rv = find_root(parent, v, pv);
     while (ru != rv) {
@@ -92,8 +102,10 @@ __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32
         const uint32_t old = atomicCAS(&parent[hi], hi, lo);
         if (old == hi) {                            // hooked: hi is no longer a root
             if (MARK) set_mark(mark, hi);
+            if (STATS) ++st->hooks;
             return;
         }
+        if (STATS) ++st->casfail;
         // hi was hooked meanwhile: continue from its true parent (old < hi, strictly
         // decreasing, so the loop ends)
         const uint32_t r = find_root(parent, old, parent[old]);
@@ -130,17 +142,19 @@ struct FoldArgs {
     const uint32_t* gbits;
     const uint32_t* giant;
     RangeCheck rc;
+    unsigned long long* stats;   // STATS: [valid, filtered, early, hooks, casfail, inits]
 };
 
 // UpdateCC over a batch. Each thread takes 4 consecutive edges per pass: endpoint reads are
 // coalesced and nontemporal (the edge stream is read once and must not evict parent[] / gbits
 // from L2 / Infinity Cache), 16 B per lane when VEC; the filter and parent[] gathers of the 4
 // edges are issued back to back before any dependent step; then the unions run.
-template <typename IdT, bool AOS, bool MARK, bool VEC, int EPT = kEdgesPerThread>
+template <typename IdT, bool AOS, bool MARK, bool VEC, int EPT = kEdgesPerThread, bool STATS = false>
 __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a, const IdT* __restrict__ b,
                                                        FoldArgs f) {
     const uint64_t n = f.n;
     const bool filt = *f.giant != kInvalid;          // wave-uniform
+    FoldStats st;
     const uint64_t groups = (n + EPT - 1) / EPT;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += stride) {
@@ -188,6 +202,8 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
         for (int k = 0; k < EPT; ++k) {
             if (!ok[k]) { u[k] = 0; v[k] = 0; }
         }
+        uint32_t nvalid = 0, nfilt = 0;
+        if (STATS) for (int k = 0; k < EPT; ++k) nvalid += ok[k];
         if (filt) {
             uint32_t wu[EPT], wv[EPT];
 #pragma unroll
@@ -207,7 +223,18 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
         }
 #pragma unroll
         for (int k = 0; k < EPT; ++k)
-            if (ok[k]) union_edge<MARK>(f.parent, f.mark, f.sbits, u[k], v[k], pu[k], pv[k]);
+            if (ok[k]) union_edge<MARK, STATS>(f.parent, f.mark, f.sbits, u[k], v[k], pu[k], pv[k], &st);
+        if (STATS) {
+            for (int k = 0; k < EPT; ++k) nfilt += ok[k];
+            atomicAdd(&f.stats[0], (unsigned long long)nvalid);
+            atomicAdd(&f.stats[1], (unsigned long long)(nvalid - nfilt));
+        }
+    }
+    if (STATS) {
+        atomicAdd(&f.stats[2], (unsigned long long)st.early);
+        atomicAdd(&f.stats[3], (unsigned long long)st.hooks);
+        atomicAdd(&f.stats[4], (unsigned long long)st.casfail);
+        atomicAdd(&f.stats[5], (unsigned long long)st.inits);
     }
 }
 
