@@ -68,6 +68,9 @@ struct gs_cc {
     bool compressed = true;
     uint64_t edges_since_reset = 0;      // drives the young-forest launch split (fold_impl)
     unsigned long long* dstats = nullptr;    // GSGPU_FOLD_STATS=1: per-window fold counters
+    uint32_t* bins = nullptr;            // XCD-local binning: 2 x kBinClasses x bin_region ids
+    uint64_t bin_region = 0;
+    unsigned long long* bin_counts = nullptr;
     // instrumentation
     bool timing = false;
     struct Pend { int k; hipEvent_t a, b; };
@@ -175,6 +178,52 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n) {
 #undef GS_LAUNCH_FOLD
 }
 
+static bool fold_bin_on() {
+    static const bool on = [] { const char* e = getenv("GSGPU_FOLD_BIN"); return !e || atoi(e) != 0; }();
+    return on;
+}
+
+// Binned fold of n device-resident uint32 SoA edges (n <= region): k_bin then k_fold_binned.
+int launch_fold_binned(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t n) {
+    const uint64_t region = std::max<uint64_t>(std::min<uint64_t>(n, 1ull << 24), 4096);
+    if (h->bin_region < region) {
+        if (h->bins) { GS_HIP(hipFree(h->bins)); h->bins = nullptr; }
+        if (hipMalloc(&h->bins, 2 * kBinClasses * region * sizeof(uint32_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            h->bin_region = 0;
+            return fail(GS_ERR_NOMEM, "bin buffers (%llu edges) allocation failed", (unsigned long long)region);
+        }
+        h->bin_region = region;
+    }
+    if (!h->bin_counts) {
+        if (hipMalloc(&h->bin_counts, kBinClasses * sizeof(unsigned long long)) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(GS_ERR_NOMEM, "bin counts allocation failed");
+        }
+    }
+    const uint64_t words = ((uint64_t)h->cap + 31) / 32;
+    BinArgs bn{(uint32_t)(words * 1 / 4 * 32), (uint32_t)(words * 2 / 4 * 32), (uint32_t)(words * 3 / 4 * 32),
+               h->bins, h->bins + kBinClasses * h->bin_region, h->bin_region, h->bin_counts};
+    FoldArgs f{0, h->parent, h->mark, h->sbits, h->gbits, h->derr + 1, RangeCheck{h->cap, h->derr}, h->dstats};
+    for (uint64_t off = 0; off < n; off += h->bin_region) {
+        const uint64_t m = std::min<uint64_t>(n - off, h->bin_region);
+        KTimer t(h, GS_K_FOLD);
+        GS_HIP(hipMemsetAsync(h->bin_counts, 0, kBinClasses * sizeof(unsigned long long), h->stream));
+        hipLaunchKernelGGL(k_bin, dim3(grid_for(m, 1024, 16384)), dim3(256), 0, h->stream, a + off, b + off, m, bn,
+                           RangeCheck{h->cap, h->derr});
+        const unsigned per_group = (unsigned)std::min<uint64_t>(std::max<uint64_t>((m / 8 + 1023) / 1024, 1), 2048);
+        if (h->dstats) {
+            if (h->mark) hipLaunchKernelGGL((k_fold_binned<true, true>), dim3(8 * per_group), dim3(kFoldThreads), 0, h->stream, bn, f);
+            else hipLaunchKernelGGL((k_fold_binned<false, true>), dim3(8 * per_group), dim3(kFoldThreads), 0, h->stream, bn, f);
+        } else {
+            if (h->mark) hipLaunchKernelGGL((k_fold_binned<true, false>), dim3(8 * per_group), dim3(kFoldThreads), 0, h->stream, bn, f);
+            else hipLaunchKernelGGL((k_fold_binned<false, false>), dim3(8 * per_group), dim3(kFoldThreads), 0, h->stream, bn, f);
+        }
+        GS_HIP(hipGetLastError());
+    }
+    return GS_OK;
+}
+
 // Young-forest launch split: while fewer than capacity/4 edges have been folded since reset,
 // the forest is being built (most edges hook) and concurrent hooks on the same few roots
 // (RMAT hubs) serialise on failed CAS retries; launches of at most kYoungChunk edges cut the
@@ -185,6 +234,15 @@ constexpr uint64_t kYoungChunk = 1ull << 18;
 template <typename IdT, bool AOS>
 void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, size_t esz) {
     const uint64_t young_limit = h->cap / 4;
+    // mature forest, large id space, aligned device uint32 SoA: XCD-local binned fold
+    if (std::is_same<IdT, uint32_t>::value && !AOS && fold_bin_on() && h->edges_since_reset >= young_limit &&
+        h->cap >= (1u << 22) && n >= (1u << 20) &&
+        ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0 && is_device_pointer(a)) {
+        if (launch_fold_binned(h, reinterpret_cast<const uint32_t*>(a), reinterpret_cast<const uint32_t*>(b), n) == GS_OK) {
+            h->edges_since_reset += n;
+            return;
+        }
+    }
     uint64_t off = 0;
     while (off < n) {
         uint64_t m = n - off;
@@ -349,6 +407,8 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->gbits) (void)hipFree(h->gbits);
     if (h->sbits) (void)hipFree(h->sbits);
     if (h->dstats) (void)hipFree(h->dstats);
+    if (h->bins) (void)hipFree(h->bins);
+    if (h->bin_counts) (void)hipFree(h->bin_counts);
     if (h->dscratch) (void)hipFree(h->dscratch);
     if (h->hscratch) (void)hipHostFree(h->hscratch);
     if (h->stage) (void)hipFree(h->stage);

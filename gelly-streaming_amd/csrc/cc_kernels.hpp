@@ -145,6 +145,44 @@ struct FoldArgs {
     unsigned long long* stats;   // STATS: [valid, filtered, early, hooks, casfail, inits]
 };
 
+// Filter, parent gathers and unions of one thread's EPT edges (ids already range-checked;
+// ok[k] false = nothing to do for edge k).
+template <bool MARK, bool STATS, int EPT>
+__device__ __forceinline__ void fold_group(const FoldArgs& f, bool filt, uint32_t (&u)[EPT], uint32_t (&v)[EPT],
+                                           bool (&ok)[EPT], FoldStats& st) {
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        if (!ok[k]) { u[k] = 0; v[k] = 0; }
+    }
+    uint32_t nvalid = 0, nfilt = 0;
+    if (STATS) for (int k = 0; k < EPT; ++k) nvalid += ok[k];
+    if (filt) {
+        uint32_t wu[EPT], wv[EPT];
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            wu[k] = f.gbits[u[k] >> 5];
+            wv[k] = f.gbits[v[k] >> 5];
+        }
+#pragma unroll
+        for (int k = 0; k < EPT; ++k)
+            ok[k] = ok[k] && !((wu[k] >> (u[k] & 31)) & (wv[k] >> (v[k] & 31)) & 1u);
+    }
+    uint32_t pu[EPT], pv[EPT];
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        pu[k] = ok[k] ? f.parent[u[k]] : 0u;
+        pv[k] = ok[k] ? f.parent[v[k]] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < EPT; ++k)
+        if (ok[k]) union_edge<MARK, STATS>(f.parent, f.mark, f.sbits, u[k], v[k], pu[k], pv[k], &st);
+    if (STATS) {
+        for (int k = 0; k < EPT; ++k) nfilt += ok[k];
+        atomicAdd(&f.stats[0], (unsigned long long)nvalid);
+        atomicAdd(&f.stats[1], (unsigned long long)(nvalid - nfilt));   // filtered (skipped)
+    }
+}
+
 // UpdateCC over a batch. Each thread takes 4 consecutive edges per pass: endpoint reads are
 // coalesced and nontemporal (the edge stream is read once and must not evict parent[] / gbits
 // from L2 / Infinity Cache), 16 B per lane when VEC; the filter and parent[] gathers of the 4
@@ -198,36 +236,120 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
             }
         }
         if (bad) atomicOr(f.rc.err, 1u);
+        fold_group<MARK, STATS, EPT>(f, filt, u, v, ok, st);
+    }
+    if (STATS) {
+        atomicAdd(&f.stats[2], (unsigned long long)st.early);
+        atomicAdd(&f.stats[3], (unsigned long long)st.hooks);
+        atomicAdd(&f.stats[4], (unsigned long long)st.casfail);
+        atomicAdd(&f.stats[5], (unsigned long long)st.inits);
+    }
+}
+
+// ---- XCD-local binned fold (steady state) ----
+// The filter's two lookups per edge into a V/8-byte bitmap are the steady-state cost; an 8 MiB
+// table is larger than one XCD's 4 MiB L2, so every XCD misses half of them to the Infinity
+// Cache. k_bin sorts a batch into 16 classes (quarter of u x quarter of v, one streaming pass);
+// k_fold_binned gives each XCD (block b runs on XCD b % 8 under round-robin dispatch — a speed
+// assumption only, any placement is correct) two classes whose lookups touch only two bitmap
+// quarters, V/16 bytes: L2-resident (tools/gather_bench.hip: 265 -> ~150 us per 2^24 edges).
+constexpr int kBinClasses = 16;
+__constant__ const uint8_t kGroupClasses[8][2] = {{0, 1}, {4, 5}, {2, 8}, {10, 11}, {14, 15}, {3, 12}, {6, 9}, {7, 13}};
+
+struct BinArgs {
+    uint32_t q1, q2, q3;                // quarter boundaries of the id space (multiples of 32)
+    uint32_t* bsrc;                     // kBinClasses regions of `region` ids each
+    uint32_t* bdst;
+    uint64_t region;
+    unsigned long long* counts;         // kBinClasses edge counts (zeroed before k_bin)
+};
+
+__device__ __forceinline__ uint32_t quarter(uint32_t x, const BinArgs& b) {
+    return (x >= b.q1) + (x >= b.q2) + (x >= b.q3);
+}
+
+__global__ __launch_bounds__(256) void k_bin(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                                             uint64_t n, BinArgs bn, RangeCheck rc) {
+    __shared__ uint32_t hist[kBinClasses];
+    __shared__ unsigned long long base[kBinClasses];
+    for (uint64_t blk = (uint64_t)blockIdx.x * 1024; blk < n; blk += (uint64_t)gridDim.x * 1024) {
+        if (threadIdx.x < kBinClasses) hist[threadIdx.x] = 0;
+        __syncthreads();
+        const uint64_t e0 = blk + threadIdx.x * 4;
+        uint32_t u[4], v[4], c[4], pos[4];
+        bool ok[4];
+        if (e0 + 4 <= n) {
+            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + e0));
+            const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(dst + e0));
+            u[0] = x.x; u[1] = x.y; u[2] = x.z; u[3] = x.w;
+            v[0] = y.x; v[1] = y.y; v[2] = y.z; v[3] = y.w;
 #pragma unroll
-        for (int k = 0; k < EPT; ++k) {
-            if (!ok[k]) { u[k] = 0; v[k] = 0; }
-        }
-        uint32_t nvalid = 0, nfilt = 0;
-        if (STATS) for (int k = 0; k < EPT; ++k) nvalid += ok[k];
-        if (filt) {
-            uint32_t wu[EPT], wv[EPT];
+            for (int k = 0; k < 4; ++k) ok[k] = true;
+        } else {
 #pragma unroll
-            for (int k = 0; k < EPT; ++k) {
-                wu[k] = f.gbits[u[k] >> 5];
-                wv[k] = f.gbits[v[k] >> 5];
+            for (int k = 0; k < 4; ++k) {
+                ok[k] = e0 + k < n;
+                u[k] = ok[k] ? src[e0 + k] : 0u;
+                v[k] = ok[k] ? dst[e0 + k] : 0u;
             }
-#pragma unroll
-            for (int k = 0; k < EPT; ++k)
-                ok[k] = ok[k] && !((wu[k] >> (u[k] & 31)) & (wv[k] >> (v[k] & 31)) & 1u);
         }
-        uint32_t pu[EPT], pv[EPT];
+        bool bad = false;
 #pragma unroll
-        for (int k = 0; k < EPT; ++k) {
-            pu[k] = ok[k] ? f.parent[u[k]] : 0u;
-            pv[k] = ok[k] ? f.parent[v[k]] : 0u;
+        for (int k = 0; k < 4; ++k) {
+            const bool in = ok[k];
+            ok[k] = in && u[k] < rc.cap && v[k] < rc.cap;
+            bad |= in && !ok[k];
+            c[k] = 4 * quarter(u[k], bn) + quarter(v[k], bn);
+            pos[k] = ok[k] ? atomicAdd(&hist[c[k]], 1u) : 0u;
         }
+        if (bad) atomicOr(rc.err, 1u);
+        __syncthreads();
+        if (threadIdx.x < kBinClasses)
+            base[threadIdx.x] = hist[threadIdx.x] ? atomicAdd(&bn.counts[threadIdx.x], (unsigned long long)hist[threadIdx.x]) : 0ull;
+        __syncthreads();
 #pragma unroll
-        for (int k = 0; k < EPT; ++k)
-            if (ok[k]) union_edge<MARK, STATS>(f.parent, f.mark, f.sbits, u[k], v[k], pu[k], pv[k], &st);
-        if (STATS) {
-            for (int k = 0; k < EPT; ++k) nfilt += ok[k];
-            atomicAdd(&f.stats[0], (unsigned long long)nvalid);
-            atomicAdd(&f.stats[1], (unsigned long long)(nvalid - nfilt));
+        for (int k = 0; k < 4; ++k) {
+            if (!ok[k]) continue;
+            const uint64_t at = (uint64_t)c[k] * bn.region + base[c[k]] + pos[k];
+            bn.bsrc[at] = u[k];
+            bn.bdst[at] = v[k];
+        }
+        __syncthreads();
+    }
+}
+
+template <bool MARK, bool STATS>
+__global__ __launch_bounds__(kFoldThreads) void k_fold_binned(BinArgs bn, FoldArgs f) {
+    const bool filt = *f.giant != kInvalid;
+    FoldStats st;
+    const uint32_t group = blockIdx.x & 7;
+    const uint32_t nb = gridDim.x >> 3, bi = blockIdx.x >> 3;
+#pragma unroll 1
+    for (int side = 0; side < 2; ++side) {
+        const uint32_t c = kGroupClasses[group][side];
+        const uint64_t cnt = bn.counts[c];
+        const uint32_t* __restrict__ a = bn.bsrc + (uint64_t)c * bn.region;
+        const uint32_t* __restrict__ b = bn.bdst + (uint64_t)c * bn.region;
+        for (uint64_t g = (uint64_t)bi * blockDim.x + threadIdx.x; g * 4 < cnt; g += (uint64_t)nb * blockDim.x) {
+            uint32_t u[4], v[4];
+            bool ok[4];
+            const uint64_t e0 = g * 4;
+            if (e0 + 4 <= cnt) {
+                const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a + e0));
+                const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b + e0));
+                u[0] = x.x; u[1] = x.y; u[2] = x.z; u[3] = x.w;
+                v[0] = y.x; v[1] = y.y; v[2] = y.z; v[3] = y.w;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) ok[k] = true;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    ok[k] = e0 + k < cnt;
+                    u[k] = ok[k] ? a[e0 + k] : 0u;
+                    v[k] = ok[k] ? b[e0 + k] : 0u;
+                }
+            }
+            fold_group<MARK, STATS, 4>(f, filt, u, v, ok, st);
         }
     }
     if (STATS) {

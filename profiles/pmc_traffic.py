@@ -38,7 +38,7 @@ def main():
             ncalls[k] = len(c[k])
     comp = [k for k in agg if "k_compress" in k]
     windows = ncalls[comp[0]] if comp else 1
-    fold = [k for k in agg if "k_fold" in k]
+    fold = [k for k in agg if "k_fold" in k or k.endswith("k_bin")]
     out = {"windows": windows, "kernels": {}}
     for k in agg:
         out["kernels"][k] = dict(agg[k], dispatches=ncalls.get(k))

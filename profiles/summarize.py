@@ -20,7 +20,7 @@ def main():
         name = r["Kernel_Name"].split("(")[0].replace("void ", "")
         per[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)   # ms
     kern = {k: {"calls": len(v), "total_ms": sum(v), "avg_ms": sum(v) / len(v)} for k, v in per.items()}
-    fold = sum(v["total_ms"] for k, v in kern.items() if "k_fold" in k)
+    fold = sum(v["total_ms"] for k, v in kern.items() if "k_fold" in k or k.endswith("k_bin"))
     comp = [v for k, v in kern.items() if "k_compress" in k]
     windows = comp[0]["calls"] if comp else None           # one compress per window on rank 0
     out = {
