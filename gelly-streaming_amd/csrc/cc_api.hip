@@ -209,7 +209,7 @@ int launch_fold_binned(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_
         const uint64_t m = std::min<uint64_t>(n - off, h->bin_region);
         KTimer t(h, GS_K_FOLD);
         GS_HIP(hipMemsetAsync(h->bin_counts, 0, kBinClasses * sizeof(unsigned long long), h->stream));
-        hipLaunchKernelGGL(k_bin, dim3(grid_for(m, 1024, 16384)), dim3(256), 0, h->stream, a + off, b + off, m, bn,
+        hipLaunchKernelGGL(k_bin, dim3(grid_for(m, kBinTile, 16384)), dim3(256), 0, h->stream, a + off, b + off, m, bn,
                            RangeCheck{h->cap, h->derr});
         const unsigned per_group = (unsigned)std::min<uint64_t>(std::max<uint64_t>((m / 8 + 1023) / 1024, 1), 2048);
         if (h->dstats) {

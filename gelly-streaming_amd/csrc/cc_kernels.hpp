@@ -268,51 +268,86 @@ __device__ __forceinline__ uint32_t quarter(uint32_t x, const BinArgs& b) {
     return (x >= b.q1) + (x >= b.q2) + (x >= b.q3);
 }
 
+// Local counting sort of a 4096-edge tile: each lane holds 16 edges; per edge slot, 16 ballots
+// rank the wave's lanes within each class; wave counts are combined in LDS into class runs; the
+// tile is staged class-major in LDS (32 KiB) and written out as one contiguous run per class
+// (coalesced, whole lines from one workgroup), after one global atomicAdd per class per tile.
+constexpr int kBinTile = 4096;
+constexpr int kBinPerLane = kBinTile / 256;
 __global__ __launch_bounds__(256) void k_bin(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
                                              uint64_t n, BinArgs bn, RangeCheck rc) {
-    __shared__ uint32_t hist[kBinClasses];
-    __shared__ unsigned long long base[kBinClasses];
-    for (uint64_t blk = (uint64_t)blockIdx.x * 1024; blk < n; blk += (uint64_t)gridDim.x * 1024) {
-        if (threadIdx.x < kBinClasses) hist[threadIdx.x] = 0;
-        __syncthreads();
-        const uint64_t e0 = blk + threadIdx.x * 4;
-        uint32_t u[4], v[4], c[4], pos[4];
-        bool ok[4];
-        if (e0 + 4 <= n) {
-            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + e0));
-            const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(dst + e0));
-            u[0] = x.x; u[1] = x.y; u[2] = x.z; u[3] = x.w;
-            v[0] = y.x; v[1] = y.y; v[2] = y.z; v[3] = y.w;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) ok[k] = true;
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                ok[k] = e0 + k < n;
-                u[k] = ok[k] ? src[e0 + k] : 0u;
-                v[k] = ok[k] ? dst[e0 + k] : 0u;
-            }
-        }
+    __shared__ uint32_t st_src[kBinTile];
+    __shared__ uint32_t st_dst[kBinTile];
+    __shared__ uint32_t wcnt[4][kBinClasses];          // per wave, per class
+    __shared__ uint32_t cstart[kBinClasses + 1];        // class runs inside the tile
+    __shared__ unsigned long long gbase[kBinClasses];   // global position of each class run
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint64_t tile = (uint64_t)blockIdx.x * kBinTile; tile < n; tile += (uint64_t)gridDim.x * kBinTile) {
+        // lane l of wave w holds edges tile + w*1024 + k*64 + l, k = 0..15 (coalesced 256 B per k)
+        uint32_t u[kBinPerLane], v[kBinPerLane], c[kBinPerLane], r[kBinPerLane];
         bool bad = false;
+        uint32_t cnt[kBinClasses];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const bool in = ok[k];
-            ok[k] = in && u[k] < rc.cap && v[k] < rc.cap;
-            bad |= in && !ok[k];
-            c[k] = 4 * quarter(u[k], bn) + quarter(v[k], bn);
-            pos[k] = ok[k] ? atomicAdd(&hist[c[k]], 1u) : 0u;
+        for (int q = 0; q < kBinClasses; ++q) cnt[q] = 0;
+#pragma unroll
+        for (int k = 0; k < kBinPerLane; ++k) {
+            const uint64_t e = tile + wid * 1024 + k * 64 + lane;
+            const bool in = e < n;
+            u[k] = in ? __builtin_nontemporal_load(src + e) : 0u;
+            v[k] = in ? __builtin_nontemporal_load(dst + e) : 0u;
+            const bool ok = in && u[k] < rc.cap && v[k] < rc.cap;
+            bad |= in && !ok;
+            c[k] = ok ? 4 * quarter(u[k], bn) + quarter(v[k], bn) : 0xFFu;
         }
         if (bad) atomicOr(rc.err, 1u);
-        __syncthreads();
-        if (threadIdx.x < kBinClasses)
-            base[threadIdx.x] = hist[threadIdx.x] ? atomicAdd(&bn.counts[threadIdx.x], (unsigned long long)hist[threadIdx.x]) : 0ull;
-        __syncthreads();
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (!ok[k]) continue;
-            const uint64_t at = (uint64_t)c[k] * bn.region + base[c[k]] + pos[k];
-            bn.bsrc[at] = u[k];
-            bn.bdst[at] = v[k];
+        for (int k = 0; k < kBinPerLane; ++k) {
+            r[k] = 0;
+#pragma unroll
+            for (int q = 0; q < kBinClasses; ++q) {
+                const unsigned long long m = __ballot(c[k] == (uint32_t)q);
+                if (c[k] == (uint32_t)q) r[k] = cnt[q] + __popcll(m & lt);
+                cnt[q] += __popcll(m);
+            }
+        }
+        if (lane < kBinClasses) {
+            uint32_t mine = 0;
+#pragma unroll
+            for (int q = 0; q < kBinClasses; ++q) mine = (lane == q) ? cnt[q] : mine;
+            wcnt[wid][lane] = mine;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t run = 0;
+            for (int q = 0; q < kBinClasses; ++q) {
+                cstart[q] = run;
+                for (int w = 0; w < 4; ++w) { const uint32_t x = wcnt[w][q]; wcnt[w][q] = run; run += x; }
+            }
+            cstart[kBinClasses] = run;
+        }
+        __syncthreads();
+        if (threadIdx.x < kBinClasses) {
+            const uint32_t len = cstart[threadIdx.x + 1] - cstart[threadIdx.x];
+            gbase[threadIdx.x] = len ? atomicAdd(&bn.counts[threadIdx.x], (unsigned long long)len) : 0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < kBinPerLane; ++k) {
+            if (c[k] == 0xFFu) continue;
+            const uint32_t at = wcnt[wid][c[k]] + r[k];
+            st_src[at] = u[k];
+            st_dst[at] = v[k];
+        }
+        __syncthreads();
+        const uint32_t total = cstart[kBinClasses];
+        for (uint32_t i = threadIdx.x; i < total; i += 256) {
+            uint32_t q = 0;
+#pragma unroll
+            for (int b = 8; b > 0; b >>= 1)
+                if (q + b < kBinClasses && cstart[q + b] <= i) q += b;
+            const uint64_t at = (uint64_t)q * bn.region + gbase[q] + (i - cstart[q]);
+            bn.bsrc[at] = st_src[i];
+            bn.bdst[at] = st_dst[i];
         }
         __syncthreads();
     }
