@@ -185,7 +185,10 @@ static bool fold_bin_on() {
 
 // Binned fold of n device-resident uint32 SoA edges (n <= region): k_bin then k_fold_binned.
 int launch_fold_binned(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t n) {
-    const uint64_t region = std::max<uint64_t>(std::min<uint64_t>(n, 1ull << 24), 4096);
+    // region = ids per class; a lane's sub-region holds every tile of that lane in full
+    const uint64_t chunk = std::max<uint64_t>(std::min<uint64_t>(n, 1ull << 24), kBinTile);
+    const uint64_t tiles_per_lane = (chunk / kBinTile + kBinLanes - 1) / kBinLanes + 1;
+    const uint64_t region = tiles_per_lane * kBinTile * kBinLanes;
     if (h->bin_region < region) {
         if (h->bins) { GS_HIP(hipFree(h->bins)); h->bins = nullptr; }
         if (hipMalloc(&h->bins, 2 * kBinClasses * region * sizeof(uint32_t)) != hipSuccess) {
@@ -196,19 +199,20 @@ int launch_fold_binned(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_
         h->bin_region = region;
     }
     if (!h->bin_counts) {
-        if (hipMalloc(&h->bin_counts, kBinClasses * sizeof(unsigned long long)) != hipSuccess) {
+        if (hipMalloc(&h->bin_counts, kBinClasses * kBinLanes * sizeof(unsigned long long)) != hipSuccess) {
             (void)hipGetLastError();
             return fail(GS_ERR_NOMEM, "bin counts allocation failed");
         }
     }
     const uint64_t words = ((uint64_t)h->cap + 31) / 32;
     BinArgs bn{(uint32_t)(words * 1 / 4 * 32), (uint32_t)(words * 2 / 4 * 32), (uint32_t)(words * 3 / 4 * 32),
-               h->bins, h->bins + kBinClasses * h->bin_region, h->bin_region, h->bin_counts};
+               h->bins, h->bins + kBinClasses * h->bin_region, h->bin_region, h->bin_region / kBinLanes, h->bin_counts};
     FoldArgs f{0, h->parent, h->mark, h->sbits, h->gbits, h->derr + 1, RangeCheck{h->cap, h->derr}, h->dstats};
-    for (uint64_t off = 0; off < n; off += h->bin_region) {
-        const uint64_t m = std::min<uint64_t>(n - off, h->bin_region);
+    const uint64_t step = (h->bin_region / kBinLanes / kBinTile - 1) * kBinLanes * kBinTile;   // edges per k_bin launch
+    for (uint64_t off = 0; off < n; off += step) {
+        const uint64_t m = std::min<uint64_t>(n - off, step);
         KTimer t(h, GS_K_FOLD);
-        GS_HIP(hipMemsetAsync(h->bin_counts, 0, kBinClasses * sizeof(unsigned long long), h->stream));
+        GS_HIP(hipMemsetAsync(h->bin_counts, 0, kBinClasses * kBinLanes * sizeof(unsigned long long), h->stream));
         hipLaunchKernelGGL(k_bin, dim3(grid_for(m, kBinTile, 16384)), dim3(256), 0, h->stream, a + off, b + off, m, bn,
                            RangeCheck{h->cap, h->derr});
         const unsigned per_group = (unsigned)std::min<uint64_t>(std::max<uint64_t>((m / 8 + 1023) / 1024, 1), 2048);

@@ -256,12 +256,17 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
 constexpr int kBinClasses = 16;
 __constant__ const uint8_t kGroupClasses[8][2] = {{0, 1}, {4, 5}, {2, 8}, {10, 11}, {14, 15}, {3, 12}, {6, 9}, {7, 13}};
 
+// Each class region is split into kBinLanes sub-regions; tile t appends to lane t % kBinLanes,
+// so the per-tile run reservations spread over 16 x 64 counters instead of 16 (one memory-side
+// atomic per tile and class; 4096 tiles on 16 words serialised ~50 us).
+constexpr int kBinLanes = 64;
 struct BinArgs {
     uint32_t q1, q2, q3;                // quarter boundaries of the id space (multiples of 32)
-    uint32_t* bsrc;                     // kBinClasses regions of `region` ids each
+    uint32_t* bsrc;                     // kBinClasses x kBinLanes sub-regions of `sub` ids each
     uint32_t* bdst;
-    uint64_t region;
-    unsigned long long* counts;         // kBinClasses edge counts (zeroed before k_bin)
+    uint64_t region;                    // ids per class = kBinLanes * sub
+    uint64_t sub;
+    unsigned long long* counts;         // [kBinClasses][kBinLanes] edge counts (zeroed before k_bin)
 };
 
 __device__ __forceinline__ uint32_t quarter(uint32_t x, const BinArgs& b) {
@@ -318,18 +323,25 @@ __global__ __launch_bounds__(256) void k_bin(const uint32_t* __restrict__ src, c
             wcnt[wid][lane] = mine;
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t run = 0;
-            for (int q = 0; q < kBinClasses; ++q) {
-                cstart[q] = run;
-                for (int w = 0; w < 4; ++w) { const uint32_t x = wcnt[w][q]; wcnt[w][q] = run; run += x; }
+        const uint32_t blane = (uint32_t)((tile / kBinTile) % kBinLanes);
+        if (threadIdx.x < 64) {                          // wave 0: class totals, exclusive scan
+            const int q = threadIdx.x;
+            const uint32_t w0 = q < kBinClasses ? wcnt[0][q] : 0u, w1 = q < kBinClasses ? wcnt[1][q] : 0u;
+            const uint32_t w2 = q < kBinClasses ? wcnt[2][q] : 0u, w3 = q < kBinClasses ? wcnt[3][q] : 0u;
+            const uint32_t len = w0 + w1 + w2 + w3;
+            uint32_t incl = len;
+#pragma unroll
+            for (int off = 1; off < kBinClasses; off <<= 1) {
+                const uint32_t y = __shfl_up(incl, off, 64);
+                if (q >= off) incl += y;
             }
-            cstart[kBinClasses] = run;
-        }
-        __syncthreads();
-        if (threadIdx.x < kBinClasses) {
-            const uint32_t len = cstart[threadIdx.x + 1] - cstart[threadIdx.x];
-            gbase[threadIdx.x] = len ? atomicAdd(&bn.counts[threadIdx.x], (unsigned long long)len) : 0ull;
+            if (q < kBinClasses) {
+                const uint32_t st = incl - len;
+                cstart[q] = st;
+                wcnt[0][q] = st; wcnt[1][q] = st + w0; wcnt[2][q] = st + w0 + w1; wcnt[3][q] = st + w0 + w1 + w2;
+                if (q == kBinClasses - 1) cstart[kBinClasses] = incl;
+                gbase[q] = len ? atomicAdd(&bn.counts[q * kBinLanes + blane], (unsigned long long)len) : 0ull;
+            }
         }
 #pragma unroll
         for (int k = 0; k < kBinPerLane; ++k) {
@@ -345,7 +357,7 @@ __global__ __launch_bounds__(256) void k_bin(const uint32_t* __restrict__ src, c
 #pragma unroll
             for (int b = 8; b > 0; b >>= 1)
                 if (q + b < kBinClasses && cstart[q + b] <= i) q += b;
-            const uint64_t at = (uint64_t)q * bn.region + gbase[q] + (i - cstart[q]);
+            const uint64_t at = (uint64_t)q * bn.region + (uint64_t)blane * bn.sub + gbase[q] + (i - cstart[q]);
             bn.bsrc[at] = st_src[i];
             bn.bdst[at] = st_dst[i];
         }
@@ -360,11 +372,12 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_binned(BinArgs bn, FoldAr
     const uint32_t group = blockIdx.x & 7;
     const uint32_t nb = gridDim.x >> 3, bi = blockIdx.x >> 3;
 #pragma unroll 1
-    for (int side = 0; side < 2; ++side) {
-        const uint32_t c = kGroupClasses[group][side];
-        const uint64_t cnt = bn.counts[c];
-        const uint32_t* __restrict__ a = bn.bsrc + (uint64_t)c * bn.region;
-        const uint32_t* __restrict__ b = bn.bdst + (uint64_t)c * bn.region;
+    for (int seg = 0; seg < 2 * kBinLanes; ++seg) {
+        const uint32_t c = kGroupClasses[group][seg / kBinLanes];
+        const uint32_t l = seg % kBinLanes;
+        const uint64_t cnt = bn.counts[c * kBinLanes + l];
+        const uint32_t* __restrict__ a = bn.bsrc + (uint64_t)c * bn.region + (uint64_t)l * bn.sub;
+        const uint32_t* __restrict__ b = bn.bdst + (uint64_t)c * bn.region + (uint64_t)l * bn.sub;
         for (uint64_t g = (uint64_t)bi * blockDim.x + threadIdx.x; g * 4 < cnt; g += (uint64_t)nb * blockDim.x) {
             uint32_t u[4], v[4];
             bool ok[4];
