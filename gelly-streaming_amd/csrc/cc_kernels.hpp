@@ -287,14 +287,12 @@ __global__ __launch_bounds__(256) void k_bin(const uint32_t* __restrict__ src, c
     __shared__ uint32_t cstart[kBinClasses + 1];        // class runs inside the tile
     __shared__ unsigned long long gbase[kBinClasses];   // global position of each class run
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     for (uint64_t tile = (uint64_t)blockIdx.x * kBinTile; tile < n; tile += (uint64_t)gridDim.x * kBinTile) {
         // lane l of wave w holds edges tile + w*1024 + k*64 + l, k = 0..15 (coalesced 256 B per k)
         uint32_t u[kBinPerLane], v[kBinPerLane], c[kBinPerLane], r[kBinPerLane];
         bool bad = false;
-        uint32_t cnt[kBinClasses];
-#pragma unroll
-        for (int q = 0; q < kBinClasses; ++q) cnt[q] = 0;
+        if (threadIdx.x < 4 * kBinClasses) (&wcnt[0][0])[threadIdx.x] = 0;
+        __syncthreads();
 #pragma unroll
         for (int k = 0; k < kBinPerLane; ++k) {
             const uint64_t e = tile + wid * 1024 + k * 64 + lane;
@@ -307,21 +305,8 @@ __global__ __launch_bounds__(256) void k_bin(const uint32_t* __restrict__ src, c
         }
         if (bad) atomicOr(rc.err, 1u);
 #pragma unroll
-        for (int k = 0; k < kBinPerLane; ++k) {
-            r[k] = 0;
-#pragma unroll
-            for (int q = 0; q < kBinClasses; ++q) {
-                const unsigned long long m = __ballot(c[k] == (uint32_t)q);
-                if (c[k] == (uint32_t)q) r[k] = cnt[q] + __popcll(m & lt);
-                cnt[q] += __popcll(m);
-            }
-        }
-        if (lane < kBinClasses) {
-            uint32_t mine = 0;
-#pragma unroll
-            for (int q = 0; q < kBinClasses; ++q) mine = (lane == q) ? cnt[q] : mine;
-            wcnt[wid][lane] = mine;
-        }
+        for (int k = 0; k < kBinPerLane; ++k)           // rank inside (wave, class): LDS atomics
+            r[k] = (c[k] != 0xFFu) ? atomicAdd(&wcnt[wid][c[k]], 1u) : 0u;
         __syncthreads();
         const uint32_t blane = (uint32_t)((tile / kBinTile) % kBinLanes);
         if (threadIdx.x < 64) {                          // wave 0: class totals, exclusive scan
@@ -367,38 +352,48 @@ __global__ __launch_bounds__(256) void k_bin(const uint32_t* __restrict__ src, c
 
 template <bool MARK, bool STATS>
 __global__ __launch_bounds__(kFoldThreads) void k_fold_binned(BinArgs bn, FoldArgs f) {
+    __shared__ unsigned long long pre[2 * kBinLanes + 1];   // edge prefix over the group's segments
     const bool filt = *f.giant != kInvalid;
     FoldStats st;
     const uint32_t group = blockIdx.x & 7;
     const uint32_t nb = gridDim.x >> 3, bi = blockIdx.x >> 3;
-#pragma unroll 1
-    for (int seg = 0; seg < 2 * kBinLanes; ++seg) {
-        const uint32_t c = kGroupClasses[group][seg / kBinLanes];
-        const uint32_t l = seg % kBinLanes;
-        const uint64_t cnt = bn.counts[c * kBinLanes + l];
-        const uint32_t* __restrict__ a = bn.bsrc + (uint64_t)c * bn.region + (uint64_t)l * bn.sub;
-        const uint32_t* __restrict__ b = bn.bdst + (uint64_t)c * bn.region + (uint64_t)l * bn.sub;
-        for (uint64_t g = (uint64_t)bi * blockDim.x + threadIdx.x; g * 4 < cnt; g += (uint64_t)nb * blockDim.x) {
-            uint32_t u[4], v[4];
-            bool ok[4];
-            const uint64_t e0 = g * 4;
-            if (e0 + 4 <= cnt) {
-                const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a + e0));
-                const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b + e0));
-                u[0] = x.x; u[1] = x.y; u[2] = x.z; u[3] = x.w;
-                v[0] = y.x; v[1] = y.y; v[2] = y.z; v[3] = y.w;
+    if (threadIdx.x < 64) {
+        // segment s = side * kBinLanes + lane; lane t sums segments t and t + 64 in two scans
+        unsigned long long carry = 0;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) ok[k] = true;
-            } else {
+        for (int side = 0; side < 2; ++side) {
+            const uint32_t c = kGroupClasses[group][side];
+            const unsigned long long x = bn.counts[c * kBinLanes + threadIdx.x];
+            unsigned long long incl = x;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    ok[k] = e0 + k < cnt;
-                    u[k] = ok[k] ? a[e0 + k] : 0u;
-                    v[k] = ok[k] ? b[e0 + k] : 0u;
-                }
+            for (int off = 1; off < 64; off <<= 1) {
+                const unsigned long long y = __shfl_up(incl, off, 64);
+                if ((int)threadIdx.x >= off) incl += y;
             }
-            fold_group<MARK, STATS, 4>(f, filt, u, v, ok, st);
+            pre[side * kBinLanes + threadIdx.x] = carry + incl - x;
+            carry += __shfl(incl, 63, 64);
         }
+        if (threadIdx.x == 0) pre[2 * kBinLanes] = carry;
+    }
+    __syncthreads();
+    const unsigned long long total = pre[2 * kBinLanes];
+    for (uint64_t g = (uint64_t)bi * blockDim.x + threadIdx.x; g * 4 < total; g += (uint64_t)nb * blockDim.x) {
+        uint32_t u[4], v[4];
+        bool ok[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const unsigned long long e = g * 4 + k;
+            ok[k] = e < total;
+            uint32_t sidx = 0;                                // last segment with pre <= e
+#pragma unroll
+            for (int b = 64; b > 0; b >>= 1)
+                if (sidx + b < 2 * kBinLanes && pre[sidx + b] <= e) sidx += b;
+            const uint32_t c = kGroupClasses[group][sidx / kBinLanes];
+            const uint64_t at = (uint64_t)c * bn.region + (uint64_t)(sidx % kBinLanes) * bn.sub + (ok[k] ? e - pre[sidx] : 0);
+            u[k] = ok[k] ? __builtin_nontemporal_load(bn.bsrc + at) : 0u;
+            v[k] = ok[k] ? __builtin_nontemporal_load(bn.bdst + at) : 0u;
+        }
+        fold_group<MARK, STATS, 4>(f, filt, u, v, ok, st);
     }
     if (STATS) {
         atomicAdd(&f.stats[2], (unsigned long long)st.early);
