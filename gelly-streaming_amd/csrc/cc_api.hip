@@ -178,8 +178,9 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n) {
 #undef GS_LAUNCH_FOLD
 }
 
+// XCD-local binned fold: off unless GSGPU_FOLD_BIN=1 (experimental)
 static bool fold_bin_on() {
-    static const bool on = [] { const char* e = getenv("GSGPU_FOLD_BIN"); return !e || atoi(e) != 0; }();
+    static const bool on = [] { const char* e = getenv("GSGPU_FOLD_BIN"); return e && atoi(e) != 0; }();
     return on;
 }
 

@@ -328,6 +328,7 @@ __global__ __launch_bounds__(256) void k_bin(const uint32_t* __restrict__ src, c
                 gbase[q] = len ? atomicAdd(&bn.counts[q * kBinLanes + blane], (unsigned long long)len) : 0ull;
             }
         }
+        __syncthreads();                                 // wcnt now holds run starts for every wave
 #pragma unroll
         for (int k = 0; k < kBinPerLane; ++k) {
             if (c[k] == 0xFFu) continue;
