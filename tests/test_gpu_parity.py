@@ -394,3 +394,16 @@ def test_bench_two_ranks_one_gpu_verified():
     line = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
     assert line["verify"] == {"edges_consistent": True, "labels_minimal_idempotent": True, "equals_torch_cc": True}
+
+
+# ---------------- opt-in fold variants, end to end against the independent torch CC ----------------
+@pytest.mark.parametrize("env", [{"GSGPU_FOLD_BIN": "1"}, {"GSGPU_FOLD_STATS": "1"}, {"GSGPU_FOLD_EPT": "8"}],
+                         ids=["binned", "stats", "ept8"])
+def test_fold_variants_verified(env):
+    import subprocess, sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--steps", "1", "--warmup", "0", "--scale", "22",
+           "--edge-factor", "16", "--window-log2", "20", "--no-cpu-baseline", "--verify"]
+    out = subprocess.check_output(cmd, env=dict(os.environ, **env), timeout=240).decode()
+    line = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert line["verify"] == {"edges_consistent": True, "labels_minimal_idempotent": True, "equals_torch_cc": True}
