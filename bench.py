@@ -45,9 +45,13 @@ def parse():
     ap.add_argument("--edge-factor", type=int, default=16)
     ap.add_argument("--window-log2", type=int, default=24)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5"],
+                    help="c3 (default, the headline): RMAT-26 EF16 per GPU, 2^24-edge windows; "
+                         "c2: RMAT-20 EF16, 2^20-edge windows; c4: Erdos-Renyi n=m=2^24, 2^20-edge windows; "
+                         "c5: RMAT-24 EF16, 2^16-edge windows, per-window emission latency p50/p99")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-windows", type=int, default=2,
-                    help="cpu_baseline sample: this many windows of the same stream")
+    ap.add_argument("--cpu-sample-edges", type=int, default=1 << 25,
+                    help="cpu_baseline sample: the first this-many edges (whole windows) of the same stream")
     ap.add_argument("--verify", action="store_true", help="check final labels with an independent torch CC "
                     "(multi-rank: rank 0 regenerates the whole global stream; small scales only)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -75,6 +79,9 @@ def main():
     if a.gpus != world and rank == 0:
         print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (a.gpus, world), file=sys.stderr)
 
+    if a.workload != "c3":                     # BASELINE.json configs other than the headline
+        a.scale, a.edge_factor, a.window_log2, a.seed = {
+            "c2": (20, 16, 20, 1), "c4": (24, 1, 20, 2), "c5": (24, 16, 16, 3)}[a.workload]
     V = 1 << a.scale
     E_rank = a.edge_factor << a.scale
     W_rank = min(1 << a.window_log2, E_rank)
@@ -87,7 +94,10 @@ def main():
     for w in range(nwin):
         lo = w * W_rank
         n = min(W_rank, E_rank - lo)
-        gen.rmat(src[lo:lo + n], dst[lo:lo + n], w * W_glob + rank * W_rank, a.scale, a.seed)
+        if a.workload == "c4":
+            gen.erdos_renyi(src[lo:lo + n], dst[lo:lo + n], w * W_glob + rank * W_rank, V, a.seed)
+        else:
+            gen.rmat(src[lo:lo + n], dst[lo:lo + n], w * W_glob + rank * W_rank, a.scale, a.seed)
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
@@ -133,6 +143,27 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    latency = None
+    if a.workload == "c5":                    # per-window emission latency: fold -> emission ready
+        lat = []
+        ds.reset()
+        for w in range(nwin):
+            lo = w * W_rank
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ds.fold(src[lo:lo + W_rank], dst[lo:lo + W_rank])
+            if tree is not None:
+                tree.merge_window()
+            else:
+                ds.close_window()
+            torch.cuda.synchronize()
+            lat.append((time.perf_counter() - t0) * 1e6)
+        lat.sort()
+        latency = {"p50_us": lat[len(lat) // 2], "p99_us": lat[min(len(lat) - 1, int(len(lat) * 0.99))],
+                   "max_us": lat[-1], "windows": len(lat)}
+
     verify = None
     if a.verify and rank == 0:
         if world == 1:
@@ -169,9 +200,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic: counter-based RMAT stream generated in HBM (seed %d), no dataset" % a.seed,
+            "data": "synthetic: counter-based %s stream generated in HBM (seed %d), no dataset"
+                    % ("Erdos-Renyi" if a.workload == "c4" else "RMAT", a.seed),
             "config": {
-                "workload": "rmat%d_ef%d_window%s" % (a.scale, a.edge_factor, _pow2(W_rank)),
+                "workload": "%s_%s%d_ef%d_window%s" % (a.workload, "er" if a.workload == "c4" else "rmat",
+                                                        a.scale, a.edge_factor, _pow2(W_rank)),
                 "scale": a.scale, "vertices": V, "edge_factor_per_gpu": a.edge_factor,
                 "edges_per_gpu": E_rank, "window_edges_per_gpu": W_rank, "windows": nwin,
                 "parallelism": "1 subtask per GPU x %d, %s" % (world, "RCCL tree merge" if world > 1 else "no merge"),
@@ -199,6 +232,8 @@ def main():
         }
         if verify is not None:
             line["verify"] = verify
+        if latency is not None:
+            line["window_latency"] = latency
         if not a.no_cpu_baseline and world == 1:
             log("timed region done (%.1f ms/step); cpu baseline..." % (elapsed / a.steps * 1e3))
             line["cpu_baseline"] = cpu_baseline(a, src, dst, W_rank)
@@ -261,7 +296,7 @@ def cpu_baseline(a, src, dst, W):
     import numpy as np
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     cores = max(1, min(cores, 16, os.cpu_count() or 1))
-    n = min(a.cpu_sample_windows * W, src.numel())
+    n = min(max(a.cpu_sample_edges // W, 1) * W, src.numel())
     hs = src[:n].cpu().numpy().astype(np.int64)
     hd = dst[:n].cpu().numpy().astype(np.int64)
     r = coracle().run(hs, hd, W, partitions=cores, threads=cores, emit=EMIT_FLATTEN)

@@ -407,3 +407,52 @@ def test_fold_variants_verified(env):
     out = subprocess.check_output(cmd, env=dict(os.environ, **env), timeout=240).decode()
     line = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
     assert line["verify"] == {"edges_consistent": True, "labels_minimal_idempotent": True, "equals_torch_cc": True}
+
+
+# ---------------- BASELINE configs at full size, per-window bit-exact vs the C oracle ----------------
+def _device_stream(gen_kind, n, param, seed):
+    import torch
+    from gsgpu import gen
+    s = torch.empty(n, dtype=torch.int32, device="cuda")
+    d = torch.empty(n, dtype=torch.int32, device="cuda")
+    if gen_kind == "rmat":
+        gen.rmat(s, d, 0, param, seed)
+    else:
+        gen.erdos_renyi(s, d, 0, param, seed)
+    torch.cuda.synchronize()
+    return s, d
+
+
+@pytest.mark.parametrize("cfg", [("rmat", 20, 1 << 20, 16 << 20, 1 << 20, 1),       # configs[1] (C2)
+                                 ("er", 1 << 24, 1 << 24, 1 << 24, 1 << 20, 2)],    # configs[3] (C4)
+                         ids=["C2_rmat20_ef16_w1M", "C4_er_n2^24_m2^24_w1M"])
+def test_baseline_config_per_window_vs_oracle(oracle, torch_cuda, cfg):
+    kind, param, cap, n, W, seed = cfg
+    s, d = _device_stream(kind, n, param, seed)
+    ds = DisjointSet(cap, id_bits=32, stream=torch_cuda.cuda.current_stream())
+    got = []
+    for lo in range(0, n, W):
+        ds.fold(s[lo:lo + W], d[lo:lo + W])
+        ds.close_window()
+        got.append(ds.checksum())
+    hs = s.cpu().numpy().astype(np.int64)
+    hd = d.cpu().numpy().astype(np.int64)
+    want = oracle.run(hs, hd, W, partitions=8, threads=8, emit=EMIT_CHECKSUM, label_cap=cap, want_final=True)
+    assert [g[0] for g in got] == [int(x) for x in want["checksums"]]
+    np.testing.assert_array_equal(ds.dense().astype(np.int64), want["final"])
+    assert got[-1][1:] == (want["final_vertices"], want["final_components"])
+
+
+def test_c5_small_windows_vs_oracle(oracle, torch_cuda):
+    """configs[4] shape (RMAT power-law, 64K-edge windows), first 4M edges of the RMAT-24 stream."""
+    n, W, cap = 1 << 22, 1 << 16, 1 << 24
+    s, d = _device_stream("rmat", n, 24, 3)
+    ds = DisjointSet(cap, id_bits=32, stream=torch_cuda.cuda.current_stream())
+    got = []
+    for lo in range(0, n, W):
+        ds.fold(s[lo:lo + W], d[lo:lo + W])
+        ds.close_window()
+        got.append(ds.checksum()[0])
+    want = oracle.run(s.cpu().numpy().astype(np.int64), d.cpu().numpy().astype(np.int64), W, partitions=4,
+                      threads=4, emit=EMIT_CHECKSUM, label_cap=cap)
+    assert got == [int(x) for x in want["checksums"]]
