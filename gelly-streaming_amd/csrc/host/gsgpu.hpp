@@ -15,6 +15,7 @@
 #include <cstdint>
 #include <functional>
 #include <map>
+#include <memory>
 #include <optional>
 #include <sstream>
 #include <stdexcept>
@@ -223,6 +224,71 @@ public:
 
 private:
     long millis_;
+    uint64_t cap_;
+    int device_;
+    uint64_t window_edges_;
+};
+
+// SummaryTreeReduce specialised to ConnectedComponents (library/ConnectedComponentsTree.java:28-34,
+// SummaryTreeReduce.java:68-123): per window, `degree` fresh partial summaries (contiguous slices
+// of the window), combined pairwise (key = partition / 2) while more than two remain, then the
+// windowAll combine and the Merger's CombineCC(windowResult, summary). Emissions are canonical and
+// equal ConnectedComponents' whatever the degree.
+template <typename K>
+class ConnectedComponentsTree {
+public:
+    explicit ConnectedComponentsTree(long mergeWindowTime, int degree = 2, uint64_t vertex_capacity = 0,
+                                     int device = 0, uint64_t window_edges = 0)
+        : millis_(mergeWindowTime), degree_(degree > 0 ? degree : 1), cap_(vertex_capacity), device_(device),
+          window_edges_(window_edges) {}
+
+    void run(const SimpleEdgeStream<K>& s, const std::function<void(DisjointSet<K>&)>& emit) {
+        uint64_t cap = cap_;
+        if (!cap) {
+            K mx = 0;
+            for (K x : s.src) mx = std::max(mx, x);
+            for (K x : s.dst) mx = std::max(mx, x);
+            cap = (uint64_t)mx + 1;
+        }
+        std::vector<std::unique_ptr<DisjointSet<K>>> pool;
+        for (int i = 0; i <= degree_; ++i) pool.emplace_back(new DisjointSet<K>(cap, device_));
+        DisjointSet<K>* summary = nullptr;
+        UpdateCC<K> update;
+        CombineCC<K> combine;
+        for (auto& w : s.windows(millis_, window_edges_)) {
+            std::vector<DisjointSet<K>*> free;
+            for (auto& d : pool) if (d.get() != summary) free.push_back(d.get());
+            const uint64_t len = w.second - w.first;
+            std::vector<DisjointSet<K>*> level;
+            for (int p = 0; p < degree_; ++p) {
+                const uint64_t a = w.first + len * p / degree_, b = w.first + len * (p + 1) / degree_;
+                if (a == b) { level.push_back(nullptr); continue; }
+                DisjointSet<K>* part = free.back();
+                free.pop_back();
+                part->reset();
+                update.foldBatch(*part, s.src.data() + a, s.dst.data() + a, b - a);
+                level.push_back(part);
+            }
+            while (level.size() > 2) {                    // enhance(): key = partition / 2
+                std::vector<DisjointSet<K>*> next;
+                for (size_t i = 0; i < level.size(); i += 2) {
+                    DisjointSet<K>* x = level[i];
+                    DisjointSet<K>* y = i + 1 < level.size() ? level[i + 1] : nullptr;
+                    next.push_back(!x ? y : (!y ? x : combine.reduce(x, y)));
+                }
+                level.swap(next);
+            }
+            DisjointSet<K>* acc = nullptr;               // windowAll reduce
+            for (auto* x : level) if (x) acc = acc ? combine.reduce(acc, x) : x;
+            summary = summary ? combine.reduce(acc, summary) : acc;
+            summary->closeWindow();
+            emit(*summary);
+        }
+    }
+
+private:
+    long millis_;
+    int degree_;
     uint64_t cap_;
     int device_;
     uint64_t window_edges_;

@@ -4,8 +4,9 @@ Python mirror of the reference's operator surface over libgsgpu.so (C ABI: inclu
 """
 from ._abi import GsError, GsgpuUnavailable, available, lib, EXPORTED_SYMBOLS  # noqa: F401
 from .summary import DisjointSet, UpdateCC, CombineCC, combine_cc  # noqa: F401
-from .aggregation import SimpleEdgeStream, SummaryBulkAggregation, ConnectedComponents  # noqa: F401
+from .aggregation import (SimpleEdgeStream, SummaryBulkAggregation, ConnectedComponents,  # noqa: F401
+                          SummaryTreeReduce, ConnectedComponentsTree)
 
 __all__ = ["DisjointSet", "UpdateCC", "CombineCC", "combine_cc", "SimpleEdgeStream",
-           "SummaryBulkAggregation", "ConnectedComponents", "GsError", "GsgpuUnavailable",
+           "SummaryBulkAggregation", "ConnectedComponents", "SummaryTreeReduce", "ConnectedComponentsTree", "GsError", "GsgpuUnavailable",
            "available", "lib"]

@@ -154,3 +154,72 @@ class ConnectedComponents(SummaryBulkAggregation):
 
     def __init__(self, mergeWindowTime: int, **kw):
         super().__init__(UpdateCC(), CombineCC(), mergeWindowTime, False, **kw)
+
+
+class SummaryTreeReduce(SummaryBulkAggregation):
+    """Partitioned fold -> log2 pairwise tree of combines -> windowAll combine -> Merger.
+
+    SummaryTreeReduce.java:68-123: partial summaries of `degree` partitions are combined in
+    rounds keyed by ``partition / 2`` (pairs (2i, 2i+1) meet at subtask i) while more than two
+    remain (``enhance``, :95-123), then the last ones go through ``timeWindowAll`` reduce and the
+    Merger (:87-90). Here every partial is a device summary and every combine is CombineCC
+    (gs_cc_combine); the canonical emission equals the bulk aggregation's.
+    """
+
+    def __init__(self, update_fun: UpdateCC, combine_fun: CombineCC, time_millis: int,
+                 transient_state: bool, degree: int = -1, **kw):
+        kw.setdefault("mode", "reference")
+        super().__init__(update_fun, combine_fun, time_millis, transient_state, **kw)
+        if degree != -1:
+            self.parallelism = max(int(degree), 1)
+        self.degree = self.parallelism
+
+    def _run_reference(self, stream, wins, cap) -> Iterator[DisjointSet]:
+        P = self.parallelism
+        pool = [self._new(cap) for _ in range(P + 1)]
+        summary: Optional[DisjointSet] = None
+        try:
+            for w in wins:
+                lo, ln = w.start, w.stop - w.start
+                free = [d for d in pool if d is not summary]
+                level: List[Optional[DisjointSet]] = []
+                for p in range(P):
+                    a, b = lo + (ln * p) // P, lo + (ln * (p + 1)) // P
+                    if a == b:
+                        level.append(None)                 # no element -> no window result
+                        continue
+                    part = free.pop()
+                    part.reset()
+                    self.update_fun.fold_batch(part, stream.src[a:b], stream.dst[a:b])
+                    level.append(part)
+                while len(level) > 2:                      # enhance(): key = partition / 2
+                    nxt: List[Optional[DisjointSet]] = []
+                    for i in range(0, len(level), 2):
+                        x = level[i]
+                        y = level[i + 1] if i + 1 < len(level) else None
+                        if x is None or y is None:
+                            nxt.append(x if y is None else y)
+                        else:
+                            nxt.append(self.combine_fun.reduce(x, y))
+                    level = nxt
+                acc: Optional[DisjointSet] = None          # windowAll reduce of what is left
+                for x in level:
+                    if x is not None:
+                        acc = x if acc is None else self.combine_fun.reduce(acc, x)
+                if summary is None or self.transient_state:
+                    summary = acc
+                else:
+                    summary = self.combine_fun.reduce(acc, summary)
+                summary.close_window()
+                yield summary
+        finally:
+            for d in pool:
+                d.close()
+
+
+class ConnectedComponentsTree(SummaryTreeReduce):
+    """ConnectedComponentsTree(long mergeWindowTime[, int degree])
+    (library/ConnectedComponentsTree.java:28-34)."""
+
+    def __init__(self, mergeWindowTime: int, degree: int = -1, **kw):
+        super().__init__(UpdateCC(), CombineCC(), mergeWindowTime, False, degree, **kw)

@@ -456,3 +456,27 @@ def test_c5_small_windows_vs_oracle(oracle, torch_cuda):
     want = oracle.run(s.cpu().numpy().astype(np.int64), d.cpu().numpy().astype(np.int64), W, partitions=4,
                       threads=4, emit=EMIT_CHECKSUM, label_cap=cap)
     assert got == [int(x) for x in want["checksums"]]
+
+
+@pytest.mark.parametrize("degree", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("case", _streams()[:3], ids=lambda c: c["name"])
+def test_connected_components_tree(case, degree):
+    """ConnectedComponentsTree(mergeWindowTime, degree): same canonical emissions per window."""
+    from gsgpu import ConnectedComponentsTree
+    stream = SimpleEdgeStream(case["src"], case["dst"])
+    cc = ConnectedComponentsTree(1000, degree, window_edges=case["window_edges"], vertex_capacity=case["cap"],
+                                 id_bits=32)
+    for w, ds in enumerate(stream.aggregate(cc)):
+        np.testing.assert_array_equal(ds.dense().astype(np.int64), case["labels"][w])
+
+
+def test_cpp_connected_components_tree_matches_bulk(oracle):
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "gelly-streaming_amd", "gsgpu", "lib", "cc_tree_check")
+    s, d = oracle.gen_rmat(0, 20000, 11, 13)
+    txt = "".join("%d %d\n" % (a, b) for a, b in zip(s.tolist(), d.tolist()))
+    for window, degree in ((1000, 4), (777, 3), (5000, 8)):
+        out = subprocess.run([exe, str(window), str(degree)], input=txt.encode(), capture_output=True, timeout=120)
+        assert out.returncode == 0, out.stdout.decode() + out.stderr.decode()
+        assert "DIFF" not in out.stdout.decode()
