@@ -87,31 +87,53 @@ __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32
         }
         return;
     }
-    if (STATS) st->inits += (pu == kInvalid) + (pv == kInvalid);
-    pu = make_set(parent, sbits, u, pu);
-    pv = make_set(parent, sbits, v, pv);
-    if (pu == pv) {                                 // common parent: already one component
+    // A side whose word was read as kInvalid is a fresh vertex: it is a root of its own, and if
+    // it ends up the larger root it is hooked straight from kInvalid (one CAS instead of an
+    // init CAS + a hook CAS). Only a fresh SMALLER root must be initialised before anything
+    // hangs below it. The CAS decides in every case: a stale kInvalid read fails and retries.
+    bool fu = pu == kInvalid, fv = pv == kInvalid;
+    if (STATS) st->inits += fu + fv;
+    if (!fu && !fv && pu == pv) {                   // common parent: already one component
         if (STATS) ++st->early;
         return;
     }
-    uint32_t ru = find_root(parent, u, pu);
-    uint32_t rv = find_root(parent, v, pv);
+    uint32_t ru = fu ? u : find_root(parent, u, pu);
+    uint32_t rv = fv ? v : find_root(parent, v, pv);
     while (ru != rv) {
-        const uint32_t hi = ru > rv ? ru : rv;
-        const uint32_t lo = ru > rv ? rv : ru;
-        const uint32_t old = atomicCAS(&parent[hi], hi, lo);
-        if (old == hi) {                            // hooked: hi is no longer a root
+        const bool uhi = ru > rv;
+        const uint32_t hi = uhi ? ru : rv, lo = uhi ? rv : ru;
+        bool& hf = uhi ? fu : fv;                   // fresh flags follow their side
+        bool& lf = uhi ? fv : fu;
+        if (lf) {                                   // the smaller root must exist first
+            const uint32_t old = atomicCAS(&parent[lo], kInvalid, lo);
+            lf = false;
+            if (old == kInvalid) {
+                set_mark(sbits, lo);
+            } else if (old != lo) {                 // initialised and hooked meanwhile
+                const uint32_t r = find_root(parent, old, parent[old]);
+                if (uhi) rv = r; else ru = r;
+                continue;
+            }
+        }
+        const uint32_t expect = hf ? kInvalid : hi;
+        const uint32_t old = atomicCAS(&parent[hi], expect, lo);
+        if (old == expect) {                        // hooked: hi is no longer a root
+            if (hf) set_mark(sbits, hi);
             if (MARK) set_mark(mark, hi);
             if (STATS) ++st->hooks;
             return;
         }
         if (STATS) ++st->casfail;
+        hf = false;
+        if (old == hi) continue;                    // was fresh, became a root meanwhile
+        if (old == kInvalid) { hf = true; continue; }   // defensive: never reached by a walk result
         // hi was hooked meanwhile: continue from its true parent (old < hi, strictly
         // decreasing, so the loop ends)
         const uint32_t r = find_root(parent, old, parent[old]);
-        if (hi == ru) ru = r; else rv = r;
+        if (uhi) ru = r; else rv = r;
     }
 }
+
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
