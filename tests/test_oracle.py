@@ -191,3 +191,13 @@ def test_rmat_scramble_is_bijection(oracle):
     for a, b in zip(np.concatenate([s, d]).tolist(), np.concatenate([s2, d2]).tolist()):
         assert pairs.setdefault(a, b) == b
     assert len(set(pairs.values())) == len(pairs)
+
+
+def test_oracle_under_host_sanitizers():
+    """The checker itself is clean under AddressSanitizer + UBSan (oracle/sanitize_main.c)."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle"), "check-asan"], capture_output=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stdout.decode() + out.stderr.decode()
+    assert b"sanitizer run OK" in out.stdout
