@@ -12,7 +12,9 @@
 // its latest emitted root. Roots are the canonical minimum vertex id of each component.
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <fstream>
+#include <iterator>
 #include <iostream>
 #include <map>
 #include <sstream>
@@ -31,14 +33,18 @@ int main(int argc, char** argv) {
             std::cerr << "Usage: cc_example <input edges path> <merge window time (ms)> <print window time (ms)>\n";
             return 1;
         }
-        std::ifstream in(argv[1]);
+        std::ifstream in(argv[1], std::ios::binary);
         if (!in) { std::cerr << "cannot open " << argv[1] << "\n"; return 1; }
-        std::string line;
-        while (std::getline(in, line)) {
-            std::istringstream ls(line);
-            long long a, b;
-            if (ls >> a >> b) { s.src.push_back(a); s.dst.push_back(b); }
-        }
+        const std::string text((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+        // parsed on the device with the reference's split("\\s") + Long.parseLong rules
+        const uint64_t cap = (uint64_t)std::count(text.begin(), text.end(), '\n') + 1;
+        s.src.resize(cap);
+        s.dst.resize(cap);
+        uint64_t n = 0;
+        const int rc = gs_parse_edges(text.data(), text.size(), 64, s.src.data(), s.dst.data(), cap, &n, 0, nullptr);
+        if (rc != GS_OK) { std::cerr << gs_last_error() << "\n"; return 2; }
+        s.src.resize(n);
+        s.dst.resize(n);
         merge_ms = std::atol(argv[2]);
         print_ms = std::atol(argv[3]);
         window_edges = merge_ms > 0 ? (uint64_t)merge_ms : 1;

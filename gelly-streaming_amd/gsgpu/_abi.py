@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = (
     "gs_cc_sync", "gs_cc_fold", "gs_cc_fold_pairs", "gs_cc_merge", "gs_cc_combine",
     "gs_cc_close_window", "gs_cc_stats", "gs_cc_emit_dense", "gs_cc_emit_pairs",
     "gs_cc_checksum", "gs_cc_find", "gs_cc_labels_device", "gs_cc_export_marks",
-    "gs_cc_fold_pairs32", "gs_cc_timing", "gs_cc_kernel_time", "gs_gen_rmat", "gs_gen_er",
+    "gs_cc_fold_pairs32", "gs_cc_timing", "gs_cc_kernel_time", "gs_gen_rmat", "gs_gen_er", "gs_parse_edges",
     "gs_last_error", "gs_version",
 )
 
@@ -97,6 +97,7 @@ def lib() -> ctypes.CDLL:
         "gs_cc_kernel_time": [vp, i32, P(ctypes.c_double), P(u64)],
         "gs_gen_rmat": [vp, vp, u32, u64, u64, i32, u64, u32, u32, u32, i32, vp],
         "gs_gen_er": [vp, vp, u32, u64, u64, u64, u64, vp],
+        "gs_parse_edges": [vp, u64, u32, vp, vp, u64, P(u64), i32, vp],
     }
     for name, args in sig.items():
         f = getattr(L, name)

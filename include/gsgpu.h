@@ -136,6 +136,15 @@ int gs_gen_rmat(void* src, void* dst, uint32_t id_bits, uint64_t first, uint64_t
 int gs_gen_er(void* src, void* dst, uint32_t id_bits, uint64_t first, uint64_t n, uint64_t nv,
               uint64_t seed, void* hip_stream);
 
+/* ---- edge-file ingestion (ConnectedComponentsExample.java:108-119) ----
+ * Parses n_bytes of text, one edge per line: Long.parseLong of fields 0 and 1 of
+ * line.split("\\s") (one whitespace character between fields; trailing whitespace and fields
+ * past the second ignored; a last line without '\n' counts). text: host or device; src/dst:
+ * host or device, id_bits wide, capacity cap edges. *n_edges = lines parsed. A line the
+ * reference would reject -> GS_ERR_INVALID, *n_edges = its 0-based index. */
+int gs_parse_edges(const char* text, uint64_t n_bytes, uint32_t id_bits, void* src, void* dst, uint64_t cap,
+                   uint64_t* n_edges, int device, void* hip_stream);
+
 const char* gs_last_error(void);
 int gs_version(void);
 

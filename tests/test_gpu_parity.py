@@ -480,3 +480,55 @@ def test_cpp_connected_components_tree_matches_bulk(oracle):
         out = subprocess.run([exe, str(window), str(degree)], input=txt.encode(), capture_output=True, timeout=120)
         assert out.returncode == 0, out.stdout.decode() + out.stderr.decode()
         assert "DIFF" not in out.stdout.decode()
+
+
+# ---------------- edge-file ingestion (ConnectedComponentsExample.java:108-119 rules) ----------------
+def _java_parse(text: bytes):
+    """Reference semantics: per line, fields = line.split("\\\\s") (trailing empties dropped),
+    Long.parseLong(fields[0]), Long.parseLong(fields[1]); returns (src, dst) or the bad line index."""
+    import re
+    lines = text.decode().split("\n")
+    if lines and lines[-1] == "":
+        lines = lines[:-1]
+    src, dst = [], []
+    for i, ln in enumerate(lines):
+        f = re.split(r"[ \t\n\x0b\f\r]", ln)
+        while f and f[-1] == "":
+            f.pop()
+        ok = len(f) >= 2 and all(re.fullmatch(r"[+-]?[0-9]+", x) for x in f[:2])
+        if ok:
+            a, b = int(f[0]), int(f[1])
+            ok = -(1 << 63) <= a < (1 << 63) and -(1 << 63) <= b < (1 << 63)
+        if not ok:
+            return i
+        src.append(a)
+        dst.append(b)
+    return np.array(src, dtype=np.int64), np.array(dst, dtype=np.int64)
+
+
+def test_parse_edges_valid_forms():
+    from gsgpu.edgefile import parse_edges
+    text = b"1 2\n3\t4\n5 6 extra fields\n+7 -8\r\n9 10  \n" + b"".join(b"%d %d\n" % (i, i * 7 % 1000) for i in range(5000)) + b"11 12"
+    want = _java_parse(text)
+    got = parse_edges(text, id_bits=64)
+    np.testing.assert_array_equal(got[0], want[0])
+    np.testing.assert_array_equal(got[1], want[1])
+
+
+@pytest.mark.parametrize("bad", [b"1  2\n", b"\n", b" 1 2\n", b"1x 2\n", b"1\n", b"1 99999999999999999999\n"])
+def test_parse_edges_rejects_what_java_rejects(bad):
+    from gsgpu.edgefile import parse_edges
+    text = b"5 6\n7 8\n" + bad + b"9 10\n"
+    assert _java_parse(text) == 2
+    with pytest.raises(GsError) as ei:
+        parse_edges(text, id_bits=64)
+    assert ei.value.code == _abi.GS_ERR_INVALID and "line 3" in str(ei.value)
+
+
+def test_parse_edges_large_random_and_fold(oracle):
+    from gsgpu.edgefile import parse_edges
+    s, d = oracle.gen_rmat(0, 300000, 16, 2)
+    text = "".join("%d %d\n" % (a, b) for a, b in zip(s.tolist(), d.tolist())).encode()
+    ps, pd = parse_edges(text, id_bits=32)
+    np.testing.assert_array_equal(ps, s)
+    np.testing.assert_array_equal(pd, d)
