@@ -8,6 +8,8 @@
 #include <mutex>
 #include <vector>
 
+#include <hip/hip_ext.h>
+
 #include "cc_kernels.hpp"
 
 namespace gsgpu {
@@ -67,6 +69,7 @@ struct gs_cc {
     size_t tmp_bytes = 0;
     bool compressed = true;
     uint64_t edges_since_reset = 0;      // drives the young-forest launch split (fold_impl)
+    uint64_t closes = 0;                 // compressions since reset (giant re-sampled every kPickEvery)
     unsigned long long* dstats = nullptr;    // GSGPU_FOLD_STATS=1: per-window fold counters
     uint32_t* bins = nullptr;            // XCD-local binning: 2 x kBinClasses x bin_region ids
     uint64_t bin_region = 0;
@@ -102,19 +105,40 @@ hipEvent_t get_event(gs_cc_t* h) {
     return e;
 }
 
-// brackets one kernel launch with events when timing is on
+// GSGPU_TIMING=marker: separate hipEventRecord marker packets around each timed launch (each
+// one is a barrier packet: ~10 us of idle GPU per marker on gfx950, profiles/r01_v3). Default:
+// the events ride on the kernel dispatch itself (hipExtLaunchKernelGGL start/stop events).
+static bool timing_markers() {
+    static const bool on = [] { const char* e = getenv("GSGPU_TIMING"); return e && !strcmp(e, "marker"); }();
+    return on;
+}
+
+// Times one span of launches of kernel class k (HIP events on the launch stream). Launch the
+// span's first kernel with start() and its last with stop() through klaunch().
 struct KTimer {
-    gs_cc_t* h; int k; hipEvent_t a = nullptr;
+    gs_cc_t* h; int k; hipEvent_t a = nullptr, b = nullptr; bool markers = false;
     KTimer(gs_cc_t* h_, int k_) : h(h_), k(k_) {
-        if (h->timing) { a = get_event(h); (void)hipEventRecord(a, h->stream); }
+        if (!h->timing) return;
+        a = get_event(h);
+        b = get_event(h);
+        markers = timing_markers();
+        if (markers) (void)hipEventRecord(a, h->stream);
     }
+    hipEvent_t start() const { return markers ? nullptr : a; }
+    hipEvent_t stop() const { return markers ? nullptr : b; }
     ~KTimer() {
-        if (!h->timing || !a) return;
-        hipEvent_t b = get_event(h);
-        (void)hipEventRecord(b, h->stream);
+        if (!a) return;
+        if (markers) (void)hipEventRecord(b, h->stream);
         h->pending.push_back({k, a, b});
     }
 };
+
+// hipLaunchKernelGGL with optional start/stop events attached to the dispatch
+template <typename F, typename... Args>
+inline void klaunch(F kernel, dim3 grid, dim3 block, hipStream_t s, hipEvent_t start, hipEvent_t stop, Args... args) {
+    if (start || stop) hipExtLaunchKernelGGL(kernel, grid, block, 0, s, start, stop, 0, args...);
+    else hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
+}
 
 int resolve_timing(gs_cc_t* h) {
     for (auto& p : h->pending) {
@@ -168,9 +192,9 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n) {
     const bool vec = std::is_same<IdT, uint32_t>::value && !AOS &&
                      ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
     KTimer t(h, GS_K_FOLD);
-#define GS_LAUNCH_FOLD(MARKV, VECV, EPTV, STV)                                                                    \
-    hipLaunchKernelGGL((k_fold<IdT, AOS, MARKV, VECV, EPTV, STV>), dim3(grid), dim3(kFoldThreads), 0, h->stream, \
-                       (const IdT*)a, (const IdT*)b, f)
+#define GS_LAUNCH_FOLD(MARKV, VECV, EPTV, STV)                                                                       \
+    klaunch((k_fold<IdT, AOS, MARKV, VECV, EPTV, STV>), dim3(grid), dim3(kFoldThreads), h->stream, t.start(), t.stop(), \
+            (const IdT*)a, (const IdT*)b, f)
     if (h->dstats) { if (h->mark) GS_LAUNCH_FOLD(true, false, 4, true); else GS_LAUNCH_FOLD(false, false, 4, true); }
     else if (vec && ept == 8) { if (h->mark) GS_LAUNCH_FOLD(true, true, 8, false); else GS_LAUNCH_FOLD(false, true, 8, false); }
     else if (h->mark) { if (vec) GS_LAUNCH_FOLD(true, true, 4, false); else GS_LAUNCH_FOLD(true, false, 4, false); }
@@ -214,15 +238,15 @@ int launch_fold_binned(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_
         const uint64_t m = std::min<uint64_t>(n - off, step);
         KTimer t(h, GS_K_FOLD);
         GS_HIP(hipMemsetAsync(h->bin_counts, 0, kBinClasses * kBinLanes * sizeof(unsigned long long), h->stream));
-        hipLaunchKernelGGL(k_bin, dim3(grid_for(m, kBinTile, 16384)), dim3(256), 0, h->stream, a + off, b + off, m, bn,
-                           RangeCheck{h->cap, h->derr});
+        klaunch(k_bin, dim3(grid_for(m, kBinTile, 16384)), dim3(256), h->stream, t.start(), nullptr, a + off, b + off, m, bn,
+                RangeCheck{h->cap, h->derr});
         const unsigned per_group = (unsigned)std::min<uint64_t>(std::max<uint64_t>((m / 8 + 1023) / 1024, 1), 2048);
         if (h->dstats) {
-            if (h->mark) hipLaunchKernelGGL((k_fold_binned<true, true>), dim3(8 * per_group), dim3(kFoldThreads), 0, h->stream, bn, f);
-            else hipLaunchKernelGGL((k_fold_binned<false, true>), dim3(8 * per_group), dim3(kFoldThreads), 0, h->stream, bn, f);
+            if (h->mark) klaunch((k_fold_binned<true, true>), dim3(8 * per_group), dim3(kFoldThreads), h->stream, nullptr, t.stop(), bn, f);
+            else klaunch((k_fold_binned<false, true>), dim3(8 * per_group), dim3(kFoldThreads), h->stream, nullptr, t.stop(), bn, f);
         } else {
-            if (h->mark) hipLaunchKernelGGL((k_fold_binned<true, false>), dim3(8 * per_group), dim3(kFoldThreads), 0, h->stream, bn, f);
-            else hipLaunchKernelGGL((k_fold_binned<false, false>), dim3(8 * per_group), dim3(kFoldThreads), 0, h->stream, bn, f);
+            if (h->mark) klaunch((k_fold_binned<true, false>), dim3(8 * per_group), dim3(kFoldThreads), h->stream, nullptr, t.stop(), bn, f);
+            else klaunch((k_fold_binned<false, false>), dim3(8 * per_group), dim3(kFoldThreads), h->stream, nullptr, t.stop(), bn, f);
         }
         GS_HIP(hipGetLastError());
     }
@@ -321,9 +345,11 @@ int compress_impl(gs_cc_t* h) {
     if (h->compressed) return GS_OK;
     {
         KTimer t(h, GS_K_COMPRESS);
-        hipLaunchKernelGGL(k_pick_giant, dim3(1), dim3(1024), 0, h->stream, h->parent, h->cap, h->derr + 1);
-        hipLaunchKernelGGL(k_compress, dim3(grid_for(h->cap, 1024, 16384)), dim3(256), 0, h->stream,
-                           h->parent, h->cap, h->gbits, h->sbits, h->derr + 1);
+        klaunch(k_pick_giant, dim3(1), dim3(1024), h->stream, t.start(), nullptr, (const uint32_t*)h->parent, h->cap, h->derr + 1,
+                (int)(h->closes % kPickEvery != 0));
+        ++h->closes;
+        klaunch(k_compress, dim3(grid_for(h->cap, 1024, 16384)), dim3(256), h->stream, nullptr, t.stop(),
+                h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)(h->derr + 1));
     }
     GS_HIP(hipGetLastError());
     h->compressed = true;
@@ -434,6 +460,7 @@ int gs_cc_reset(gs_cc_t* h) {
     GS_HIP(hipMemsetAsync(h->derr + 2, 0, 4, h->stream));          // next close: full
     h->compressed = true;
     h->edges_since_reset = 0;
+    h->closes = 0;
     return GS_OK;
 }
 
@@ -488,8 +515,8 @@ int gs_cc_merge(gs_cc_t* into, gs_cc_t* from) {
     {
         KTimer t(into, GS_K_MERGE);
         const dim3 grid(grid_for(from->cap, 256, 16384));
-        if (into->mark) hipLaunchKernelGGL(k_merge_dense<true>, grid, dim3(256), 0, into->stream, from->parent, from->cap, into->parent, into->mark, into->sbits);
-        else hipLaunchKernelGGL(k_merge_dense<false>, grid, dim3(256), 0, into->stream, from->parent, from->cap, into->parent, into->mark, into->sbits);
+        if (into->mark) klaunch(k_merge_dense<true>, grid, dim3(256), into->stream, t.start(), t.stop(), (const uint32_t*)from->parent, from->cap, into->parent, into->mark, into->sbits);
+        else klaunch(k_merge_dense<false>, grid, dim3(256), into->stream, t.start(), t.stop(), (const uint32_t*)from->parent, from->cap, into->parent, into->mark, into->sbits);
     }
     GS_HIP(hipGetLastError());
     if (from->stream != into->stream) {   // `from` must not be reused before the merge read it
@@ -659,8 +686,8 @@ int gs_cc_export_marks(gs_cc_t* h, void* pairs, uint64_t cap, uint64_t* n_out) {
     GS_HIP(hipMemsetAsync(h->dscratch, 0, sizeof(unsigned long long), h->stream));
     {
         KTimer t(h, GS_K_EXPORT);
-        hipLaunchKernelGGL(k_export_marks, dim3(grid_for((h->cap + 31) / 32, 256, 4096)), dim3(256), 0, h->stream,
-                           h->mark, h->parent, h->cap, (uint32_t*)out, cap, h->dscratch);
+        klaunch(k_export_marks, dim3(grid_for((h->cap + 31) / 32, 256, 4096)), dim3(256), h->stream, t.start(), t.stop(),
+                h->mark, (const uint32_t*)h->parent, h->cap, (uint32_t*)out, cap, h->dscratch);
     }
     GS_HIP(hipGetLastError());
     GS_HIP(hipMemcpyAsync(h->hscratch, h->dscratch, 8, hipMemcpyDeviceToHost, h->stream));

@@ -448,8 +448,22 @@ constexpr int kPickSlots = 2048;
 // state[0] = giant root (kInvalid: none), state[1] = 1 iff the next close may be incremental:
 // the picked root equals the root the last close built gbits for (so it was not hooked: roots
 // only ever become non-roots, and the pick returns roots).
+//
+// follow != 0 and a giant root is known: no sampling, the giant is followed to its current root
+// (components only merge, so the sampled giant stays the component holding its old root; the
+// host re-samples every kPickEvery closes in case another component overtook it).
+constexpr int kPickEvery = 8;
 __global__ __launch_bounds__(1024) void k_pick_giant(const uint32_t* __restrict__ parent, uint32_t n,
-                                                    uint32_t* __restrict__ giant) {
+                                                    uint32_t* __restrict__ giant, int follow) {
+    if (follow && giant[0] != kInvalid) {       // uniform over the block
+        if (threadIdx.x == 0) {
+            const uint32_t g0 = giant[0];
+            const uint32_t g = find_root_ro(parent, g0);
+            giant[1] = (g == g0) ? 1u : 0u;
+            giant[0] = g;
+        }
+        return;
+    }
     __shared__ uint32_t keys[kPickSlots];
     __shared__ uint32_t cnt[kPickSlots];
     __shared__ unsigned long long best[16];
