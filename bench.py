@@ -217,7 +217,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "k_fold<uint32,SoA> (UpdateCC), per window fold",
+                "kernel": "UpdateCC per window: k_fold_ring (steady windows) / k_fold (young-forest launches)",
                 "alg_bytes_per_window": BYTES_PER_EDGE_ALG * W_rank,
                 "fold_ms_per_window": fold_win_ms,
                 "fold_launches": fold_n,

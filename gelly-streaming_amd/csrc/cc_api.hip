@@ -71,9 +71,10 @@ struct gs_cc {
     uint64_t edges_since_reset = 0;      // drives the young-forest launch split (fold_impl)
     uint64_t closes = 0;                 // compressions since reset (giant re-sampled every kPickEvery)
     unsigned long long* dstats = nullptr;    // GSGPU_FOLD_STATS=1: per-window fold counters
-    uint32_t* bins = nullptr;            // XCD-local binning: 2 x kBinClasses x bin_region ids
-    uint64_t bin_region = 0;
-    unsigned long long* bin_counts = nullptr;
+    uint2* hot = nullptr;                // LDS hot set master copy (kHotBuckets uint2), steady folds
+    uint32_t hot_bits = 0;               // ids < 2^hot_bits
+    uint32_t* hot_cand = nullptr;        // hot-set admission candidates (2^kHotCandBits ids)
+    int cus = 0;                         // compute units: k_fold_ring grid
     // instrumentation
     bool timing = false;
     struct Pend { int k; hipEvent_t a, b; };
@@ -202,55 +203,35 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n) {
 #undef GS_LAUNCH_FOLD
 }
 
-// XCD-local binned fold: off unless GSGPU_FOLD_BIN=1 (experimental)
-static bool fold_bin_on() {
-    static const bool on = [] { const char* e = getenv("GSGPU_FOLD_BIN"); return e && atoi(e) != 0; }();
-    return on;
+// Steady-state fold (mature forest, aligned device uint32 SoA), GSGPU_FOLD_MODE:
+//   ring  (default) k_fold_ring: LDS hot set + survivor rings, one persistent launch
+//   plain k_fold, as for young windows (the A/B baseline)
+enum FoldMode { kFoldPlain = 0, kFoldRing = 1 };
+static int fold_mode() {
+    static const int m = [] {
+        const char* e = getenv("GSGPU_FOLD_MODE");
+        return (e && !strcmp(e, "plain")) ? (int)kFoldPlain : (int)kFoldRing;
+    }();
+    return m;
 }
 
-// Binned fold of n device-resident uint32 SoA edges (n <= region): k_bin then k_fold_binned.
-int launch_fold_binned(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t n) {
-    // region = ids per class; a lane's sub-region holds every tile of that lane in full
-    const uint64_t chunk = std::max<uint64_t>(std::min<uint64_t>(n, 1ull << 24), kBinTile);
-    const uint64_t tiles_per_lane = (chunk / kBinTile + kBinLanes - 1) / kBinLanes + 1;
-    const uint64_t region = tiles_per_lane * kBinTile * kBinLanes;
-    if (h->bin_region < region) {
-        if (h->bins) { GS_HIP(hipFree(h->bins)); h->bins = nullptr; }
-        if (hipMalloc(&h->bins, 2 * kBinClasses * region * sizeof(uint32_t)) != hipSuccess) {
-            (void)hipGetLastError();
-            h->bin_region = 0;
-            return fail(GS_ERR_NOMEM, "bin buffers (%llu edges) allocation failed", (unsigned long long)region);
-        }
-        h->bin_region = region;
+void launch_fold_ring(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t n) {
+    if (fold_stats_on() && !h->dstats) {
+        (void)hipMalloc(&h->dstats, 8 * sizeof(unsigned long long));
+        (void)hipMemsetAsync(h->dstats, 0, 8 * sizeof(unsigned long long), h->stream);
     }
-    if (!h->bin_counts) {
-        if (hipMalloc(&h->bin_counts, kBinClasses * kBinLanes * sizeof(unsigned long long)) != hipSuccess) {
-            (void)hipGetLastError();
-            return fail(GS_ERR_NOMEM, "bin counts allocation failed");
-        }
+    const HotArgs hot{h->hot, h->hot_bits, h->hot_cand};
+    FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, h->derr + 1, RangeCheck{h->cap, h->derr}, h->dstats};
+    KTimer t(h, GS_K_FOLD);
+    const bool st = h->dstats != nullptr;
+    const dim3 grid(grid_for(n / 4, kHotThreads, (unsigned)std::max(h->cus, 1)));
+    if (h->mark) {
+        if (st) klaunch(k_fold_ring<true, true>, grid, dim3(kHotThreads), h->stream, t.start(), t.stop(), a, b, f, hot);
+        else klaunch(k_fold_ring<true, false>, grid, dim3(kHotThreads), h->stream, t.start(), t.stop(), a, b, f, hot);
+    } else {
+        if (st) klaunch(k_fold_ring<false, true>, grid, dim3(kHotThreads), h->stream, t.start(), t.stop(), a, b, f, hot);
+        else klaunch(k_fold_ring<false, false>, grid, dim3(kHotThreads), h->stream, t.start(), t.stop(), a, b, f, hot);
     }
-    const uint64_t words = ((uint64_t)h->cap + 31) / 32;
-    BinArgs bn{(uint32_t)(words * 1 / 4 * 32), (uint32_t)(words * 2 / 4 * 32), (uint32_t)(words * 3 / 4 * 32),
-               h->bins, h->bins + kBinClasses * h->bin_region, h->bin_region, h->bin_region / kBinLanes, h->bin_counts};
-    FoldArgs f{0, h->parent, h->mark, h->sbits, h->gbits, h->derr + 1, RangeCheck{h->cap, h->derr}, h->dstats};
-    const uint64_t step = (h->bin_region / kBinLanes / kBinTile - 1) * kBinLanes * kBinTile;   // edges per k_bin launch
-    for (uint64_t off = 0; off < n; off += step) {
-        const uint64_t m = std::min<uint64_t>(n - off, step);
-        KTimer t(h, GS_K_FOLD);
-        GS_HIP(hipMemsetAsync(h->bin_counts, 0, kBinClasses * kBinLanes * sizeof(unsigned long long), h->stream));
-        klaunch(k_bin, dim3(grid_for(m, kBinTile, 16384)), dim3(256), h->stream, t.start(), nullptr, a + off, b + off, m, bn,
-                RangeCheck{h->cap, h->derr});
-        const unsigned per_group = (unsigned)std::min<uint64_t>(std::max<uint64_t>((m / 8 + 1023) / 1024, 1), 2048);
-        if (h->dstats) {
-            if (h->mark) klaunch((k_fold_binned<true, true>), dim3(8 * per_group), dim3(kFoldThreads), h->stream, nullptr, t.stop(), bn, f);
-            else klaunch((k_fold_binned<false, true>), dim3(8 * per_group), dim3(kFoldThreads), h->stream, nullptr, t.stop(), bn, f);
-        } else {
-            if (h->mark) klaunch((k_fold_binned<true, false>), dim3(8 * per_group), dim3(kFoldThreads), h->stream, nullptr, t.stop(), bn, f);
-            else klaunch((k_fold_binned<false, false>), dim3(8 * per_group), dim3(kFoldThreads), h->stream, nullptr, t.stop(), bn, f);
-        }
-        GS_HIP(hipGetLastError());
-    }
-    return GS_OK;
 }
 
 // Young-forest launch split: while fewer than capacity/4 edges have been folded since reset,
@@ -263,14 +244,18 @@ constexpr uint64_t kYoungChunk = 1ull << 18;
 template <typename IdT, bool AOS>
 void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, size_t esz) {
     const uint64_t young_limit = h->cap / 4;
-    // mature forest, large id space, aligned device uint32 SoA: XCD-local binned fold
-    if (std::is_same<IdT, uint32_t>::value && !AOS && fold_bin_on() && h->edges_since_reset >= young_limit &&
-        h->cap >= (1u << 22) && n >= (1u << 20) &&
-        ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0 && is_device_pointer(a)) {
-        if (launch_fold_binned(h, reinterpret_cast<const uint32_t*>(a), reinterpret_cast<const uint32_t*>(b), n) == GS_OK) {
-            h->edges_since_reset += n;
-            return;
-        }
+    // mature forest (past twice the young limit: the hot set has been filling for a window),
+    // aligned device uint32 SoA: the steady ring fold
+    if (std::is_same<IdT, uint32_t>::value && !AOS && h->hot && fold_mode() == kFoldRing &&
+        h->edges_since_reset >= 2 * young_limit && n >= 4 &&
+        ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0) {
+        const uint64_t done = n & ~(uint64_t)3;
+        launch_fold_ring(h, reinterpret_cast<const uint32_t*>(a), reinterpret_cast<const uint32_t*>(b), done);
+        h->edges_since_reset += done;
+        if (done == n) return;
+        a += done * esz;
+        b += done * esz;
+        n -= done;
     }
     uint64_t off = 0;
     while (off < n) {
@@ -335,8 +320,8 @@ void report_fold_stats(gs_cc_t* h) {
     unsigned long long c[8];
     if (hipMemcpyAsync(c, h->dstats, sizeof(c), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
         hipStreamSynchronize(h->stream) != hipSuccess) return;
-    fprintf(stderr, "[gsgpu fold-stats] valid=%llu unfiltered=%llu early=%llu hooks=%llu casfail=%llu inits=%llu\n",
-            c[0], c[1], c[2], c[3], c[4], c[5]);
+    fprintf(stderr, "[gsgpu fold-stats] valid=%llu filtered=%llu early=%llu hooks=%llu casfail=%llu inits=%llu hot_hits=%llu\n",
+            c[0], c[1], c[2], c[3], c[4], c[5], c[6]);
     (void)hipMemsetAsync(h->dstats, 0, sizeof(c), h->stream);
 }
 
@@ -346,7 +331,7 @@ int compress_impl(gs_cc_t* h) {
     {
         KTimer t(h, GS_K_COMPRESS);
         klaunch(k_pick_giant, dim3(1), dim3(1024), h->stream, t.start(), nullptr, (const uint32_t*)h->parent, h->cap, h->derr + 1,
-                (int)(h->closes % kPickEvery != 0));
+                (int)(h->closes % kPickEvery != 0), h->hot);
         ++h->closes;
         klaunch(k_compress, dim3(grid_for(h->cap, 1024, 16384)), dim3(256), h->stream, nullptr, t.stop(),
                 h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)(h->derr + 1));
@@ -417,6 +402,22 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
         return bail(fail(GS_ERR_NOMEM, "scratch allocation failed"));
     }
     std::memset(h->hscratch, 0, 8 * sizeof(unsigned long long));
+    if (hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, cfg->device) != hipSuccess) h->cus = 0;
+    {
+        uint32_t bits = 0;
+        while (bits < 32 && (1ull << bits) < (uint64_t)h->cap) ++bits;
+        if (bits >= 20 && bits <= kHotBucketBits + 15) {     // remainders fit 15 bits (+1 in 16)
+            if (hipMalloc(&h->hot, kHotBuckets * sizeof(uint2)) != hipSuccess ||
+                hipMalloc(&h->hot_cand, sizeof(uint32_t) << kHotCandBits) != hipSuccess) {
+                (void)hipGetLastError();
+                if (h->hot) (void)hipFree(h->hot);
+                if (h->hot_cand) (void)hipFree(h->hot_cand);
+                h->hot = nullptr;
+                h->hot_cand = nullptr;
+            }
+            h->hot_bits = bits;
+        }
+    }
     if (hipMemsetAsync(h->derr, 0, 4, h->stream) != hipSuccess) return bail(fail(GS_ERR_HIP, "memset failed"));
     int rc = gs_cc_reset(h);
     if (rc != GS_OK) return bail(rc);
@@ -438,8 +439,8 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->gbits) (void)hipFree(h->gbits);
     if (h->sbits) (void)hipFree(h->sbits);
     if (h->dstats) (void)hipFree(h->dstats);
-    if (h->bins) (void)hipFree(h->bins);
-    if (h->bin_counts) (void)hipFree(h->bin_counts);
+    if (h->hot) (void)hipFree(h->hot);
+    if (h->hot_cand) (void)hipFree(h->hot_cand);
     if (h->dscratch) (void)hipFree(h->dscratch);
     if (h->hscratch) (void)hipHostFree(h->hscratch);
     if (h->stage) (void)hipFree(h->stage);
@@ -458,6 +459,9 @@ int gs_cc_reset(gs_cc_t* h) {
     GS_HIP(hipMemsetAsync(h->sbits, 0, mark_bytes(h->cap), h->stream));
     GS_HIP(hipMemsetAsync(h->derr + 1, 0xFF, 4, h->stream));       // no giant root yet
     GS_HIP(hipMemsetAsync(h->derr + 2, 0, 4, h->stream));          // next close: full
+    GS_HIP(hipMemsetAsync(h->derr + 3, 0xFF, 4, h->stream));       // hot set owner: none
+    if (h->hot) GS_HIP(hipMemsetAsync(h->hot, 0, kHotBuckets * sizeof(uint2), h->stream));
+    if (h->hot_cand) GS_HIP(hipMemsetAsync(h->hot_cand, 0xFF, sizeof(uint32_t) << kHotCandBits, h->stream));
     h->compressed = true;
     h->edges_since_reset = 0;
     h->closes = 0;

@@ -167,6 +167,129 @@ struct FoldArgs {
     unsigned long long* stats;   // STATS: [valid, filtered, early, hooks, casfail, inits]
 };
 
+// ---- LDS hot set (steady state) ----
+// The filter's two gbits lookups per edge miss L2 half the time (an 8 MiB bitmap against a 4 MiB
+// L2 per XCD) and the Infinity-Cache transfers of those misses bound the steady fold. The most
+// frequent endpoints of a power-law stream are few: a 128 KiB exact set of giant-component
+// members, copied into every workgroup's LDS at launch, answers ~1/3 of the lookups of an RMAT-26
+// window from LDS (tools/hot_lab.hip: 268 -> 225 us per 2^24 edges).
+// Layout: 2^14 buckets x 4 slots of 16-bit remainders. With ids < 2^B (B = hot_bits, 20..29),
+// h = v * kHotMul mod 2^B (odd multiplier: a bijection), bucket = h >> (B - 14), slot value =
+// (h mod 2^(B-14)) + 1; (bucket, slot value) <-> v is one-to-one, so membership is exact. 0 = empty.
+// Entries are only ever added (a 0 half-word CASed to a remainder) and every entry is a vertex
+// whose gbits bit was set, i.e. a member of the giant component; components only merge until
+// reset, so an entry stays a member while the giant is the same component (k_pick_giant clears
+// the table when a re-sample picks another one). Filling: each steady fold launch inserts the
+// filter-confirmed endpoints of its first kHotSampleEdges edges into free slots; hubs appear
+// first in any prefix of a power-law stream, so the table fills with them.
+constexpr int kHotBucketBits = 14;
+constexpr uint32_t kHotBuckets = 1u << kHotBucketBits;
+constexpr uint32_t kHotMul = 0x9E3779B1u;
+constexpr int kHotThreads = 1024;
+constexpr uint64_t kHotSampleEdges = 1u << 18;
+
+__device__ __forceinline__ uint32_t hot_hash(uint32_t v, uint32_t B) {
+    return (v * kHotMul) & ((B >= 32) ? ~0u : ((1u << B) - 1));
+}
+
+__device__ __forceinline__ bool hot_probe(const uint2* tab, uint32_t v, uint32_t B) {
+    const uint32_t h = hot_hash(v, B);
+    const uint32_t rb = B - kHotBucketBits;
+    const uint2 w = tab[h >> rb];
+    const uint32_t r = (h & ((1u << rb) - 1)) + 1;
+    return ((w.x & 0xFFFFu) == r) | ((w.x >> 16) == r) | ((w.y & 0xFFFFu) == r) | ((w.y >> 16) == r);
+}
+
+// add v to the global table if a slot of its bucket is free (a full bucket drops it)
+__device__ inline void hot_insert(uint2* gtab, uint32_t v, uint32_t B) {
+    const uint32_t h = hot_hash(v, B);
+    const uint32_t rb = B - kHotBucketBits;
+    const uint32_t r = (h & ((1u << rb) - 1)) + 1;
+    uint32_t* words = reinterpret_cast<uint32_t*>(gtab + (h >> rb));
+#pragma unroll
+    for (int wi = 0; wi < 2; ++wi) {
+        uint32_t x = __hip_atomic_load(&words[wi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int attempt = 0; attempt < 4; ++attempt) {
+            const uint32_t lo = x & 0xFFFFu, hi = x >> 16;
+            if (lo == r || hi == r) return;
+            if (lo && hi) break;                             // this word is full
+            const uint32_t want = lo ? (x | (r << 16)) : (x | r);
+            const uint32_t old = atomicCAS(&words[wi], x, want);
+            if (old == x) return;
+            x = old;
+        }
+    }
+}
+
+// Admission: a sampled giant member enters the hot set on its second sighting. `cand` is a
+// direct-mapped table of the last sampled id per slot (overwritten on collision), so an id gets
+// in only if it recurs before another sampled id lands on its slot: ids are admitted roughly in
+// order of frequency, the hubs within the first sampled window. Plain racing stores are fine
+// here: any value in a slot is only a candidate.
+constexpr uint32_t kHotCandBits = 20;                // 2^20 candidate slots (4 MiB)
+struct HotArgs {
+    uint2* table;       // global master copy (kHotBuckets uint2), nullptr = no hot set
+    uint32_t bits;      // B: every id < 2^B
+    uint32_t* cand;     // 2^kHotCandBits candidate slots
+};
+
+__device__ __forceinline__ void hot_admit(const HotArgs& hot, uint32_t v) {
+    uint32_t* slot = &hot.cand[(uint32_t)(splitmix64(v) >> (64 - kHotCandBits))];
+    if (__hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == v) hot_insert(hot.table, v, hot.bits);
+    else __hip_atomic_store(slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Filter of one thread's EPT edges (ids already range-checked and zeroed where !ok): ok[k]
+// becomes false for an edge whose endpoints are both in the giant component. HOT: probe the LDS
+// hot set `tab` before gbits, and (insert) offer the gbits-confirmed endpoints for admission.
+template <bool STATS, int EPT, bool HOT>
+__device__ __forceinline__ void filter_group(const FoldArgs& f, const uint32_t (&u)[EPT], const uint32_t (&v)[EPT],
+                                             bool (&ok)[EPT], const uint2* tab, const HotArgs& hot, bool insert) {
+    bool hu[EPT], hv[EPT];
+    uint32_t wu[EPT], wv[EPT];
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        hu[k] = HOT && hot_probe(tab, u[k], hot.bits);
+        hv[k] = HOT && hot_probe(tab, v[k], hot.bits);
+    }
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        wu[k] = hu[k] ? ~0u : f.gbits[u[k] >> 5];
+        wv[k] = hv[k] ? ~0u : f.gbits[v[k] >> 5];
+    }
+    if (HOT && STATS) {
+        uint32_t nh = 0;
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) nh += (ok[k] && hu[k]) + (ok[k] && hv[k]);
+        if (nh) atomicAdd(&f.stats[6], (unsigned long long)nh);
+    }
+    if (HOT && insert) {
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            if (ok[k] && !hu[k] && ((wu[k] >> (u[k] & 31)) & 1u)) hot_admit(hot, u[k]);
+            if (ok[k] && !hv[k] && ((wv[k] >> (v[k] & 31)) & 1u)) hot_admit(hot, v[k]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < EPT; ++k)
+        ok[k] = ok[k] && !((wu[k] >> (u[k] & 31)) & (wv[k] >> (v[k] & 31)) & 1u);
+}
+
+// Parent gathers and unions of the edges with ok[k] (all issued before any dependent step).
+template <bool MARK, bool STATS, int EPT>
+__device__ __forceinline__ void union_group(const FoldArgs& f, const uint32_t (&u)[EPT], const uint32_t (&v)[EPT],
+                                            const bool (&ok)[EPT], FoldStats& st) {
+    uint32_t pu[EPT], pv[EPT];
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        pu[k] = ok[k] ? f.parent[u[k]] : 0u;
+        pv[k] = ok[k] ? f.parent[v[k]] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < EPT; ++k)
+        if (ok[k]) union_edge<MARK, STATS>(f.parent, f.mark, f.sbits, u[k], v[k], pu[k], pv[k], &st);
+}
+
 // Filter, parent gathers and unions of one thread's EPT edges (ids already range-checked;
 // ok[k] false = nothing to do for edge k).
 template <bool MARK, bool STATS, int EPT>
@@ -178,26 +301,8 @@ __device__ __forceinline__ void fold_group(const FoldArgs& f, bool filt, uint32_
     }
     uint32_t nvalid = 0, nfilt = 0;
     if (STATS) for (int k = 0; k < EPT; ++k) nvalid += ok[k];
-    if (filt) {
-        uint32_t wu[EPT], wv[EPT];
-#pragma unroll
-        for (int k = 0; k < EPT; ++k) {
-            wu[k] = f.gbits[u[k] >> 5];
-            wv[k] = f.gbits[v[k] >> 5];
-        }
-#pragma unroll
-        for (int k = 0; k < EPT; ++k)
-            ok[k] = ok[k] && !((wu[k] >> (u[k] & 31)) & (wv[k] >> (v[k] & 31)) & 1u);
-    }
-    uint32_t pu[EPT], pv[EPT];
-#pragma unroll
-    for (int k = 0; k < EPT; ++k) {
-        pu[k] = ok[k] ? f.parent[u[k]] : 0u;
-        pv[k] = ok[k] ? f.parent[v[k]] : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < EPT; ++k)
-        if (ok[k]) union_edge<MARK, STATS>(f.parent, f.mark, f.sbits, u[k], v[k], pu[k], pv[k], &st);
+    if (filt) filter_group<STATS, EPT, false>(f, u, v, ok, nullptr, HotArgs{nullptr, 0, nullptr}, false);
+    union_group<MARK, STATS, EPT>(f, u, v, ok, st);
     if (STATS) {
         for (int k = 0; k < EPT; ++k) nfilt += ok[k];
         atomicAdd(&f.stats[0], (unsigned long long)nvalid);
@@ -268,157 +373,102 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
     }
 }
 
-// ---- XCD-local binned fold (steady state) ----
-// The filter's two lookups per edge into a V/8-byte bitmap are the steady-state cost; an 8 MiB
-// table is larger than one XCD's 4 MiB L2, so every XCD misses half of them to the Infinity
-// Cache. k_bin sorts a batch into 16 classes (quarter of u x quarter of v, one streaming pass);
-// k_fold_binned gives each XCD (block b runs on XCD b % 8 under round-robin dispatch — a speed
-// assumption only, any placement is correct) two classes whose lookups touch only two bitmap
-// quarters, V/16 bytes: L2-resident (tools/gather_bench.hip: 265 -> ~150 us per 2^24 edges).
-constexpr int kBinClasses = 16;
-__constant__ const uint8_t kGroupClasses[8][2] = {{0, 1}, {4, 5}, {2, 8}, {10, 11}, {14, 15}, {3, 12}, {6, 9}, {7, 13}};
-
-// Each class region is split into kBinLanes sub-regions; tile t appends to lane t % kBinLanes,
-// so the per-tile run reservations spread over 16 x 64 counters instead of 16 (one memory-side
-// atomic per tile and class; 4096 tiles on 16 words serialised ~50 us).
-constexpr int kBinLanes = 64;
-struct BinArgs {
-    uint32_t q1, q2, q3;                // quarter boundaries of the id space (multiples of 32)
-    uint32_t* bsrc;                     // kBinClasses x kBinLanes sub-regions of `sub` ids each
-    uint32_t* bdst;
-    uint64_t region;                    // ids per class = kBinLanes * sub
-    uint64_t sub;
-    unsigned long long* counts;         // [kBinClasses][kBinLanes] edge counts (zeroed before k_bin)
-};
-
-__device__ __forceinline__ uint32_t quarter(uint32_t x, const BinArgs& b) {
-    return (x >= b.q1) + (x >= b.q2) + (x >= b.q3);
-}
-
-// Local counting sort of a 4096-edge tile: each lane holds 16 edges; per edge slot, 16 ballots
-// rank the wave's lanes within each class; wave counts are combined in LDS into class runs; the
-// tile is staged class-major in LDS (32 KiB) and written out as one contiguous run per class
-// (coalesced, whole lines from one workgroup), after one global atomicAdd per class per tile.
-constexpr int kBinTile = 4096;
-constexpr int kBinPerLane = kBinTile / 256;
-__global__ __launch_bounds__(256) void k_bin(const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
-                                             uint64_t n, BinArgs bn, RangeCheck rc) {
-    __shared__ uint32_t st_src[kBinTile];
-    __shared__ uint32_t st_dst[kBinTile];
-    __shared__ uint32_t wcnt[4][kBinClasses];          // per wave, per class
-    __shared__ uint32_t cstart[kBinClasses + 1];        // class runs inside the tile
-    __shared__ unsigned long long gbase[kBinClasses];   // global position of each class run
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (uint64_t tile = (uint64_t)blockIdx.x * kBinTile; tile < n; tile += (uint64_t)gridDim.x * kBinTile) {
-        // lane l of wave w holds edges tile + w*1024 + k*64 + l, k = 0..15 (coalesced 256 B per k)
-        uint32_t u[kBinPerLane], v[kBinPerLane], c[kBinPerLane], r[kBinPerLane];
-        bool bad = false;
-        if (threadIdx.x < 4 * kBinClasses) (&wcnt[0][0])[threadIdx.x] = 0;
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < kBinPerLane; ++k) {
-            const uint64_t e = tile + wid * 1024 + k * 64 + lane;
-            const bool in = e < n;
-            u[k] = in ? __builtin_nontemporal_load(src + e) : 0u;
-            v[k] = in ? __builtin_nontemporal_load(dst + e) : 0u;
-            const bool ok = in && u[k] < rc.cap && v[k] < rc.cap;
-            bad |= in && !ok;
-            c[k] = ok ? 4 * quarter(u[k], bn) + quarter(v[k], bn) : 0xFFu;
-        }
-        if (bad) atomicOr(rc.err, 1u);
-#pragma unroll
-        for (int k = 0; k < kBinPerLane; ++k)           // rank inside (wave, class): LDS atomics
-            r[k] = (c[k] != 0xFFu) ? atomicAdd(&wcnt[wid][c[k]], 1u) : 0u;
-        __syncthreads();
-        const uint32_t blane = (uint32_t)((tile / kBinTile) % kBinLanes);
-        if (threadIdx.x < 64) {                          // wave 0: class totals, exclusive scan
-            const int q = threadIdx.x;
-            const uint32_t w0 = q < kBinClasses ? wcnt[0][q] : 0u, w1 = q < kBinClasses ? wcnt[1][q] : 0u;
-            const uint32_t w2 = q < kBinClasses ? wcnt[2][q] : 0u, w3 = q < kBinClasses ? wcnt[3][q] : 0u;
-            const uint32_t len = w0 + w1 + w2 + w3;
-            uint32_t incl = len;
-#pragma unroll
-            for (int off = 1; off < kBinClasses; off <<= 1) {
-                const uint32_t y = __shfl_up(incl, off, 64);
-                if (q >= off) incl += y;
-            }
-            if (q < kBinClasses) {
-                const uint32_t st = incl - len;
-                cstart[q] = st;
-                wcnt[0][q] = st; wcnt[1][q] = st + w0; wcnt[2][q] = st + w0 + w1; wcnt[3][q] = st + w0 + w1 + w2;
-                if (q == kBinClasses - 1) cstart[kBinClasses] = incl;
-                gbase[q] = len ? atomicAdd(&bn.counts[q * kBinLanes + blane], (unsigned long long)len) : 0ull;
-            }
-        }
-        __syncthreads();                                 // wcnt now holds run starts for every wave
-#pragma unroll
-        for (int k = 0; k < kBinPerLane; ++k) {
-            if (c[k] == 0xFFu) continue;
-            const uint32_t at = wcnt[wid][c[k]] + r[k];
-            st_src[at] = u[k];
-            st_dst[at] = v[k];
-        }
-        __syncthreads();
-        const uint32_t total = cstart[kBinClasses];
-        for (uint32_t i = threadIdx.x; i < total; i += 256) {
-            uint32_t q = 0;
-#pragma unroll
-            for (int b = 8; b > 0; b >>= 1)
-                if (q + b < kBinClasses && cstart[q + b] <= i) q += b;
-            const uint64_t at = (uint64_t)q * bn.region + (uint64_t)blane * bn.sub + gbase[q] + (i - cstart[q]);
-            bn.bsrc[at] = st_src[i];
-            bn.bdst[at] = st_dst[i];
-        }
-        __syncthreads();
+// Steady-state UpdateCC (mature forest, aligned uint32 SoA device edges): one 1024-thread
+// workgroup per CU (the hot set takes 128 KiB of its LDS, the survivor rings 16 KiB) streams the
+// edges, 16 B per lane, and filters each through the LDS hot set and gbits. A wave keeps its
+// survivors (edges not known to lie inside the giant) in a wave-private LDS ring and unions them
+// 64 at a time, one per lane, whenever the ring holds a wave's worth, while the CU's other waves
+// keep streaming: the unions' latency chains (parent walks, CAS) overlap the lookups, and run on
+// full waves instead of a few lanes of a filter pass (unions inline in the filter pass: 280 us
+// per steady RMAT-26 window; survivors queued for a second launch: 252 + 18-107 us; ring: 259 us).
+constexpr int kRingCap = 128;                       // pairs per wave: 16 waves x 1 KiB of LDS
+template <bool MARK, bool STATS>
+__device__ __forceinline__ void ring_flush(const FoldArgs& f, uint2* ring, uint32_t& cnt, uint32_t keep, FoldStats& st) {
+    const int lane = threadIdx.x & 63;
+    // the ring is written and read by different lanes of this wave: order those LDS accesses
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    while (cnt > keep) {                            // uniform
+        const uint32_t take = min(cnt - keep, 64u);
+        const uint32_t at = cnt - take;
+        const bool ok1 = (uint32_t)lane < take;
+        const uint2 e = ok1 ? ring[at + lane] : make_uint2(0u, 0u);
+        const uint32_t u[1] = {e.x}, v[1] = {e.y};
+        const bool ok[1] = {ok1};
+        union_group<MARK, STATS, 1>(f, u, v, ok, st);
+        cnt = at;
     }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
 }
 
 template <bool MARK, bool STATS>
-__global__ __launch_bounds__(kFoldThreads) void k_fold_binned(BinArgs bn, FoldArgs f) {
-    __shared__ unsigned long long pre[2 * kBinLanes + 1];   // edge prefix over the group's segments
-    const bool filt = *f.giant != kInvalid;
-    FoldStats st;
-    const uint32_t group = blockIdx.x & 7;
-    const uint32_t nb = gridDim.x >> 3, bi = blockIdx.x >> 3;
-    if (threadIdx.x < 64) {
-        // segment s = side * kBinLanes + lane; lane t sums segments t and t + 64 in two scans
-        unsigned long long carry = 0;
-#pragma unroll
-        for (int side = 0; side < 2; ++side) {
-            const uint32_t c = kGroupClasses[group][side];
-            const unsigned long long x = bn.counts[c * kBinLanes + threadIdx.x];
-            unsigned long long incl = x;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const unsigned long long y = __shfl_up(incl, off, 64);
-                if ((int)threadIdx.x >= off) incl += y;
-            }
-            pre[side * kBinLanes + threadIdx.x] = carry + incl - x;
-            carry += __shfl(incl, 63, 64);
-        }
-        if (threadIdx.x == 0) pre[2 * kBinLanes] = carry;
+__global__ __launch_bounds__(kHotThreads) void k_fold_ring(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
+                                                           FoldArgs f, HotArgs hot) {
+    __shared__ uint2 tab[kHotBuckets];
+    __shared__ uint2 rings[kHotThreads / 64][kRingCap];
+    const uint64_t n = f.n;
+    const bool filt = *f.giant != kInvalid;          // uniform
+    if (filt) {
+        for (uint32_t i = threadIdx.x; i < kHotBuckets; i += blockDim.x) tab[i] = hot.table[i];
     }
     __syncthreads();
-    const unsigned long long total = pre[2 * kBinLanes];
-    for (uint64_t g = (uint64_t)bi * blockDim.x + threadIdx.x; g * 4 < total; g += (uint64_t)nb * blockDim.x) {
-        uint32_t u[4], v[4];
-        bool ok[4];
+    const int lane = threadIdx.x & 63;
+    uint2* const ring = rings[threadIdx.x >> 6];
+    uint32_t cnt = 0;                                // wave-uniform ring fill
+    FoldStats st;
+    const uint64_t groups = n / 4;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t nvalid = 0, nkept = 0;
+    for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < groups; g0 += stride) {
+        const uint64_t g = g0 + lane;
+        uint32_t u[4] = {0, 0, 0, 0}, v[4] = {0, 0, 0, 0};
+        bool ok[4] = {false, false, false, false};
+        if (g < groups) {
+            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a) + g);
+            const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b) + g);
+            u[0] = x.x; u[1] = x.y; u[2] = x.z; u[3] = x.w;
+            v[0] = y.x; v[1] = y.y; v[2] = y.z; v[3] = y.w;
+            bool bad = false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                ok[k] = u[k] < f.rc.cap && v[k] < f.rc.cap;
+                bad |= !ok[k];
+                if (!ok[k]) { u[k] = 0; v[k] = 0; }
+            }
+            if (bad) atomicOr(f.rc.err, 1u);
+        }
+        if (STATS) for (int k = 0; k < 4; ++k) nvalid += ok[k];
+        if (filt) filter_group<STATS, 4, true>(f, u, v, ok, tab, hot, g * 4 < kHotSampleEdges);
+        const uint32_t c = (uint32_t)ok[0] + ok[1] + ok[2] + ok[3];
+        if (STATS) nkept += c;
+        uint32_t incl = c;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        const uint32_t wtot = __shfl(incl, 63, 64);
+        if (wtot == 0) continue;                     // uniform
+        if (wtot > kRingCap / 2) {                   // young window: union in place
+            union_group<MARK, STATS, 4>(f, u, v, ok, st);
+            continue;
+        }
+        if (cnt + wtot > kRingCap) ring_flush<MARK, STATS>(f, ring, cnt, kRingCap - wtot, st);
+        uint32_t pos = cnt + incl - c;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const unsigned long long e = g * 4 + k;
-            ok[k] = e < total;
-            uint32_t sidx = 0;                                // last segment with pre <= e
-#pragma unroll
-            for (int b = 64; b > 0; b >>= 1)
-                if (sidx + b < 2 * kBinLanes && pre[sidx + b] <= e) sidx += b;
-            const uint32_t c = kGroupClasses[group][sidx / kBinLanes];
-            const uint64_t at = (uint64_t)c * bn.region + (uint64_t)(sidx % kBinLanes) * bn.sub + (ok[k] ? e - pre[sidx] : 0);
-            u[k] = ok[k] ? __builtin_nontemporal_load(bn.bsrc + at) : 0u;
-            v[k] = ok[k] ? __builtin_nontemporal_load(bn.bdst + at) : 0u;
+            if (!ok[k]) continue;
+            ring[pos] = make_uint2(u[k], v[k]);
+            ++pos;
         }
-        fold_group<MARK, STATS, 4>(f, filt, u, v, ok, st);
+        cnt += wtot;
+        if (cnt >= 64) ring_flush<MARK, STATS>(f, ring, cnt, cnt - 64, st);
     }
+    ring_flush<MARK, STATS>(f, ring, cnt, 0, st);
     if (STATS) {
+        atomicAdd(&f.stats[0], nvalid);
+        atomicAdd(&f.stats[1], nvalid - nkept);
         atomicAdd(&f.stats[2], (unsigned long long)st.early);
         atomicAdd(&f.stats[3], (unsigned long long)st.hooks);
         atomicAdd(&f.stats[4], (unsigned long long)st.casfail);
@@ -453,17 +503,21 @@ constexpr int kPickSlots = 2048;
 // (components only merge, so the sampled giant stays the component holding its old root; the
 // host re-samples every kPickEvery closes in case another component overtook it).
 constexpr int kPickEvery = 8;
+// giant[2] = the root of the component the hot set's entries belong to (kInvalid: none yet); a
+// pick of another component clears the hot set (the tail of this kernel).
 __global__ __launch_bounds__(1024) void k_pick_giant(const uint32_t* __restrict__ parent, uint32_t n,
-                                                    uint32_t* __restrict__ giant, int follow) {
+                                                    uint32_t* __restrict__ giant, int follow, uint2* __restrict__ hot) {
     if (follow && giant[0] != kInvalid) {       // uniform over the block
         if (threadIdx.x == 0) {
             const uint32_t g0 = giant[0];
             const uint32_t g = find_root_ro(parent, g0);
             giant[1] = (g == g0) ? 1u : 0u;
             giant[0] = g;
+            giant[2] = g;
         }
         return;
     }
+    __shared__ uint32_t clear_hot;
     __shared__ uint32_t keys[kPickSlots];
     __shared__ uint32_t cnt[kPickSlots];
     __shared__ unsigned long long best[16];
@@ -506,6 +560,14 @@ __global__ __launch_bounds__(1024) void k_pick_giant(const uint32_t* __restrict_
         const uint32_t g = (c >= 16 && 4 * c >= seen_total) ? (uint32_t)b : kInvalid;
         giant[1] = (g != kInvalid && g == giant[0]) ? 1u : 0u;
         giant[0] = g;
+        const uint32_t owner = giant[2];
+        const bool other = g != kInvalid && (owner == kInvalid || find_root_ro(parent, owner) != g);
+        clear_hot = other ? 1u : 0u;
+        if (g != kInvalid) giant[2] = g;
+    }
+    __syncthreads();
+    if (clear_hot && hot) {
+        for (uint32_t i = threadIdx.x; i < kHotBuckets; i += blockDim.x) hot[i] = make_uint2(0u, 0u);
     }
 }
 

@@ -397,8 +397,11 @@ def test_bench_two_ranks_one_gpu_verified():
 
 
 # ---------------- opt-in fold variants, end to end against the independent torch CC ----------------
-@pytest.mark.parametrize("env", [{"GSGPU_FOLD_BIN": "1"}, {"GSGPU_FOLD_STATS": "1"}, {"GSGPU_FOLD_EPT": "8"}],
-                         ids=["binned", "stats", "ept8"])
+@pytest.mark.parametrize("env", [{"GSGPU_FOLD_MODE": "plain"}, {"GSGPU_FOLD_MODE": "ring"},
+                                 {"GSGPU_FOLD_MODE": "ring", "GSGPU_FOLD_STATS": "1"},
+                                 {"GSGPU_FOLD_MODE": "plain", "GSGPU_FOLD_STATS": "1"},
+                                 {"GSGPU_FOLD_MODE": "plain", "GSGPU_FOLD_EPT": "8"}, {"GSGPU_TIMING": "marker"}],
+                         ids=["plain", "ring", "ring_stats", "plain_stats", "plain_ept8", "marker_timing"])
 def test_fold_variants_verified(env):
     import subprocess, sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
