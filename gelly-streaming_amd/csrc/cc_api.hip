@@ -11,6 +11,9 @@
 #include <hip/hip_ext.h>
 
 #include "cc_kernels.hpp"
+#include "sparse_ids.hpp"
+
+#include <hipcub/hipcub.hpp>
 
 namespace gsgpu {
 
@@ -75,6 +78,13 @@ struct gs_cc {
     uint32_t hot_bits = 0;               // ids < 2^hot_bits
     uint32_t* hot_cand = nullptr;        // hot-set admission candidates (2^kHotCandBits ids)
     int cus = 0;                         // compute units: k_fold_ring grid
+    // GS_CC_SPARSE_IDS: id -> slot table; cap (above) = slots = 2^hbits + 1
+    bool sparse = false;
+    int64_t* keys = nullptr;             // 2^hbits slot keys (INT64_MIN = empty)
+    uint32_t hbits = 0;
+    unsigned long long* nkeys = nullptr; // distinct ids inserted
+    int64_t* minkey = nullptr;           // per root: minimum id of its component (emission)
+    bool minkey_valid = false;
     // instrumentation
     bool timing = false;
     struct Pend { int k; hipEvent_t a, b; };
@@ -160,8 +170,12 @@ int sync_and_check(gs_cc_t* h) {
     GS_HIP(hipMemcpyAsync(hflag, h->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
     GS_HIP(hipStreamSynchronize(h->stream));
     if (*hflag) {
+        const uint32_t f = *hflag;
         *hflag = 0;
         GS_HIP(hipMemsetAsync(h->derr, 0, sizeof(uint32_t), h->stream));
+        if (f & 2u)
+            return fail(GS_ERR_CAPACITY, "more than %llu distinct ids were folded into a sparse-id summary",
+                        (unsigned long long)h->cfg.vertex_capacity);
         return fail(GS_ERR_RANGE, "a vertex id outside [0, %u) was folded; such edges were skipped", h->cap);
     }
     return GS_OK;
@@ -271,7 +285,41 @@ void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, siz
     }
 }
 
+SparseArgs sparse_args(gs_cc_t* h) {
+    return SparseArgs{h->keys, h->hbits, h->nkeys, h->cfg.vertex_capacity, h->derr};
+}
+
+// UpdateCC over arbitrary int64 ids (GS_CC_SPARSE_IDS), young-forest split as for dense ids
+void launch_fold_sparse(gs_cc_t* h, const int64_t* a, const int64_t* b, uint64_t n, bool aos) {
+    const SparseArgs sa = sparse_args(h);
+    const uint64_t young_limit = h->cfg.vertex_capacity / 4;
+    uint64_t off = 0;
+    while (off < n) {
+        uint64_t m = n - off;
+        if (h->edges_since_reset < young_limit)
+            m = std::min(m, std::max<uint64_t>(std::min(kYoungChunk, young_limit - h->edges_since_reset), 1));
+        FoldArgs f{m, h->parent, h->mark, h->sbits, h->gbits, h->derr + 1, RangeCheck{h->cap, h->derr}, h->dstats};
+        const unsigned grid = grid_for((m + 1) / 2, 256, 16384);
+        KTimer t(h, GS_K_FOLD);
+        const int64_t* pa = a + (aos ? 2 * off : off);
+        const int64_t* pb = aos ? nullptr : b + off;
+        if (aos) {
+            if (h->mark) klaunch(k_fold_sparse<true, true>, dim3(grid), dim3(256), h->stream, t.start(), t.stop(), pa, pb, f, sa);
+            else klaunch(k_fold_sparse<true, false>, dim3(grid), dim3(256), h->stream, t.start(), t.stop(), pa, pb, f, sa);
+        } else {
+            if (h->mark) klaunch(k_fold_sparse<false, true>, dim3(grid), dim3(256), h->stream, t.start(), t.stop(), pa, pb, f, sa);
+            else klaunch(k_fold_sparse<false, false>, dim3(grid), dim3(256), h->stream, t.start(), t.stop(), pa, pb, f, sa);
+        }
+        h->edges_since_reset += m;
+        off += m;
+    }
+}
+
 void launch_fold_any(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, uint32_t id_bits) {
+    if (h->sparse) {
+        launch_fold_sparse(h, static_cast<const int64_t*>(a), static_cast<const int64_t*>(b), n, aos);
+        return;
+    }
     const char* ca = static_cast<const char*>(a);
     const char* cb = static_cast<const char*>(b);
     if (id_bits == 32) {
@@ -288,9 +336,11 @@ int fold_impl(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, ui
     if (n == 0) return GS_OK;
     if (!a || (!aos && !b)) return fail(GS_ERR_INVALID, "fold: null edge buffer");
     DeviceGuard g(h->device);
+    if (h->sparse && id_bits != 64) return fail(GS_ERR_UNSUPPORTED, "fold: a sparse-id summary takes 64-bit ids");
     const size_t esz = id_bits / 8;
     const bool dev = is_device_pointer(a) && (aos || is_device_pointer(b));
     h->compressed = false;
+    h->minkey_valid = false;
     if (dev) {
         launch_fold_any(h, a, b, n, aos, id_bits);
         GS_HIP(hipGetLastError());
@@ -341,7 +391,34 @@ int compress_impl(gs_cc_t* h) {
     return GS_OK;
 }
 
+// sparse ids: close the window, then minkey[root] = minimum id of every component
+int ensure_minkey(gs_cc_t* h) {
+    GS_TRY(compress_impl(h));
+    if (h->minkey_valid) return GS_OK;
+    const SparseArgs sa = sparse_args(h);
+    const dim3 grid(grid_for(h->cap, 256, 16384));
+    hipLaunchKernelGGL(k_minkey_init, grid, dim3(256), 0, h->stream, (const uint32_t*)h->parent, h->cap, sa, h->minkey);
+    hipLaunchKernelGGL(k_minkey_reduce, grid, dim3(256), 0, h->stream, (const uint32_t*)h->parent, h->cap, sa,
+                       (const uint32_t*)(h->derr + 1), h->minkey);
+    GS_HIP(hipGetLastError());
+    h->minkey_valid = true;
+    return GS_OK;
+}
+
 int stats_impl(gs_cc_t* h, bool checksum, uint64_t* nv, uint64_t* nc, uint64_t* sum) {
+    if (h->sparse && checksum) {
+        GS_TRY(ensure_minkey(h));
+        GS_HIP(hipMemsetAsync(h->dscratch, 0, 3 * sizeof(unsigned long long), h->stream));
+        hipLaunchKernelGGL(k_stats_sparse, dim3(grid_for(h->cap, 256, 4096)), dim3(256), 0, h->stream,
+                           (const uint32_t*)h->parent, h->cap, sparse_args(h), (const int64_t*)h->minkey, h->dscratch);
+        GS_HIP(hipGetLastError());
+        GS_HIP(hipMemcpyAsync(h->hscratch, h->dscratch, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
+        GS_TRY(sync_and_check(h));
+        if (nv) *nv = h->hscratch[0];
+        if (nc) *nc = h->hscratch[1];
+        if (sum) *sum = h->hscratch[2];
+        return GS_OK;
+    }
     GS_HIP(hipMemsetAsync(h->dscratch, 0, 3 * sizeof(unsigned long long), h->stream));
     const dim3 grid(grid_for(h->cap, 256, 4096));
     if (checksum) hipLaunchKernelGGL(k_stats<true>, grid, dim3(256), 0, h->stream, h->parent, h->cap, h->dscratch);
@@ -361,6 +438,67 @@ int copy_out(gs_cc_t* h, void* dst, const void* src, size_t n) {
     return GS_OK;
 }
 
+int emit_pairs_sparse(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uint64_t* n_out) {
+    GS_TRY(ensure_minkey(h));
+    uint64_t nv = 0;
+    GS_TRY(stats_impl(h, false, &nv, nullptr, nullptr));
+    *n_out = nv;
+    const uint64_t w = nv < cap ? nv : cap;
+    if (nv) {
+        // tmp: [counter][keys in][labels in][keys out][labels out][radix-sort temp]
+        size_t sort_bytes = 0;
+        GS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (const int64_t*)nullptr, (int64_t*)nullptr,
+                                                   (const int64_t*)nullptr, (int64_t*)nullptr, (int)nv, 0, 64, h->stream));
+        const size_t arr = ((nv * 8) + 255) & ~(size_t)255;
+        GS_TRY(ensure_buf(&h->tmp, &h->tmp_bytes, 256 + 4 * arr + sort_bytes));
+        char* base = static_cast<char*>(h->tmp);
+        auto* counter = reinterpret_cast<unsigned long long*>(base);
+        auto* ki = reinterpret_cast<int64_t*>(base + 256);
+        auto* li = reinterpret_cast<int64_t*>(base + 256 + arr);
+        auto* ko = reinterpret_cast<int64_t*>(base + 256 + 2 * arr);
+        auto* lo = reinterpret_cast<int64_t*>(base + 256 + 3 * arr);
+        void* st = base + 256 + 4 * arr;
+        GS_HIP(hipMemsetAsync(counter, 0, 8, h->stream));
+        hipLaunchKernelGGL(k_emit_sparse, dim3(grid_for(h->cap, 256, 16384)), dim3(256), 0, h->stream,
+                           (const uint32_t*)h->parent, h->cap, sparse_args(h), (const int64_t*)h->minkey, ki, li, counter);
+        GS_HIP(hipGetLastError());
+        GS_HIP(hipcub::DeviceRadixSort::SortPairs(st, sort_bytes, (const int64_t*)ki, ko, (const int64_t*)li, lo, (int)nv,
+                                                   0, 64, h->stream));
+        if (w) {
+            GS_TRY(copy_out(h, vertices, ko, w * 8));
+            GS_TRY(copy_out(h, labels, lo, w * 8));
+        }
+    }
+    GS_TRY(sync_and_check(h));
+    if (nv > cap) return fail(GS_ERR_CAPACITY, "gs_cc_emit_pairs: %llu pairs, capacity %llu",
+                              (unsigned long long)nv, (unsigned long long)cap);
+    return GS_OK;
+}
+
+int find_sparse(gs_cc_t* h, const int64_t* ids, int64_t* roots, uint8_t* found, uint64_t n) {
+    GS_TRY(ensure_minkey(h));
+    const bool dev = is_device_pointer(ids) && is_device_pointer(roots) && (!found || is_device_pointer(found));
+    const int64_t* di = ids;
+    int64_t* dr = roots;
+    uint8_t* df = found;
+    if (!dev) {
+        GS_TRY(ensure_buf(&h->tmp, &h->tmp_bytes, 2 * n * 8 + n));
+        di = static_cast<const int64_t*>(h->tmp);
+        dr = static_cast<int64_t*>(h->tmp) + n;
+        df = found ? reinterpret_cast<uint8_t*>(static_cast<int64_t*>(h->tmp) + 2 * n) : nullptr;
+        GS_HIP(hipMemcpyAsync(const_cast<int64_t*>(di), ids, n * 8,
+                              is_device_pointer(ids) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->stream));
+    }
+    hipLaunchKernelGGL(k_find_sparse, dim3(grid_for(n, 256, 16384)), dim3(256), 0, h->stream, di, dr, df, n,
+                       (const uint32_t*)h->parent, sparse_args(h), (const int64_t*)h->minkey);
+    GS_HIP(hipGetLastError());
+    if (!dev) {
+        GS_TRY(copy_out(h, roots, dr, n * 8));
+        if (found) GS_TRY(copy_out(h, found, df, n));
+    }
+    return sync_and_check(h);
+}
+
 }  // namespace
 
 extern "C" {
@@ -374,6 +512,10 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
     if (cfg->struct_size != sizeof(gs_cc_config))
         return fail(GS_ERR_INVALID, "gs_cc_create: struct_size %u != %zu", cfg->struct_size, sizeof(gs_cc_config));
     if (cfg->id_bits != 32 && cfg->id_bits != 64) return fail(GS_ERR_INVALID, "gs_cc_create: id_bits must be 32 or 64");
+    const bool sparse = (cfg->flags & GS_CC_SPARSE_IDS) != 0;
+    if (sparse && cfg->id_bits != 64) return fail(GS_ERR_INVALID, "gs_cc_create: GS_CC_SPARSE_IDS needs id_bits 64");
+    if (sparse && (cfg->vertex_capacity == 0 || cfg->vertex_capacity > (1ull << 30)))
+        return fail(GS_ERR_INVALID, "gs_cc_create: sparse vertex_capacity must be in [1, 2^30]");
     if (cfg->vertex_capacity == 0 || cfg->vertex_capacity > 0xFFFFFFFFull)
         return fail(GS_ERR_INVALID, "gs_cc_create: vertex_capacity must be in [1, 2^32-1]");
     int ndev = 0;
@@ -388,6 +530,12 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
     h->cfg = *cfg;
     h->cap = (uint32_t)cfg->vertex_capacity;
     h->device = cfg->device;
+    if (sparse) {                        // slots: 2^hbits >= 2 x capacity, + the INT64_MIN slot
+        h->sparse = true;
+        h->hbits = 4;
+        while ((1ull << h->hbits) < 2 * cfg->vertex_capacity) ++h->hbits;
+        h->cap = (1u << h->hbits) + 1;
+    }
     auto bail = [&](int rc) { gs_cc_destroy(h); return rc; };
     if (hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess) return bail(fail(GS_ERR_HIP, "hipStreamCreate failed"));
     h->stream = h->own;
@@ -402,11 +550,17 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
         return bail(fail(GS_ERR_NOMEM, "scratch allocation failed"));
     }
     std::memset(h->hscratch, 0, 8 * sizeof(unsigned long long));
+    if (sparse && (hipMalloc(&h->keys, sizeof(int64_t) << h->hbits) != hipSuccess ||
+                   hipMalloc(&h->minkey, sizeof(int64_t) * (size_t)h->cap) != hipSuccess ||
+                   hipMalloc(&h->nkeys, sizeof(unsigned long long)) != hipSuccess)) {
+        (void)hipGetLastError();
+        return bail(fail(GS_ERR_NOMEM, "sparse id table (2^%u slots) allocation failed", h->hbits));
+    }
     if (hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, cfg->device) != hipSuccess) h->cus = 0;
     {
         uint32_t bits = 0;
         while (bits < 32 && (1ull << bits) < (uint64_t)h->cap) ++bits;
-        if (bits >= 20 && bits <= kHotBucketBits + 15) {     // remainders fit 15 bits (+1 in 16)
+        if (!sparse && bits >= 20 && bits <= kHotBucketBits + 15) {     // remainders fit 15 bits (+1 in 16)
             if (hipMalloc(&h->hot, kHotBuckets * sizeof(uint2)) != hipSuccess ||
                 hipMalloc(&h->hot_cand, sizeof(uint32_t) << kHotCandBits) != hipSuccess) {
                 (void)hipGetLastError();
@@ -441,6 +595,9 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->dstats) (void)hipFree(h->dstats);
     if (h->hot) (void)hipFree(h->hot);
     if (h->hot_cand) (void)hipFree(h->hot_cand);
+    if (h->keys) (void)hipFree(h->keys);
+    if (h->minkey) (void)hipFree(h->minkey);
+    if (h->nkeys) (void)hipFree(h->nkeys);
     if (h->dscratch) (void)hipFree(h->dscratch);
     if (h->hscratch) (void)hipHostFree(h->hscratch);
     if (h->stage) (void)hipFree(h->stage);
@@ -462,7 +619,14 @@ int gs_cc_reset(gs_cc_t* h) {
     GS_HIP(hipMemsetAsync(h->derr + 3, 0xFF, 4, h->stream));       // hot set owner: none
     if (h->hot) GS_HIP(hipMemsetAsync(h->hot, 0, kHotBuckets * sizeof(uint2), h->stream));
     if (h->hot_cand) GS_HIP(hipMemsetAsync(h->hot_cand, 0xFF, sizeof(uint32_t) << kHotCandBits, h->stream));
+    if (h->sparse) {
+        hipLaunchKernelGGL(k_fill64, dim3(grid_for(1ull << h->hbits, 256, 4096)), dim3(256), 0, h->stream, h->keys,
+                           (uint64_t)1 << h->hbits, kEmptyKey);
+        GS_HIP(hipGetLastError());
+        GS_HIP(hipMemsetAsync(h->nkeys, 0, sizeof(unsigned long long), h->stream));
+    }
     h->compressed = true;
+    h->minkey_valid = false;
     h->edges_since_reset = 0;
     h->closes = 0;
     return GS_OK;
@@ -507,7 +671,9 @@ int gs_cc_merge(gs_cc_t* into, gs_cc_t* from) {
     GS_TRY(check(from));
     if (into == from) return GS_OK;
     if (into->device != from->device) return fail(GS_ERR_UNSUPPORTED, "gs_cc_merge: summaries on different devices");
-    if (from->cap > into->cap) return fail(GS_ERR_RANGE, "gs_cc_merge: source capacity %u exceeds target %u", from->cap, into->cap);
+    if (into->sparse != from->sparse) return fail(GS_ERR_UNSUPPORTED, "gs_cc_merge: sparse-id and dense-id summaries do not mix");
+    if (!into->sparse && from->cap > into->cap)
+        return fail(GS_ERR_RANGE, "gs_cc_merge: source capacity %u exceeds target %u", from->cap, into->cap);
     DeviceGuard g(into->device);
     if (from->stream != into->stream) {
         hipEvent_t e = get_event(into);
@@ -516,7 +682,14 @@ int gs_cc_merge(gs_cc_t* into, gs_cc_t* from) {
         into->pool.push_back(e);
     }
     into->compressed = false;
-    {
+    into->minkey_valid = false;
+    if (into->sparse) {
+        KTimer t(into, GS_K_MERGE);
+        const dim3 grid(grid_for(from->cap, 256, 16384));
+        FoldArgs f{0, into->parent, into->mark, into->sbits, into->gbits, into->derr + 1, RangeCheck{into->cap, into->derr}, nullptr};
+        if (into->mark) klaunch(k_merge_sparse<true>, grid, dim3(256), into->stream, t.start(), t.stop(), (const uint32_t*)from->parent, sparse_args(from), f, sparse_args(into));
+        else klaunch(k_merge_sparse<false>, grid, dim3(256), into->stream, t.start(), t.stop(), (const uint32_t*)from->parent, sparse_args(from), f, sparse_args(into));
+    } else {
         KTimer t(into, GS_K_MERGE);
         const dim3 grid(grid_for(from->cap, 256, 16384));
         if (into->mark) klaunch(k_merge_dense<true>, grid, dim3(256), into->stream, t.start(), t.stop(), (const uint32_t*)from->parent, from->cap, into->parent, into->mark, into->sbits);
@@ -566,6 +739,7 @@ int gs_cc_checksum(gs_cc_t* h, uint64_t* sum, uint64_t* nv, uint64_t* nc) {
 int gs_cc_emit_dense(gs_cc_t* h, void* labels, uint64_t n) {
     GS_TRY(check(h));
     if (n && !labels) return fail(GS_ERR_INVALID, "gs_cc_emit_dense: null output");
+    if (h->sparse) return fail(GS_ERR_UNSUPPORTED, "gs_cc_emit_dense: sparse-id summary (use gs_cc_emit_pairs)");
     DeviceGuard g(h->device);
     GS_TRY(compress_impl(h));
     const uint64_t m = n < h->cap ? n : h->cap;
@@ -594,6 +768,7 @@ int gs_cc_emit_pairs(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uin
     if (!n_out) return fail(GS_ERR_INVALID, "gs_cc_emit_pairs: null n_out");
     if (cap && (!vertices || !labels)) return fail(GS_ERR_INVALID, "gs_cc_emit_pairs: null output");
     DeviceGuard g(h->device);
+    if (h->sparse) return emit_pairs_sparse(h, vertices, labels, cap, n_out);
     GS_TRY(compress_impl(h));
     const uint32_t ntiles = (uint32_t)((h->cap + kTile - 1) / kTile);
     const size_t esz = h->cfg.id_bits / 8;
@@ -644,10 +819,15 @@ int gs_cc_emit_pairs(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uin
 }
 
 int gs_cc_find(gs_cc_t* h, const void* ids, void* roots, uint64_t n) {
+    return gs_cc_find_flags(h, ids, roots, nullptr, n);
+}
+
+int gs_cc_find_flags(gs_cc_t* h, const void* ids, void* roots, uint8_t* found, uint64_t n) {
     GS_TRY(check(h));
     if (n == 0) return GS_OK;
     if (!ids || !roots) return fail(GS_ERR_INVALID, "gs_cc_find: null buffer");
     DeviceGuard g(h->device);
+    if (h->sparse) return find_sparse(h, static_cast<const int64_t*>(ids), static_cast<int64_t*>(roots), found, n);
     const size_t esz = h->cfg.id_bits / 8;
     const bool dev = is_device_pointer(ids) && is_device_pointer(roots);
     const void* di = ids;
@@ -665,12 +845,24 @@ int gs_cc_find(gs_cc_t* h, const void* ids, void* roots, uint64_t n) {
         hipLaunchKernelGGL(k_find<int64_t>, grid, dim3(256), 0, h->stream, (const int64_t*)di, (int64_t*)dr, n, h->parent, h->cap);
     GS_HIP(hipGetLastError());
     if (!dev) GS_TRY(copy_out(h, roots, dr, n * esz));
-    return sync_and_check(h);
+    GS_TRY(sync_and_check(h));
+    if (found) {                           // dense ids: found <=> label != -1 (ids are < 2^32 - 1)
+        const bool host_roots = !is_device_pointer(roots);
+        if (host_roots && !is_device_pointer(found)) {
+            for (uint64_t i = 0; i < n; ++i)
+                found[i] = esz == 4 ? (static_cast<const uint32_t*>(roots)[i] != 0xFFFFFFFFu)
+                                    : (static_cast<const int64_t*>(roots)[i] >= 0);
+        } else {
+            return fail(GS_ERR_UNSUPPORTED, "gs_cc_find_flags: found flags for device buffers need a sparse-id summary");
+        }
+    }
+    return GS_OK;
 }
 
 int gs_cc_labels_device(gs_cc_t* h, const void** p) {
     GS_TRY(check(h));
     if (!p) return fail(GS_ERR_INVALID, "null out");
+    if (h->sparse) return fail(GS_ERR_UNSUPPORTED, "gs_cc_labels_device: sparse-id summary (labels are per slot)");
     *p = h->parent;
     return GS_OK;
 }
@@ -679,6 +871,7 @@ int gs_cc_export_marks(gs_cc_t* h, void* pairs, uint64_t cap, uint64_t* n_out) {
     GS_TRY(check(h));
     if (!n_out) return fail(GS_ERR_INVALID, "gs_cc_export_marks: null n_out");
     if (!h->mark) return fail(GS_ERR_UNSUPPORTED, "gs_cc_export_marks: handle created without GS_CC_TRACK_MARKS");
+    if (h->sparse) return fail(GS_ERR_UNSUPPORTED, "gs_cc_export_marks: sparse-id summary");
     if (cap && !pairs) return fail(GS_ERR_INVALID, "gs_cc_export_marks: null output");
     DeviceGuard g(h->device);
     const bool dev = cap == 0 || is_device_pointer(pairs);

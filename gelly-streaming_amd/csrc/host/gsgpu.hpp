@@ -43,7 +43,8 @@ inline void check(int rc, const char* where) {
     if (rc != GS_OK) throw GsError(rc, where);
 }
 
-// DisjointSet<K> on the device. K = int32_t or int64_t ids in [0, capacity).
+// DisjointSet<K> on the device. K = int32_t or int64_t ids in [0, capacity); with
+// flags = GS_CC_SPARSE_IDS (K = int64_t) any long id, at most `capacity` distinct ones.
 template <typename K>
 class DisjointSet {
     static_assert(std::is_same<K, int32_t>::value || std::is_same<K, int64_t>::value, "K must be int32_t or int64_t");
@@ -77,8 +78,9 @@ public:
     // find (:66-80): root, or nullopt for an unknown id (Java null)
     std::optional<K> find(K e) {
         K r = -1;
-        check(gs_cc_find(h_, &e, &r, 1), "gs_cc_find");
-        if (r < 0) return std::nullopt;
+        uint8_t found = 0;
+        check(gs_cc_find_flags(h_, &e, &r, &found, 1), "gs_cc_find_flags");
+        if (!found) return std::nullopt;
         return r;
     }
 

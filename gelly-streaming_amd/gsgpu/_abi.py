@@ -23,6 +23,7 @@ GS_ERR_UNSUPPORTED = -6
 GS_ERR_CAPACITY = -7
 
 GS_CC_TRACK_MARKS = 1
+GS_CC_SPARSE_IDS = 2
 
 GS_K_FOLD, GS_K_COMPRESS, GS_K_MERGE, GS_K_EXPORT = 0, 1, 2, 3
 
@@ -35,7 +36,7 @@ EXPORTED_SYMBOLS = (
     "gs_cc_create", "gs_cc_destroy", "gs_cc_reset", "gs_cc_set_stream", "gs_cc_get_stream",
     "gs_cc_sync", "gs_cc_fold", "gs_cc_fold_pairs", "gs_cc_merge", "gs_cc_combine",
     "gs_cc_close_window", "gs_cc_stats", "gs_cc_emit_dense", "gs_cc_emit_pairs",
-    "gs_cc_checksum", "gs_cc_find", "gs_cc_labels_device", "gs_cc_export_marks",
+    "gs_cc_checksum", "gs_cc_find", "gs_cc_find_flags", "gs_cc_labels_device", "gs_cc_export_marks",
     "gs_cc_fold_pairs32", "gs_cc_timing", "gs_cc_kernel_time", "gs_gen_rmat", "gs_gen_er", "gs_parse_edges",
     "gs_last_error", "gs_version",
 )
@@ -91,6 +92,7 @@ def lib() -> ctypes.CDLL:
         "gs_cc_emit_pairs": [vp, vp, vp, u64, P(u64)],
         "gs_cc_checksum": [vp, P(u64), P(u64), P(u64)],
         "gs_cc_find": [vp, vp, vp, u64],
+        "gs_cc_find_flags": [vp, vp, vp, vp, u64],
         "gs_cc_labels_device": [vp, P(vp)],
         "gs_cc_export_marks": [vp, vp, u64, P(u64)],
         "gs_cc_timing": [vp, i32],

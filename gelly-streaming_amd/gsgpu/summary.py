@@ -64,15 +64,18 @@ def _stream_ptr(stream) -> Optional[int]:
 
 
 class DisjointSet:
-    """GPU union-find summary (DisjointSet<K>), K = int32 or int64 vertex ids in [0, capacity)."""
+    """GPU union-find summary (DisjointSet<K>), K = int32 or int64 vertex ids in [0, capacity);
+    ``sparse=True`` (64-bit ids only): ANY Java long ids, at most ``vertex_capacity`` distinct."""
 
     def __init__(self, vertex_capacity: int, id_bits: int = 64, device: int = 0,
-                 track_marks: bool = False, stream=None, staging_edges: int = 0):
+                 track_marks: bool = False, stream=None, staging_edges: int = 0, sparse: bool = False):
         self.id_bits = int(id_bits)
         self.capacity = int(vertex_capacity)
         self.device = int(device)
-        cfg = GsCcConfig(ctypes.sizeof(GsCcConfig), self.id_bits, self.capacity, self.device,
-                         _abi.GS_CC_TRACK_MARKS if track_marks else 0, int(staging_edges))
+        self.sparse = bool(sparse)
+        flags = (_abi.GS_CC_TRACK_MARKS if track_marks else 0) | (_abi.GS_CC_SPARSE_IDS if sparse else 0)
+        cfg = GsCcConfig(ctypes.sizeof(GsCcConfig), self.id_bits, self.capacity, self.device, flags,
+                         int(staging_edges))
         h = ctypes.c_void_p()
         call("gs_cc_create", ctypes.byref(h), ctypes.byref(cfg))
         self._h = h
@@ -119,6 +122,9 @@ class DisjointSet:
 
     def find(self, e: int) -> Optional[int]:
         """find (:66-80): root of e, or None if e is not in the summary."""
+        if self.sparse:
+            r, found = self.find_batch_flags(np.array([e], dtype=np.int64))
+            return int(r[0]) if found[0] else None
         r = self.find_batch(np.array([e]))
         return None if int(r[0]) < 0 else int(r[0])
 
@@ -127,6 +133,16 @@ class DisjointSet:
         out = np.empty(n, dtype=np.uint32 if self.id_bits == 32 else np.int64)
         call("gs_cc_find", self.handle, p, out.ctypes.data_as(ctypes.c_void_p), n)
         return out.view(np.int32).astype(np.int64) if self.id_bits == 32 else out
+
+    def find_batch_flags(self, ids) -> Tuple[np.ndarray, np.ndarray]:
+        """(labels, found): found[i] False where ids[i] is not in the summary (null)."""
+        p, keep, n = _buf(ids, self.id_bits, "ids")
+        out = np.empty(n, dtype=np.uint32 if self.id_bits == 32 else np.int64)
+        found = np.empty(n, dtype=np.uint8)
+        call("gs_cc_find_flags", self.handle, p, out.ctypes.data_as(ctypes.c_void_p),
+             found.ctypes.data_as(ctypes.c_void_p), n)
+        lab = out.view(np.int32).astype(np.int64) if self.id_bits == 32 else out
+        return lab, found.astype(bool)
 
     def merge(self, other: "DisjointSet") -> None:
         """merge (:127-131): union every (key, parent) of ``other`` into this summary."""

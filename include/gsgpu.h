@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GSGPU_VERSION 1
+#define GSGPU_VERSION 2
 
 enum {
     GS_OK = 0,
@@ -56,8 +56,14 @@ enum {
 
 /* gs_cc_config.flags */
 enum {
-    GS_CC_TRACK_MARKS = 1u << 0  /* keep per-vertex marks of this window's hooks, needed by
+    GS_CC_TRACK_MARKS = 1u << 0, /* keep per-vertex marks of this window's hooks, needed by
                                     gs_cc_export_marks (multi-GPU / multi-handle merge)    */
+    GS_CC_SPARSE_IDS = 1u << 1   /* id_bits 64 only: ids are ANY 64-bit values (Java long,
+                                    negatives included), hashed to slots on the device;
+                                    vertex_capacity = most distinct ids (<= 2^30). Canonical
+                                    labels are still the minimum id of each component.
+                                    gs_cc_emit_dense, gs_cc_export_marks and
+                                    gs_cc_labels_device are not available in this mode.      */
 };
 
 typedef struct gs_cc gs_cc_t;
@@ -65,7 +71,8 @@ typedef struct gs_cc gs_cc_t;
 typedef struct gs_cc_config {
     uint32_t struct_size;       /* sizeof(gs_cc_config)                                    */
     uint32_t id_bits;           /* 32 (int/uint32 ids) or 64 (long ids, the reference's K=Long) */
-    uint64_t vertex_capacity;   /* ids must lie in [0, vertex_capacity); <= 2^32 - 1       */
+    uint64_t vertex_capacity;   /* ids must lie in [0, vertex_capacity); <= 2^32 - 1
+                                   (GS_CC_SPARSE_IDS: the number of distinct ids, <= 2^30)   */
     int32_t  device;            /* HIP device ordinal                                      */
     uint32_t flags;             /* GS_CC_*                                                 */
     uint64_t staging_edges;     /* staging size for host-pointer folds (0 = 2^22)          */
@@ -112,6 +119,9 @@ int gs_cc_checksum(gs_cc_t* h, uint64_t* checksum, uint64_t* n_vertices, uint64_
 /* DisjointSet.find for n ids: roots[i] = current root of ids[i], -1 if unknown (null).
  * The root is the canonical label (roots are always component minima). */
 int gs_cc_find(gs_cc_t* h, const void* ids, void* roots, uint64_t n);
+/* as gs_cc_find, and found[i] = 1 if ids[i] is in the summary, 0 if not (null) — needed where -1
+ * is itself a valid id (GS_CC_SPARSE_IDS). found may be NULL. Implies close_window. */
+int gs_cc_find_flags(gs_cc_t* h, const void* ids, void* roots, uint8_t* found, uint64_t n);
 /* device pointer to the uint32 label/parent array (length vertex_capacity, 0xFFFFFFFF = unseen). */
 int gs_cc_labels_device(gs_cc_t* h, const void** dev_ptr);
 

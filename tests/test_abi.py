@@ -32,7 +32,7 @@ def test_library_exports_every_symbol():
 
 def test_library_loads_and_reports_version():
     L = gsgpu.lib()
-    assert L.gs_version() == 1
+    assert L.gs_version() == 2
     for s in _abi.EXPORTED_SYMBOLS:
         assert hasattr(L, s)
 
