@@ -76,7 +76,7 @@ class SummaryBulkAggregation:
     def __init__(self, update_fun: UpdateCC, combine_fun: CombineCC, time_millis: int,
                  transient_state: bool, *, vertex_capacity: Optional[int] = None, id_bits: int = 64,
                  device: int = 0, parallelism: int = 1, window_edges: Optional[int] = None,
-                 mode: str = "fused"):
+                 mode: str = "fused", sparse: Optional[bool] = None):
         if mode not in ("fused", "reference"):
             raise ValueError("mode must be 'fused' or 'reference'")
         self.update_fun = update_fun
@@ -89,18 +89,31 @@ class SummaryBulkAggregation:
         self.parallelism = max(int(parallelism), 1)
         self.window_edges = window_edges
         self.mode = mode
+        self.sparse = sparse          # None: sparse ids (GS_CC_SPARSE_IDS) iff some id is < 0 or >= 2^32 - 1
+
+    def _use_sparse(self, stream: SimpleEdgeStream) -> bool:
+        if self.sparse is not None:
+            return bool(self.sparse)
+        if self.id_bits != 64 or len(stream) == 0:
+            return False
+        lo = min(int(stream.src.min()), int(stream.dst.min()))
+        hi = max(int(stream.src.max()), int(stream.dst.max()))
+        return lo < 0 or hi >= 0xFFFFFFFF
 
     def _capacity(self, stream: SimpleEdgeStream) -> int:
         if self.vertex_capacity:
             return int(self.vertex_capacity)
         if len(stream) == 0:
             return 1
+        if self._sparse_run:
+            return int(np.unique(np.concatenate([stream.src, stream.dst])).size)
         return int(max(stream.src.max(), stream.dst.max())) + 1
 
     def _new(self, cap: int) -> DisjointSet:
-        return DisjointSet(cap, id_bits=self.id_bits, device=self.device)
+        return DisjointSet(cap, id_bits=self.id_bits, device=self.device, sparse=self._sparse_run)
 
     def run(self, stream: SimpleEdgeStream) -> Iterator[DisjointSet]:
+        self._sparse_run = self._use_sparse(stream)
         cap = self._capacity(stream)
         wins = stream.windows(self.time_millis, self.window_edges)
         if self.mode == "fused":

@@ -160,3 +160,25 @@ def test_sparse_device_buffers_and_reset(oracle):
     assert ds.stats() == (0, 0)
     ds.fold(hs, hd)
     assert ds.checksum() == c1
+
+
+@pytest.mark.parametrize("mode", ["fused", "reference"])
+def test_aggregation_selects_sparse_ids(mode):
+    """ConnectedComponents over Long ids outside [0, 2^32): the operator switches to sparse ids
+    and every window's emission equals the Python twin's cumulative summary."""
+    from gsgpu import ConnectedComponents, SimpleEdgeStream
+    s, d = _dense_stream(3000, 500, seed=31)
+    m = _sparse_map(500, seed=32)
+    hs, hd = m[s], m[d]
+    W = 600
+    py = PyDisjointSet()
+    nwin = 0
+    for w, ds in enumerate(SimpleEdgeStream(hs, hd).aggregate(ConnectedComponents(1000, window_edges=W, mode=mode,
+                                                                                 parallelism=3))):
+        for a, b in zip(hs[w * W:(w + 1) * W].tolist(), hd[w * W:(w + 1) * W].tolist()):
+            py.union(a, b)
+        assert ds.sparse
+        v, l = ds.pairs()
+        assert dict(zip(v.tolist(), l.tolist())) == py.canonical()
+        nwin += 1
+    assert nwin == (len(hs) + W - 1) // W
