@@ -110,7 +110,20 @@ def kat_fixtures():
         "note": "Only the final emission is pinned by the reference (its windows are ingestion-time); "
                 "the 11 event-time windows are this build's deterministic windowing.",
     }
-    return {"DisjointSetTest": dstest, "ConnectedComponentsTest": cctest, "ConnectedComponentsExample": example}
+    # BipartitenessCheckTest: edges and the expected emission strings, as the test holds them
+    bip = {
+        "source": "src/test/java/org/apache/flink/graph/streaming/example/test/BipartitenessCheckTest.java:35-90",
+        "bipartite_edges": [[1, 2], [1, 3], [1, 4], [4, 5], [4, 7], [4, 9]],
+        "bipartite_expect": ["(true,{1={1=(1,true), 2=(2,false), 3=(3,false), 4=(4,false), 5=(5,true), "
+                             "7=(7,true), 9=(9,true)}})"],
+        "non_bipartite_edges": [[1, 2], [2, 3], [3, 1], [4, 5], [5, 7], [4, 1]],
+        "non_bipartite_expect": ["(false,{})"],
+        "merge_window_ms": 500,
+        "note": "env.setParallelism(1); one 500 ms ingestion-time window holds the whole collection, "
+                "so each test pins exactly one emission.",
+    }
+    return {"DisjointSetTest": dstest, "ConnectedComponentsTest": cctest, "ConnectedComponentsExample": example,
+            "BipartitenessCheckTest": bip}
 
 
 def random_cases():

@@ -1,0 +1,95 @@
+"""CPU: the BipartitenessCheck oracle (oracle/bipartite.py) pinned by the reference's known answers
+(BipartitenessCheckTest.java:35-90) and cross-checked: literal restatement of Candidates vs the
+intended semantics vs an independent BFS 2-colouring."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from bipartite import (LiteralCandidates, bfs_bipartition, emission_string, intended_run, literal_run)
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _kat():
+    return json.load(open(os.path.join(GOLD, "reference_kats.json")))["BipartitenessCheckTest"]
+
+
+@pytest.mark.parametrize("which", ["bipartite", "non_bipartite"])
+def test_reference_kats_literal_and_intended(which):
+    k = _kat()
+    e = np.array(k[which + "_edges"])
+    assert literal_run(e[:, 0], e[:, 1], 0) == k[which + "_expect"]
+    assert [emission_string(*x) for x in intended_run(e[:, 0], e[:, 1], 0)] == k[which + "_expect"]
+
+
+def _bfs_ordered_tree_stream(nv: int, extra: int, seed: int, odd_chord: bool):
+    """Edges in an order that never reaches Candidates.merge's split branch: every edge's smaller
+    endpoint is already in a component keyed no higher (BFS from vertex 0 over increasing ids)."""
+    rng = np.random.default_rng(seed)
+    parent = [0] + [int(rng.integers(0, v)) for v in range(1, nv)]       # parent < child
+    depth = [0] * nv
+    for v in range(1, nv):
+        depth[v] = depth[parent[v]] + 1
+    src, dst = [], []
+    for v in range(1, nv):
+        src.append(parent[v]); dst.append(v)
+    for _ in range(extra):                                               # even chords keep it bipartite
+        a, b = sorted(int(x) for x in rng.integers(0, nv, 2))
+        if a != b and (depth[a] + depth[b]) % 2 == 1:
+            src.append(a); dst.append(b)
+    if odd_chord:
+        a, b = [(x, y) for x in range(nv) for y in range(x + 1, nv) if (depth[x] + depth[y]) % 2 == 0][0]
+        src.append(a); dst.append(b)
+    return np.array(src), np.array(dst)
+
+
+@pytest.mark.parametrize("seed,odd", [(1, False), (2, False), (3, True), (4, False)])
+def test_literal_equals_intended_where_the_reference_is_consistent(seed, odd):
+    """One window, one partition (the reference tests' setting): every fold merges a one-edge
+    candidate whose key is >= the key of the component it joins."""
+    s, d = _bfs_ordered_tree_stream(60, 40, seed, odd)
+    assert literal_run(s, d, 0) == [emission_string(*x) for x in intended_run(s, d, 0)]
+
+
+def test_literal_windows_diverge():
+    """Across windows the reference's Merger merges the cumulative summary INTO the window's
+    candidates (summary = window.merge(summary), SummaryAggregation.java:110): the older
+    component arrives as the input with the smaller key, so its signs are flipped to the
+    window's orientation and the window's component survives beside it (Candidates.java:117-126).
+    The intended emission keys each component once with its minimum vertex signed true."""
+    s, d = _bfs_ordered_tree_stream(15, 0, 1, False)
+    lit = literal_run(s, d, 7)
+    ref = [emission_string(*x) for x in intended_run(s, d, 7)]
+    assert lit[0] == ref[0] and lit[1] != ref[1]
+    assert "0=(0,false)" in lit[1] and "0=(0,true)" in ref[1]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_intended_equals_bfs_colouring(seed):
+    rng = np.random.default_rng(100 + seed)
+    nv = 300
+    # random bipartite graph (sides by a hidden colouring), sometimes with one odd edge
+    col = rng.integers(0, 2, nv)
+    s, d = [], []
+    while len(s) < 500:
+        a, b = (int(x) for x in rng.integers(0, nv, 2))
+        if col[a] != col[b]:
+            s.append(a); d.append(b)
+    if seed % 2:
+        same = [(a, b) for a in range(nv) for b in range(a + 1, nv) if col[a] == col[b]][seed]
+        s.append(same[0]); d.append(same[1])
+    got = intended_run(np.array(s), np.array(d), 0)[-1]
+    assert got == bfs_bipartition(s, d)
+
+
+def test_literal_split_branch_is_reachable():
+    """Documented divergence (oracle/bipartite.py header): edges (5,7), (3,7), (3,5) form a
+    triangle; the literal Candidates keeps {3,7} and {5,7} apart after (3,7) and then loses the
+    odd cycle, the intended semantics report non-bipartite."""
+    lit = literal_run(np.array([5, 3, 3]), np.array([7, 7, 5]), 0)
+    assert lit == ["(true,{3={3=(3,true), 5=(5,false), 7=(7,false)}})"]
+    assert emission_string(*intended_run(np.array([5, 3, 3]), np.array([7, 7, 5]), 0)[-1]) == "(false,{})"
+    c = LiteralCandidates(True)
+    assert c.to_string() == "(true,{})"
