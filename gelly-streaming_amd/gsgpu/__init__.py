@@ -6,7 +6,9 @@ from ._abi import GsError, GsgpuUnavailable, available, lib, EXPORTED_SYMBOLS  #
 from .summary import DisjointSet, UpdateCC, CombineCC, combine_cc  # noqa: F401
 from .aggregation import (SimpleEdgeStream, SummaryBulkAggregation, ConnectedComponents,  # noqa: F401
                           SummaryTreeReduce, ConnectedComponentsTree)
+from .bipartite import Candidates, BipartitenessCheck  # noqa: F401
 
 __all__ = ["DisjointSet", "UpdateCC", "CombineCC", "combine_cc", "SimpleEdgeStream",
-           "SummaryBulkAggregation", "ConnectedComponents", "SummaryTreeReduce", "ConnectedComponentsTree", "GsError", "GsgpuUnavailable",
+           "SummaryBulkAggregation", "ConnectedComponents", "SummaryTreeReduce", "ConnectedComponentsTree",
+           "Candidates", "BipartitenessCheck", "GsError", "GsgpuUnavailable",
            "available", "lib"]

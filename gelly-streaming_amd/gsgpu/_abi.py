@@ -38,6 +38,9 @@ EXPORTED_SYMBOLS = (
     "gs_cc_close_window", "gs_cc_stats", "gs_cc_emit_dense", "gs_cc_emit_pairs",
     "gs_cc_checksum", "gs_cc_find", "gs_cc_find_flags", "gs_cc_labels_device", "gs_cc_export_marks",
     "gs_cc_fold_pairs32", "gs_cc_timing", "gs_cc_kernel_time", "gs_gen_rmat", "gs_gen_er", "gs_parse_edges",
+    "gs_bip_create", "gs_bip_destroy", "gs_bip_reset", "gs_bip_set_stream", "gs_bip_sync", "gs_bip_fold",
+    "gs_bip_fold_pairs", "gs_bip_merge", "gs_bip_close_window", "gs_bip_status", "gs_bip_checksum",
+    "gs_bip_emit_pairs",
     "gs_last_error", "gs_version",
 )
 
@@ -100,6 +103,18 @@ def lib() -> ctypes.CDLL:
         "gs_gen_rmat": [vp, vp, u32, u64, u64, i32, u64, u32, u32, u32, i32, vp],
         "gs_gen_er": [vp, vp, u32, u64, u64, u64, u64, vp],
         "gs_parse_edges": [vp, u64, u32, vp, vp, u64, P(u64), i32, vp],
+        "gs_bip_create": [P(vp), u64, u32, i32],
+        "gs_bip_destroy": [vp],
+        "gs_bip_reset": [vp],
+        "gs_bip_set_stream": [vp, vp],
+        "gs_bip_sync": [vp],
+        "gs_bip_fold": [vp, vp, vp, u64],
+        "gs_bip_fold_pairs": [vp, vp, u64],
+        "gs_bip_merge": [vp, vp],
+        "gs_bip_close_window": [vp],
+        "gs_bip_status": [vp, P(i32), P(u64), P(u64)],
+        "gs_bip_checksum": [vp, P(u64), P(i32), P(u64), P(u64)],
+        "gs_bip_emit_pairs": [vp, vp, vp, vp, u64, P(u64)],
     }
     for name, args in sig.items():
         f = getattr(L, name)

@@ -155,6 +155,33 @@ int gs_gen_er(void* src, void* dst, uint32_t id_bits, uint64_t first, uint64_t n
 int gs_parse_edges(const char* text, uint64_t n_bytes, uint32_t id_bits, void* src, void* dst, uint64_t cap,
                    uint64_t* n_edges, int device, void* hip_stream);
 
+/* ---- BipartitenessCheck (library/BipartitenessCheck.java:38-133, summaries/Candidates.java) ----
+ * A Candidates summary on the device: union-find with a parity bit per vertex. ids in
+ * [0, vertex_capacity), vertex_capacity <= 2^31 - 1, id_bits 32 or 64. The emission of a
+ * bipartite summary = every vertex with its component key (the component's minimum id) and its
+ * sign (true iff on the key vertex's side); a summary that has seen an odd cycle is failed for
+ * good (Candidates.fail(): "(false,{})"). Self-loops only add their vertex (edgeToCandidate).
+ *   gs_bip_create / _reset     new Candidates(true)                       (Candidates.java:30-33)
+ *   gs_bip_fold / _fold_pairs  updateFunction.foldEdges over a batch      (BipartitenessCheck.java:93-95)
+ *   gs_bip_merge               combineFunction.reduce: into.merge(from)   (BipartitenessCheck.java:121-124)
+ *   gs_bip_close_window        the Merger's per-window emission           (SummaryAggregation.java:106-119)
+ *   gs_bip_status / _checksum  getSuccess() (Candidates.java:40-42), sizes, and
+ *                              sum over v of splitmix64(v ^ splitmix64(((key << 1) | sign) ^ 0xD1B54A32D192ED03))
+ *   gs_bip_emit_pairs          (vertex, key, sign) ordered by vertex      (Candidates.getMap(), :44-46) */
+typedef struct gs_bip gs_bip_t;
+int gs_bip_create(gs_bip_t** out, uint64_t vertex_capacity, uint32_t id_bits, int device);
+int gs_bip_destroy(gs_bip_t* h);
+int gs_bip_reset(gs_bip_t* h);
+int gs_bip_set_stream(gs_bip_t* h, void* hip_stream);
+int gs_bip_sync(gs_bip_t* h);
+int gs_bip_fold(gs_bip_t* h, const void* src, const void* dst, uint64_t n);
+int gs_bip_fold_pairs(gs_bip_t* h, const void* pairs, uint64_t n);
+int gs_bip_merge(gs_bip_t* into, gs_bip_t* from);
+int gs_bip_close_window(gs_bip_t* h);
+int gs_bip_status(gs_bip_t* h, int* bipartite, uint64_t* n_vertices, uint64_t* n_components);
+int gs_bip_checksum(gs_bip_t* h, uint64_t* checksum, int* bipartite, uint64_t* n_vertices, uint64_t* n_components);
+int gs_bip_emit_pairs(gs_bip_t* h, void* vertices, void* keys, uint8_t* signs, uint64_t cap, uint64_t* n_out);
+
 const char* gs_last_error(void);
 int gs_version(void);
 

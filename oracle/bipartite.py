@@ -10,10 +10,12 @@ Two restatements live here:
   :93-95, combineFunction :121-124), SummaryBulkAggregation.java:68-130 (fresh Candidates(true)
   per partition per window, windowAll reduce) and SummaryAggregation.java:106-119 (Merger:
   summary = combine(windowResult, summary), transientState = false). Pure Python: small cases.
-* ``bipartition`` / ``intended_run`` — the semantics the reference's own tests pin
+* ``ParityUnionFind`` / ``intended_run`` — the semantics the reference's own tests pin
   (T/example/test/BipartitenessCheckTest.java:35-90): the stream so far is bipartite or not;
   when it is, every component keyed by its minimum vertex id, every vertex signed true iff it
-  is on the key vertex's side. Union-find with parity; cross-checked against a BFS 2-colouring.
+  is on the key vertex's side; a self-loop only adds its vertex (edgeToCandidate(v, v): the
+  second add is refused and the refusal ignored). Union-find with parity; cross-checked
+  against a BFS 2-colouring (``bfs_bipartition``).
 
 Where they differ. Candidates.merge (Candidates.java:71-128) folds an input component into the
 LOWEST-keyed overlapping candidate component `firstKey`, but writes the merged vertices under
@@ -176,7 +178,7 @@ class ParityUnionFind:
             if x not in self.parent:
                 self.parent[x] = x
                 self.par[x] = 0
-        if not self.ok:
+        if not self.ok or u == v:           # self-loop: edgeToCandidate adds (v, true) only
             return
         ru, pu = self.find(u)
         rv, pv = self.find(v)
@@ -227,8 +229,11 @@ def bfs_bipartition(src, dst) -> Tuple[bool, Dict[int, int], Dict[int, bool]]:
     """Independent check: BFS 2-colouring from each component's minimum vertex."""
     adj: Dict[int, List[int]] = {}
     for a, b in zip(np.asarray(src).tolist(), np.asarray(dst).tolist()):
-        adj.setdefault(a, []).append(b)
-        adj.setdefault(b, []).append(a)
+        adj.setdefault(a, [])
+        adj.setdefault(b, [])
+        if a != b:                             # self-loops only add their vertex (edgeToCandidate)
+            adj[a].append(b)
+            adj[b].append(a)
     key: Dict[int, int] = {}
     side: Dict[int, int] = {}
     for s in sorted(adj):

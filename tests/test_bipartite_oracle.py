@@ -93,3 +93,10 @@ def test_literal_split_branch_is_reachable():
     assert emission_string(*intended_run(np.array([5, 3, 3]), np.array([7, 7, 5]), 0)[-1]) == "(false,{})"
     c = LiteralCandidates(True)
     assert c.to_string() == "(true,{})"
+
+
+def test_self_loops_only_add_vertices():
+    assert literal_run(np.array([3, 1]), np.array([3, 2]), 0) == ["(true,{1={1=(1,true), 2=(2,false)}, 3={3=(3,true)}})"]
+    assert [emission_string(*x) for x in intended_run(np.array([3, 1]), np.array([3, 2]), 0)] == \
+        ["(true,{1={1=(1,true), 2=(2,false)}, 3={3=(3,true)}})"]
+    assert bfs_bipartition([3, 1], [3, 2])[0]

@@ -1,0 +1,112 @@
+"""GPU parity of BipartitenessCheck (gs_bip_*): the reference's known answers
+(BipartitenessCheckTest.java:35-90) exactly, and every window's emission of random streams equal
+to the oracle's intended semantics (oracle/bipartite.py: union-find with parity, cross-checked
+with a BFS 2-colouring). Integer path: bit-exact."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from gsgpu import BipartitenessCheck, Candidates, GsError, SimpleEdgeStream
+from gsgpu import _abi
+from bipartite import ParityUnionFind, bfs_bipartition, emission_string, intended_run
+from pyoracle import _np_splitmix64
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _kat():
+    return json.load(open(os.path.join(GOLD, "reference_kats.json")))["BipartitenessCheckTest"]
+
+
+@pytest.mark.parametrize("mode", ["fused", "reference"])
+@pytest.mark.parametrize("which", ["bipartite", "non_bipartite"])
+def test_reference_kats(which, mode):
+    k = _kat()
+    e = np.array(k[which + "_edges"])
+    out = [c.toString() for c in SimpleEdgeStream(e[:, 0], e[:, 1]).aggregate(
+        BipartitenessCheck(k["merge_window_ms"], mode=mode, parallelism=1))]
+    assert out == k[which + "_expect"]
+
+
+def _bipartite_stream(nv: int, n: int, seed: int, odd_at: int = -1):
+    rng = np.random.default_rng(seed)
+    col = rng.integers(0, 2, nv)
+    s = rng.integers(0, nv, 4 * n)
+    d = rng.integers(0, nv, 4 * n)
+    keep = (col[s] != col[d]) | (s == d)                 # cross edges and self-loops
+    s, d = s[keep][:n], d[keep][:n]
+    if odd_at >= 0:                                     # one same-side edge at position odd_at
+        a = int(rng.integers(0, nv))
+        b = int(np.nonzero((col == col[a]) & (np.arange(nv) != a))[0][0])
+        s[odd_at], d[odd_at] = a, b
+    return s.astype(np.int64), d.astype(np.int64)
+
+
+@pytest.mark.parametrize("mode", ["fused", "reference"])
+@pytest.mark.parametrize("nv,n,W,odd_at", [(200, 600, 100, -1), (200, 600, 100, 350), (5000, 20000, 3000, -1),
+                                           (5000, 20000, 3000, 17000)])
+def test_windows_vs_oracle(mode, nv, n, W, odd_at):
+    s, d = _bipartite_stream(nv, n, seed=nv + n + odd_at, odd_at=odd_at)
+    want = [emission_string(*x) for x in intended_run(s, d, W)]
+    got = [c.toString() for c in SimpleEdgeStream(s, d).aggregate(
+        BipartitenessCheck(1000, window_edges=W, mode=mode, parallelism=3))]
+    assert got == want
+    if odd_at >= 0:
+        assert got[-1] == "(false,{})" and got[odd_at // W - 1].startswith("(true,")
+
+
+def _checksum(key, sign):
+    v = np.array(sorted(key), dtype=np.uint64)
+    lab = np.array([(key[x] << 1) | (1 if sign[x] else 0) for x in sorted(key)], dtype=np.uint64)
+    mix = _np_splitmix64(v ^ _np_splitmix64(lab ^ np.uint64(0xD1B54A32D192ED03)))
+    with np.errstate(over="ignore"):
+        return int(np.sum(mix, dtype=np.uint64))
+
+
+@pytest.mark.parametrize("bits", [32, 64])
+def test_large_stream_checksum_and_bfs(bits):
+    import torch
+    nv, n = 1 << 17, 1 << 20
+    s, d = _bipartite_stream(nv, n, seed=5)
+    uf = ParityUnionFind()
+    for a, b in zip(s.tolist(), d.tolist()):
+        uf.union(a, b)
+    ok, key, sign = uf.emission()
+    assert (ok, key, sign) == bfs_bipartition(s, d)
+    c = Candidates(nv, id_bits=bits, stream=torch.cuda.current_stream())
+    dt = torch.int32 if bits == 32 else torch.int64
+    c.fold(torch.from_numpy(s).to(dt).cuda(), torch.from_numpy(d).to(dt).cuda())
+    h, good, nverts, ncomp = c.checksum()
+    assert good and nverts == len(key) and ncomp == len(set(key.values()))
+    assert h == _checksum(key, sign)
+
+
+def test_merge_of_partials_equals_whole():
+    s, d = _bipartite_stream(3000, 12000, seed=9)
+    a, b, whole = Candidates(3000), Candidates(3000), Candidates(3000)
+    a.fold(s[:6000], d[:6000])
+    b.fold(s[6000:], d[6000:])
+    whole.fold(s, d)
+    assert a.merge(b).toString() == whole.toString()
+    bad = Candidates(3000)
+    bad.fold(np.array([1, 2, 3]), np.array([2, 3, 1]))
+    assert not bad.getSuccess()
+    assert a.merge(bad).toString() == "(false,{})"          # a failed input fails the result
+
+
+def test_self_loops_range_and_reset():
+    c = Candidates(16, id_bits=32)
+    c.fold(np.array([3, 1, 5]), np.array([3, 2, 5]))
+    assert c.toString() == "(true,{1={1=(1,true), 2=(2,false)}, 3={3=(3,true)}, 5={5=(5,true)}})"
+    with pytest.raises(GsError) as e:
+        c.fold(np.array([1]), np.array([99]))
+        c.sync()
+    assert e.value.code == _abi.GS_ERR_RANGE
+    c.fold(np.array([1, 2]), np.array([4, 4]))              # 1 and 2 on opposite sides: odd cycle
+    assert c.toString() == "(false,{})"
+    c.reset()
+    assert c.toString() == "(true,{})"
