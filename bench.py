@@ -57,6 +57,10 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo = host-staged, for testing the "
                          "multi-rank path with several ranks on one GPU")
+    ap.add_argument("--merge", default="tree", choices=["gather", "tree"],
+                    help="multi-rank CombineCC: gather = flat windowAll gather to rank 0 (ConnectedComponents, "
+                         "SummaryBulkAggregation.java:81); tree = log2(P) pairwise rounds (ConnectedComponentsTree, "
+                         "SummaryTreeReduce.java:95-123)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "fold_traffic.json"),
                     help="PMC-derived HBM bytes per fold launch (written by profiles/pmc_traffic.py)")
     return ap.parse_args()
@@ -104,13 +108,16 @@ def main():
     ds = gsgpu.DisjointSet(V, id_bits=32, device=local, track_marks=(world > 1 and rank != 0), stream=stream)
     tree = None
     if world > 1:
-        from gsgpu.tree import TreeMerge
-        tree = TreeMerge(ds, capacity_pairs=V, device=dev)
+        from gsgpu.tree import GatherMerge, TreeMerge
+        tree = (GatherMerge if a.merge == "gather" else TreeMerge)(ds, capacity_pairs=V, device=dev)
+    gather = world > 1 and a.merge == "gather"
 
     def step():
         ds.reset()
         for w in range(nwin):
             lo = w * W_rank
+            if gather:
+                tree.before_fold()
             ds.fold(src[lo:lo + W_rank], dst[lo:lo + W_rank])
             if tree is not None:
                 tree.merge_window()
@@ -153,6 +160,8 @@ def main():
                 dist.barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
+            if gather:
+                tree.before_fold()
             ds.fold(src[lo:lo + W_rank], dst[lo:lo + W_rank])
             if tree is not None:
                 tree.merge_window()
@@ -207,7 +216,7 @@ def main():
                                                         a.scale, a.edge_factor, _pow2(W_rank)),
                 "scale": a.scale, "vertices": V, "edge_factor_per_gpu": a.edge_factor,
                 "edges_per_gpu": E_rank, "window_edges_per_gpu": W_rank, "windows": nwin,
-                "parallelism": "1 subtask per GPU x %d, %s" % (world, "RCCL tree merge" if world > 1 else "no merge"),
+                "parallelism": "1 subtask per GPU x %d, %s" % (world, ("RCCL %s merge" % a.merge) if world > 1 else "no merge"),
                 "emission": "per window, canonical min-id labels resident in HBM",
             },
             "roofline": {
@@ -238,6 +247,8 @@ def main():
             log("timed region done (%.1f ms/step); cpu baseline..." % (elapsed / a.steps * 1e3))
             line["cpu_baseline"] = cpu_baseline(a, src, dst, W_rank)
         print(json.dumps(line), flush=True)
+    if gather:
+        tree.drain()
     ds.close()
     if world > 1:
         dist.destroy_process_group()

@@ -1,4 +1,10 @@
-"""Multi-GPU CombineCC: log2(P) pairwise tree merge of per-rank partial summaries.
+"""Multi-GPU CombineCC: per-window exchange of per-rank partial summaries.
+
+``GatherMerge`` (default for ConnectedComponents): the reference's windowAll reduce
+(SummaryBulkAggregation.java:81: every partition's partial summary goes to the one
+parallelism-1 task) as one flat gather to rank 0 — every other rank sends its window's pairs
+straight to rank 0 over its own xGMI link, all at once, and rank 0 folds them in one launch.
+``TreeMerge`` (ConnectedComponentsTree): log2(P) pairwise rounds (SummaryTreeReduce.enhance).
 
 Restates the reference's tree reduction ``SummaryTreeReduce.enhance``
 (src/main/java/org/apache/flink/graph/streaming/SummaryTreeReduce.java:95-123: each round keys
@@ -111,3 +117,131 @@ class TreeMerge:
         # ranks it keeps their own giant-component filter current for their next fold
         self.summary.close_window()
         return self.rank == 0
+
+
+class GatherMerge:
+    """Flat gather of every rank's window pairs to rank 0 (windowAll reduce + Merger).
+
+    Per window, rank r != 0: export its marks into one of two device buffers (alternating, so
+    a send still in flight is never overwritten: the buffer's previous sends are waited on, on
+    the current stream, before the next export into it) and isend the count and the pairs to
+    rank 0. Rank 0 posts the count receives before its own fold is enqueued, learns the counts
+    (one host sync), receives every payload into one contiguous buffer (all peers at once, on a
+    side stream so the transfers overlap its fold), and folds all pairs in one launch; then every
+    rank closes its window. Senders never wait for rank 0's emission: they run at most two
+    windows ahead. Summary contract as TreeMerge.
+    """
+
+    def __init__(self, summary, capacity_pairs: int, device: torch.device, group=None):
+        self.summary = summary
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = torch.device(device)
+        self.cap = int(capacity_pairs)
+        self.stage = (dist.get_backend(group) == "gloo" and self.device.type == "cuda")
+        if self.rank == 0:
+            self.cnts = torch.zeros(max(self.world - 1, 1), dtype=torch.int64,
+                                    device="cpu" if self.stage else self.device)
+            self.buf = torch.empty(2 * max(self.cap, 1), dtype=torch.int32, device=self.device)
+            self.hbuf = torch.empty(0, dtype=torch.int32).pin_memory() if self.stage else None
+            self.side = torch.cuda.Stream(self.device) if self.device.type == "cuda" and not self.stage else None
+            self.free_ev = None            # recorded after the last fold out of self.buf
+            self._cnt_works = None
+        else:
+            self.bufs = [torch.empty(2 * self.cap, dtype=torch.int32, device=self.device) for _ in range(2)]
+            self.cnt = [torch.zeros(1, dtype=torch.int64, device="cpu" if self.stage else self.device) for _ in range(2)]
+            self.hbufs = [torch.empty(2 * self.cap, dtype=torch.int32).pin_memory() for _ in range(2)] if self.stage else None
+            self.works = [[], []]
+            self.turn = 0
+        self.bytes_sent = 0
+        self.bytes_recv = 0
+        dist.barrier(group=self.group)     # communicators up before the first point-to-point batch
+
+    def _grank(self, r: int) -> int:
+        return r if self.group is None else dist.get_global_rank(self.group, r)
+
+    def before_fold(self) -> None:
+        """Rank 0: post this window's count receives before its own fold is enqueued, so the
+        counts are not ordered behind the fold on the communicator's stream."""
+        if self.rank != 0 or self.world == 1 or self._cnt_works is not None:
+            return
+        ops = [dist.P2POp(dist.irecv, self.cnts[i - 1:i], self._grank(i), group=self.group)
+               for i in range(1, self.world)]
+        self._cnt_works = dist.batch_isend_irecv(ops)
+
+    def merge_window(self) -> bool:
+        if self.world == 1:
+            self.summary.close_window()
+            return True
+        if self.rank != 0:
+            t = self.turn
+            for w in self.works[t]:                    # the previous sends out of this buffer
+                w.wait()
+            n = self.summary.export_marks(self.bufs[t], self.cap)
+            self.cnt[t].fill_(n)
+            if self.stage:
+                if n:
+                    self.hbufs[t][: 2 * n].copy_(self.bufs[t][: 2 * n])
+                ops = [dist.P2POp(dist.isend, self.cnt[t], self._grank(0), group=self.group)]
+                if n:
+                    ops.append(dist.P2POp(dist.isend, self.hbufs[t][: 2 * n], self._grank(0), group=self.group))
+            else:
+                ops = [dist.P2POp(dist.isend, self.cnt[t], self._grank(0), group=self.group)]
+                if n:
+                    ops.append(dist.P2POp(dist.isend, self.bufs[t][: 2 * n], self._grank(0), group=self.group))
+            self.works[t] = dist.batch_isend_irecv(ops)
+            if self.stage:                             # gloo: the staging buffer is reused next turn
+                for w in self.works[t]:
+                    w.wait()
+                self.works[t] = []
+            self.turn ^= 1
+            self.bytes_sent += 8 * n
+            self.summary.close_window()
+            return False
+        # rank 0
+        self.before_fold()
+        for w in self._cnt_works:
+            w.wait()
+        self._cnt_works = None
+        counts = [int(x) for x in self.cnts.tolist()]
+        total = sum(counts)
+        if total > self.cap:
+            raise RuntimeError("partial summaries of %d pairs exceed capacity %d" % (total, self.cap))
+        if total:
+            dst = self.buf
+            if self.stage:
+                if self.hbuf.numel() < 2 * total:
+                    self.hbuf = torch.empty(2 * total, dtype=torch.int32).pin_memory()
+                dst = self.hbuf
+            ops, off = [], 0
+            for i, c in enumerate(counts):
+                if c:
+                    ops.append(dist.P2POp(dist.irecv, dst[2 * off: 2 * (off + c)], self._grank(i + 1), group=self.group))
+                    off += c
+            if self.side is not None:                  # transfers overlap this rank's fold
+                if self.free_ev is not None:           # ... but not the previous fold out of self.buf
+                    self.side.wait_event(self.free_ev)
+                with torch.cuda.stream(self.side):
+                    works = dist.batch_isend_irecv(ops)
+            else:
+                works = dist.batch_isend_irecv(ops)
+            for w in works:
+                w.wait()                               # NCCL: the current stream waits, not the host
+            if self.stage:
+                self.buf[: 2 * total].copy_(self.hbuf[: 2 * total])
+            self.summary.fold_pairs(self.buf, total, id_bits=32)
+            if self.side is not None:
+                self.free_ev = torch.cuda.Event()
+                self.free_ev.record(torch.cuda.current_stream(self.device))
+            self.bytes_recv += 8 * total
+        self.summary.close_window()
+        return True
+
+    def drain(self) -> None:
+        """Wait for every send still in flight (before tearing the process group down)."""
+        if self.rank != 0:
+            for t in range(2):
+                for w in self.works[t]:
+                    w.wait()
+                self.works[t] = []

@@ -382,14 +382,15 @@ def test_cc_example_file_input(tmp_path):
 
 
 # ---------------- bench.py multi-rank path (2 ranks on one GPU, gloo-staged exchange) ----------------
-def test_bench_two_ranks_one_gpu_verified():
+@pytest.mark.parametrize("merge", ["gather", "tree"])
+def test_bench_two_ranks_one_gpu_verified(merge):
     import subprocess, sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(root, "bench.py"),
            "--gpus", "2", "--steps", "1", "--warmup", "1", "--scale", "16", "--edge-factor", "16",
-           "--window-log2", "16", "--dist-backend", "gloo", "--verify"]
+           "--window-log2", "16", "--dist-backend", "gloo", "--verify", "--merge", merge]
     out = subprocess.check_output(cmd, env=env, timeout=240).decode()
     line = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
