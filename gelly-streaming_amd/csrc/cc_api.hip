@@ -63,7 +63,7 @@ struct gs_cc {
     uint32_t* mark = nullptr;            // export mark bitmap, 1 bit per vertex (GS_CC_TRACK_MARKS)
     uint32_t* gbits = nullptr;           // giant-component filter bitmap (1 bit per vertex)
     uint32_t* sbits = nullptr;           // seen bitmap (1 bit per vertex), set on first touch
-    uint32_t* derr = nullptr;            // deferred device error flags; derr[1] = giant root
+    uint32_t* derr = nullptr;            // derr[0] deferred device error flags; derr[1..5] giant state
     unsigned long long* dscratch = nullptr;  // reduction outputs (8 words)
     unsigned long long* hscratch = nullptr;  // pinned mirror
     void* stage = nullptr;               // host->device staging (2 * staging_edges ids)
@@ -126,6 +126,10 @@ static bool timing_markers() {
 
 // Times one span of launches of kernel class k (HIP events on the launch stream). Launch the
 // span's first kernel with start() and its last with stop() through klaunch().
+// the current giant-state slot (cc_kernels.hpp): derr[1 + 2 * (closes & 1)] = giant, [+1] = built;
+// close c reads slot c & 1 and writes slot (c + 1) & 1; derr[5] = hot set owner
+inline uint32_t* giant_state(gs_cc_t* h) { return h->derr + 1 + 2 * (h->closes & 1); }
+
 struct KTimer {
     gs_cc_t* h; int k; hipEvent_t a = nullptr, b = nullptr; bool markers = false;
     KTimer(gs_cc_t* h_, int k_) : h(h_), k(k_) {
@@ -195,15 +199,29 @@ static bool fold_stats_on() {
     return on;
 }
 
+// young-forest knobs (read once; tools/sweep_young.sh): GSGPU_YOUNG_EPT (edges per thread in young
+// launches: 2 by default, 1/4/8), GSGPU_YOUNG_CHUNK (edges per young launch, 2^18), GSGPU_RING_FROM
+// (the ring fold starts once edges_since_reset >= RING_FROM * capacity / 4; 1). RMAT-26 windows
+// 1-12: EPT 4 -> 2 took window 1 from 1873 to 1715 us; starting the ring (and the hot set's
+// admission) one window earlier saved 140 us over windows 2-12; larger chunks were slower.
+static uint64_t env_u64(const char* name, uint64_t dflt) {
+    const char* e = getenv(name);
+    return (e && *e) ? strtoull(e, nullptr, 0) : dflt;
+}
+static int young_ept() {
+    static const int v = [] { const uint64_t x = env_u64("GSGPU_YOUNG_EPT", 2); return (x == 1 || x == 2 || x == 4 || x == 8) ? (int)x : 0; }();
+    return v;
+}
+
 template <typename IdT, bool AOS>
-void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n) {
-    const int ept = fold_ept();
+void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool young = false) {
+    const int ept = (young && young_ept()) ? young_ept() : fold_ept();
     const unsigned grid = grid_for((n + ept - 1) / ept, kFoldThreads, 16384);
     if (fold_stats_on() && !h->dstats) {
         (void)hipMalloc(&h->dstats, 8 * sizeof(unsigned long long));
         (void)hipMemsetAsync(h->dstats, 0, 8 * sizeof(unsigned long long), h->stream);
     }
-    FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, h->derr + 1, RangeCheck{h->cap, h->derr}, h->dstats};
+    FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
     const bool vec = std::is_same<IdT, uint32_t>::value && !AOS &&
                      ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
     KTimer t(h, GS_K_FOLD);
@@ -211,6 +229,8 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n) {
     klaunch((k_fold<IdT, AOS, MARKV, VECV, EPTV, STV>), dim3(grid), dim3(kFoldThreads), h->stream, t.start(), t.stop(), \
             (const IdT*)a, (const IdT*)b, f)
     if (h->dstats) { if (h->mark) GS_LAUNCH_FOLD(true, false, 4, true); else GS_LAUNCH_FOLD(false, false, 4, true); }
+    else if (ept == 1) { if (h->mark) GS_LAUNCH_FOLD(true, false, 1, false); else GS_LAUNCH_FOLD(false, false, 1, false); }
+    else if (ept == 2) { if (h->mark) GS_LAUNCH_FOLD(true, false, 2, false); else GS_LAUNCH_FOLD(false, false, 2, false); }
     else if (vec && ept == 8) { if (h->mark) GS_LAUNCH_FOLD(true, true, 8, false); else GS_LAUNCH_FOLD(false, true, 8, false); }
     else if (h->mark) { if (vec) GS_LAUNCH_FOLD(true, true, 4, false); else GS_LAUNCH_FOLD(true, false, 4, false); }
     else { if (vec) GS_LAUNCH_FOLD(false, true, 4, false); else GS_LAUNCH_FOLD(false, false, 4, false); }
@@ -235,7 +255,7 @@ void launch_fold_ring(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t
         (void)hipMemsetAsync(h->dstats, 0, 8 * sizeof(unsigned long long), h->stream);
     }
     const HotArgs hot{h->hot, h->hot_bits, h->hot_cand};
-    FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, h->derr + 1, RangeCheck{h->cap, h->derr}, h->dstats};
+    FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
     KTimer t(h, GS_K_FOLD);
     const bool st = h->dstats != nullptr;
     const dim3 grid(grid_for(n / 4, kHotThreads, (unsigned)std::max(h->cus, 1)));
@@ -254,14 +274,21 @@ void launch_fold_ring(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t
 // edges in flight and let later edges see earlier unions (RMAT-26 window 1: 6.4 -> 2.0 ms,
 // tools/exp_chunks.py). Once mature, a batch is one launch (steady windows are filter-bound).
 constexpr uint64_t kYoungChunk = 1ull << 18;
+static uint64_t young_chunk() {
+    static const uint64_t v = env_u64("GSGPU_YOUNG_CHUNK", kYoungChunk);
+    return v ? v : kYoungChunk;
+}
+static uint64_t ring_from() {
+    static const uint64_t v = env_u64("GSGPU_RING_FROM", 1);
+    return v;
+}
 
 template <typename IdT, bool AOS>
 void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, size_t esz) {
     const uint64_t young_limit = h->cap / 4;
-    // mature forest (past twice the young limit: the hot set has been filling for a window),
-    // aligned device uint32 SoA: the steady ring fold
+    // mature forest (past the young limit), aligned device uint32 SoA: the steady ring fold
     if (std::is_same<IdT, uint32_t>::value && !AOS && h->hot && fold_mode() == kFoldRing &&
-        h->edges_since_reset >= 2 * young_limit && n >= 4 &&
+        h->edges_since_reset >= ring_from() * young_limit && n >= 4 &&
         ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0) {
         const uint64_t done = n & ~(uint64_t)3;
         launch_fold_ring(h, reinterpret_cast<const uint32_t*>(a), reinterpret_cast<const uint32_t*>(b), done);
@@ -276,10 +303,11 @@ void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, siz
         uint64_t m = n - off;
         if (h->edges_since_reset < young_limit) {
             const uint64_t left = young_limit - h->edges_since_reset;
-            m = std::min(m, std::max<uint64_t>(std::min(kYoungChunk, left), 1));
+            m = std::min(m, std::max<uint64_t>(std::min(young_chunk(), left), 1));
         }
         const size_t stride = AOS ? 2 * esz : esz;
-        launch_fold<IdT, AOS>(h, a + off * stride, b ? b + off * esz : nullptr, m);
+        launch_fold<IdT, AOS>(h, a + off * stride, b ? b + off * esz : nullptr, m,
+                              h->edges_since_reset < young_limit);
         h->edges_since_reset += m;
         off += m;
     }
@@ -298,7 +326,7 @@ void launch_fold_sparse(gs_cc_t* h, const int64_t* a, const int64_t* b, uint64_t
         uint64_t m = n - off;
         if (h->edges_since_reset < young_limit)
             m = std::min(m, std::max<uint64_t>(std::min(kYoungChunk, young_limit - h->edges_since_reset), 1));
-        FoldArgs f{m, h->parent, h->mark, h->sbits, h->gbits, h->derr + 1, RangeCheck{h->cap, h->derr}, h->dstats};
+        FoldArgs f{m, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
         const unsigned grid = grid_for((m + 1) / 2, 256, 16384);
         KTimer t(h, GS_K_FOLD);
         const int64_t* pa = a + (aos ? 2 * off : off);
@@ -380,11 +408,17 @@ int compress_impl(gs_cc_t* h) {
     if (h->compressed) return GS_OK;
     {
         KTimer t(h, GS_K_COMPRESS);
-        klaunch(k_pick_giant, dim3(1), dim3(1024), h->stream, t.start(), nullptr, (const uint32_t*)h->parent, h->cap, h->derr + 1,
-                (int)(h->closes % kPickEvery != 0), h->hot);
+        // re-sample the giant every kPickEvery closes (and, while there may be none yet, before
+        // each of the first 2 * kPickEvery closes); otherwise k_compress follows it itself
+        const bool force = h->closes % kPickEvery == 0;
+        const bool pick = force || h->closes < 2 * kPickEvery;
+        uint32_t* in = giant_state(h);
+        if (pick)
+            klaunch(k_pick_giant, dim3(1), dim3(1024), h->stream, t.start(), nullptr, (const uint32_t*)h->parent, h->cap,
+                    in, (int)force);
         ++h->closes;
-        klaunch(k_compress, dim3(grid_for(h->cap, 1024, 16384)), dim3(256), h->stream, nullptr, t.stop(),
-                h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)(h->derr + 1));
+        klaunch(k_compress, dim3(grid_for(h->cap, 1024, 16384)), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
+                h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot);
     }
     GS_HIP(hipGetLastError());
     h->compressed = true;
@@ -399,7 +433,7 @@ int ensure_minkey(gs_cc_t* h) {
     const dim3 grid(grid_for(h->cap, 256, 16384));
     hipLaunchKernelGGL(k_minkey_init, grid, dim3(256), 0, h->stream, (const uint32_t*)h->parent, h->cap, sa, h->minkey);
     hipLaunchKernelGGL(k_minkey_reduce, grid, dim3(256), 0, h->stream, (const uint32_t*)h->parent, h->cap, sa,
-                       (const uint32_t*)(h->derr + 1), h->minkey);
+                       (const uint32_t*)(giant_state(h) + 1), h->minkey);
     GS_HIP(hipGetLastError());
     h->minkey_valid = true;
     return GS_OK;
@@ -614,9 +648,9 @@ int gs_cc_reset(gs_cc_t* h) {
     if (h->mark) GS_HIP(hipMemsetAsync(h->mark, 0, mark_bytes(h->cap), h->stream));
     GS_HIP(hipMemsetAsync(h->gbits, 0, mark_bytes(h->cap), h->stream));
     GS_HIP(hipMemsetAsync(h->sbits, 0, mark_bytes(h->cap), h->stream));
-    GS_HIP(hipMemsetAsync(h->derr + 1, 0xFF, 4, h->stream));       // no giant root yet
-    GS_HIP(hipMemsetAsync(h->derr + 2, 0, 4, h->stream));          // next close: full
-    GS_HIP(hipMemsetAsync(h->derr + 3, 0xFF, 4, h->stream));       // hot set owner: none
+    // giant state (cc_kernels.hpp, giant_state()): both slots no giant / gbits built for none,
+    // hot set owner none
+    GS_HIP(hipMemsetAsync(h->derr + 1, 0xFF, 5 * sizeof(uint32_t), h->stream));
     if (h->hot) GS_HIP(hipMemsetAsync(h->hot, 0, kHotBuckets * sizeof(uint2), h->stream));
     if (h->hot_cand) GS_HIP(hipMemsetAsync(h->hot_cand, 0xFF, sizeof(uint32_t) << kHotCandBits, h->stream));
     if (h->sparse) {
@@ -686,7 +720,7 @@ int gs_cc_merge(gs_cc_t* into, gs_cc_t* from) {
     if (into->sparse) {
         KTimer t(into, GS_K_MERGE);
         const dim3 grid(grid_for(from->cap, 256, 16384));
-        FoldArgs f{0, into->parent, into->mark, into->sbits, into->gbits, into->derr + 1, RangeCheck{into->cap, into->derr}, nullptr};
+        FoldArgs f{0, into->parent, into->mark, into->sbits, into->gbits, giant_state(into), RangeCheck{into->cap, into->derr}, nullptr};
         if (into->mark) klaunch(k_merge_sparse<true>, grid, dim3(256), into->stream, t.start(), t.stop(), (const uint32_t*)from->parent, sparse_args(from), f, sparse_args(into));
         else klaunch(k_merge_sparse<false>, grid, dim3(256), into->stream, t.start(), t.stop(), (const uint32_t*)from->parent, sparse_args(from), f, sparse_args(into));
     } else {

@@ -490,40 +490,37 @@ __global__ __launch_bounds__(256) void k_merge_dense(const uint32_t* __restrict_
     }
 }
 
-// Pick the giant component's root for the filter: labels (read-only root walks) of 1024 sampled
-// vertex ids, counted in an LDS hash table; the most frequent label wins if it holds at least a
-// quarter of the seen samples (else no filter: *giant = kInvalid). One workgroup.
+// Giant-component state (gs_cc_t::derr, cc_api.hip giant_state()): two slots of two words,
+// double-buffered by close parity, plus the hot set's owner:
+//   slot[0] giant: the root the next close builds gbits for (followed to its current root first);
+//         kInvalid = none (no filter). The folds read the current slot's word: != kInvalid turns
+//         the filter on.
+//   slot[1] built: the root the last close built gbits for (kInvalid: none). A close whose
+//         followed giant equals it may be incremental (that root was never hooked: roots only ever
+//         become non-roots).
+//   owner: the root of the component the hot set's entries belong to (kInvalid: none yet).
+// Close c reads slot c & 1 and writes slot (c + 1) & 1, so no workgroup's store can overtake
+// another workgroup's read within the launch. Components only merge until reset, so a sampled
+// giant stays the component holding its old root; k_pick_giant re-samples before every
+// kPickEvery-th close in case another component overtook it (and before the early closes while
+// there is no giant yet).
 constexpr int kPickSamples = 1024;
 constexpr int kPickSlots = 2048;
-// state[0] = giant root (kInvalid: none), state[1] = 1 iff the next close may be incremental:
-// the picked root equals the root the last close built gbits for (so it was not hooked: roots
-// only ever become non-roots, and the pick returns roots).
-//
-// follow != 0 and a giant root is known: no sampling, the giant is followed to its current root
-// (components only merge, so the sampled giant stays the component holding its old root; the
-// host re-samples every kPickEvery closes in case another component overtook it).
 constexpr int kPickEvery = 8;
-// giant[2] = the root of the component the hot set's entries belong to (kInvalid: none yet); a
-// pick of another component clears the hot set (the tail of this kernel).
-__global__ __launch_bounds__(1024) void k_pick_giant(const uint32_t* __restrict__ parent, uint32_t n,
-                                                    uint32_t* __restrict__ giant, int follow, uint2* __restrict__ hot) {
-    if (follow && giant[0] != kInvalid) {       // uniform over the block
-        if (threadIdx.x == 0) {
-            const uint32_t g0 = giant[0];
-            const uint32_t g = find_root_ro(parent, g0);
-            giant[1] = (g == g0) ? 1u : 0u;
-            giant[0] = g;
-            giant[2] = g;
-        }
-        return;
-    }
-    __shared__ uint32_t clear_hot;
-    __shared__ uint32_t keys[kPickSlots];
-    __shared__ uint32_t cnt[kPickSlots];
-    __shared__ unsigned long long best[16];
-    __shared__ uint32_t seen_total;
-    for (int i = threadIdx.x; i < kPickSlots; i += blockDim.x) { keys[i] = kInvalid; cnt[i] = 0; }
-    if (threadIdx.x == 0) seen_total = 0;
+
+struct PickLds {
+    uint32_t keys[kPickSlots];
+    uint32_t cnt[kPickSlots];
+    unsigned long long best[16];
+    uint32_t seen_total;
+};
+
+// Labels (read-only root walks) of kPickSamples sampled vertex ids, counted in an LDS hash table
+// by one whole workgroup; the most frequent label wins if it holds at least a quarter of the seen
+// samples. Returns the pick (kInvalid: no giant) to every thread.
+__device__ uint32_t sample_giant(const uint32_t* __restrict__ parent, uint32_t n, PickLds& L) {
+    for (int i = threadIdx.x; i < kPickSlots; i += blockDim.x) { L.keys[i] = kInvalid; L.cnt[i] = 0; }
+    if (threadIdx.x == 0) L.seen_total = 0;
     __syncthreads();
     uint32_t seen = 0;
     for (int i = threadIdx.x; i < kPickSamples; i += blockDim.x) {
@@ -533,17 +530,17 @@ __global__ __launch_bounds__(1024) void k_pick_giant(const uint32_t* __restrict_
         ++seen;
         uint32_t h = (lab * 2654435761u) & (kPickSlots - 1);
         for (;;) {
-            const uint32_t old = atomicCAS(&keys[h], kInvalid, lab);
-            if (old == kInvalid || old == lab) { atomicAdd(&cnt[h], 1u); break; }
+            const uint32_t old = atomicCAS(&L.keys[h], kInvalid, lab);
+            if (old == kInvalid || old == lab) { atomicAdd(&L.cnt[h], 1u); break; }
             h = (h + 1) & (kPickSlots - 1);
         }
     }
-    atomicAdd(&seen_total, seen);
+    atomicAdd(&L.seen_total, seen);
     __syncthreads();
     unsigned long long mine = 0;                 // (count << 32) | key, max-reduced
     for (int i = threadIdx.x; i < kPickSlots; i += blockDim.x)
-        if (cnt[i]) {
-            const unsigned long long c = ((unsigned long long)cnt[i] << 32) | keys[i];
+        if (L.cnt[i]) {
+            const unsigned long long c = ((unsigned long long)L.cnt[i] << 32) | L.keys[i];
             mine = c > mine ? c : mine;
         }
 #pragma unroll
@@ -551,24 +548,24 @@ __global__ __launch_bounds__(1024) void k_pick_giant(const uint32_t* __restrict_
         const unsigned long long o = __shfl_down(mine, off, 64);
         mine = o > mine ? o : mine;
     }
-    if ((threadIdx.x & 63) == 0) best[threadIdx.x >> 6] = mine;
+    if ((threadIdx.x & 63) == 0) L.best[threadIdx.x >> 6] = mine;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long b = 0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) b = best[w] > b ? best[w] : b;
-        const uint32_t c = (uint32_t)(b >> 32);
-        const uint32_t g = (c >= 16 && 4 * c >= seen_total) ? (uint32_t)b : kInvalid;
-        giant[1] = (g != kInvalid && g == giant[0]) ? 1u : 0u;
-        giant[0] = g;
-        const uint32_t owner = giant[2];
-        const bool other = g != kInvalid && (owner == kInvalid || find_root_ro(parent, owner) != g);
-        clear_hot = other ? 1u : 0u;
-        if (g != kInvalid) giant[2] = g;
-    }
-    __syncthreads();
-    if (clear_hot && hot) {
-        for (uint32_t i = threadIdx.x; i < kHotBuckets; i += blockDim.x) hot[i] = make_uint2(0u, 0u);
-    }
+    unsigned long long b = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) b = L.best[w] > b ? L.best[w] : b;
+    const uint32_t c = (uint32_t)(b >> 32);
+    const uint32_t g = (c >= 16 && 4 * c >= L.seen_total) ? (uint32_t)b : kInvalid;
+    __syncthreads();                             // L is reused by the caller
+    return g;
+}
+
+// Sample the giant before a close into the slot that close reads (force: even if one is known).
+// One workgroup.
+__global__ __launch_bounds__(1024) void k_pick_giant(const uint32_t* __restrict__ parent, uint32_t n,
+                                                    uint32_t* __restrict__ slot, int force) {
+    if (!force && slot[0] != kInvalid) return;   // uniform
+    __shared__ PickLds L;
+    const uint32_t g = sample_giant(parent, n, L);
+    if (threadIdx.x == 0) slot[0] = g;
 }
 
 // Merger emission: full compression. Afterwards parent[v] = root(v) = canonical label, and
@@ -577,19 +574,45 @@ __global__ __launch_bounds__(1024) void k_pick_giant(const uint32_t* __restrict_
 // stored the root and put back an intermediate ancestor. A workgroup covers 1024 consecutive
 // vertices (4 KiB of parent[], 128 B of gbits), so every line it stores to is its own.
 //
-// Incremental mode (state[1] == 1, the giant root g is unchanged since the last close): every
-// vertex with its gbit set is a depth-1 child of g and stays so (g was never hooked, and a walk
-// through g's children never writes), so only seen vertices outside the giant (sbits & ~gbits)
-// are relabelled; the per-window cost drops from a 4-B read per vertex to two bitmap words per
-// 32 vertices plus the stragglers. The 32 vertices of a bitmap word are one thread's, as are
-// their 128 B of parent[].
+// Incremental mode (the giant root g is the one the last close built gbits for): every vertex
+// with its gbit set is a depth-1 child of g and stays so (g was never hooked, and a walk through
+// g's children never writes), so only seen vertices outside the giant (sbits & ~gbits) are
+// relabelled; the per-window cost drops from a 4-B read per vertex to two bitmap words per 32
+// vertices plus the stragglers. The 32 vertices of a bitmap word are one thread's, as are their
+// 128 B of parent[].
+//
+// Giant state (above): every workgroup follows the input slot's giant to its current root g
+// itself (a short read-only walk), so a close needs no separate pick launch; workgroup 0 clears
+// the hot set when g is another component than the hot set's owner, and writes g to the output
+// slot as the next close's giant and the root gbits were built for.
 __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent, uint32_t n,
                                                   uint32_t* __restrict__ gbits, const uint32_t* __restrict__ sbits,
-                                                  const uint32_t* __restrict__ giant) {
-    const uint32_t g = giant[0];
-    const bool incremental = giant[1] != 0;
+                                                  const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                  uint32_t* __restrict__ owner, uint2* __restrict__ hot) {
+    __shared__ uint32_t s_g, s_inc, s_clear;
+    if (threadIdx.x == 0) {
+        const uint32_t g0 = in[0];
+        const uint32_t g = (g0 == kInvalid) ? kInvalid : find_root_ro(parent, g0);
+        s_g = g;
+        s_inc = (g != kInvalid && g == in[1]) ? 1u : 0u;
+        s_clear = 0;
+        if (blockIdx.x == 0) {
+            if (g != kInvalid) {
+                const uint32_t o = *owner;
+                s_clear = (o == kInvalid || find_root_ro(parent, o) != g) ? 1u : 0u;
+                *owner = g;
+            }
+            out[0] = g;
+            out[1] = g;
+        }
+    }
+    __syncthreads();
+    const uint32_t g = s_g;
+    if (s_clear && hot) {                            // workgroup 0 only: the hot set belonged to another component
+        for (uint32_t i = threadIdx.x; i < kHotBuckets; i += blockDim.x) hot[i] = make_uint2(0u, 0u);
+    }
     const int lane = threadIdx.x & 63;
-    if (incremental) {                               // one bitmap word (32 vertices) per thread
+    if (s_inc) {                                     // one bitmap word (32 vertices) per thread
         const uint32_t nwords = (uint32_t)((n + 31) >> 5);
         for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += gridDim.x * blockDim.x) {
             uint32_t cand = sbits[w] & ~gbits[w];
@@ -611,40 +634,40 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
             }
             if (add) gbits[w] |= add;
         }
-        return;
-    }
-    for (uint64_t blk = (uint64_t)blockIdx.x * 1024; blk < n; blk += (uint64_t)gridDim.x * 1024) {
-        const uint32_t base = (uint32_t)blk + threadIdx.x * 4;
-        uint32_t p[4];
-        if ((uint64_t)base + 4 <= n) {
-            const uint4 q = *reinterpret_cast<const uint4*>(parent + base);
-            p[0] = q.x; p[1] = q.y; p[2] = q.z; p[3] = q.w;
-        } else {
+    } else {
+        for (uint64_t blk = (uint64_t)blockIdx.x * 1024; blk < n; blk += (uint64_t)gridDim.x * 1024) {
+            const uint32_t base = (uint32_t)blk + threadIdx.x * 4;
+            uint32_t p[4];
+            if ((uint64_t)base + 4 <= n) {
+                const uint4 q = *reinterpret_cast<const uint4*>(parent + base);
+                p[0] = q.x; p[1] = q.y; p[2] = q.z; p[3] = q.w;
+            } else {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) p[k] = ((uint64_t)base + k < n) ? parent[base + k] : kInvalid;
-        }
-        uint32_t gp[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t v = base + k;
-            gp[k] = (p[k] != kInvalid && p[k] != v) ? parent[p[k]] : p[k];
-        }
-        uint32_t nib = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t v = base + k;
-            uint32_t lab = p[k];
-            if (p[k] != kInvalid && p[k] != v && gp[k] != p[k]) {   // depth >= 2: walk, store the root
-                lab = find_root_ro(parent, gp[k]);
-                parent[v] = lab;
+                for (int k = 0; k < 4; ++k) p[k] = ((uint64_t)base + k < n) ? parent[base + k] : kInvalid;
             }
-            nib |= (lab == g && lab != kInvalid) ? (1u << k) : 0u;
+            uint32_t gp[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t v = base + k;
+                gp[k] = (p[k] != kInvalid && p[k] != v) ? parent[p[k]] : p[k];
+            }
+            uint32_t nib = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t v = base + k;
+                uint32_t lab = p[k];
+                if (p[k] != kInvalid && p[k] != v && gp[k] != p[k]) {   // depth >= 2: walk, store the root
+                    lab = find_root_ro(parent, gp[k]);
+                    parent[v] = lab;
+                }
+                nib |= (lab == g && lab != kInvalid) ? (1u << k) : 0u;
+            }
+            uint32_t word = nib << (4 * (lane & 7));
+            word |= __shfl_xor(word, 1, 64);
+            word |= __shfl_xor(word, 2, 64);
+            word |= __shfl_xor(word, 4, 64);
+            if ((lane & 7) == 0 && base < n) gbits[base >> 5] = word;
         }
-        uint32_t word = nib << (4 * (lane & 7));
-        word |= __shfl_xor(word, 1, 64);
-        word |= __shfl_xor(word, 2, 64);
-        word |= __shfl_xor(word, 4, 64);
-        if ((lane & 7) == 0 && base < n) gbits[base >> 5] = word;
     }
 }
 
