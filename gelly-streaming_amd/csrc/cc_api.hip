@@ -213,6 +213,10 @@ static int young_ept() {
     return v;
 }
 
+// path halving in young / merge launches: GSGPU_YOUNG_HALVE, GSGPU_MERGE_HALVE (1 = on)
+static bool young_halve() { static const bool v = env_u64("GSGPU_YOUNG_HALVE", 1) != 0; return v; }
+static bool merge_halve() { static const bool v = env_u64("GSGPU_MERGE_HALVE", 1) != 0; return v; }
+
 template <typename IdT, bool AOS>
 void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool young = false) {
     const int ept = (young && young_ept()) ? young_ept() : fold_ept();
@@ -222,6 +226,7 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
         (void)hipMemsetAsync(h->dstats, 0, 8 * sizeof(unsigned long long), h->stream);
     }
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
+    f.halve = AOS ? merge_halve() : young ? young_halve() : 1u;
     const bool vec = std::is_same<IdT, uint32_t>::value && !AOS &&
                      ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
     KTimer t(h, GS_K_FOLD);
@@ -278,6 +283,28 @@ static uint64_t young_chunk() {
     static const uint64_t v = env_u64("GSGPU_YOUNG_CHUNK", kYoungChunk);
     return v ? v : kYoungChunk;
 }
+// Folding a partial summary (AOS pairs: fold_pairs / the multi-GPU merge): the pairs (v, R) of one
+// component all name its root R. If R's component is not yet joined to the receiver's component of
+// the v's, every pair in flight reads the same stale roots and CASes the same word (R's or the
+// receiver's giant root): millions of same-address atomics, 5-14 ms for 6M pairs (RMAT-26 window
+// 1, tools/sim_ranks.py), where a receiver that already holds the join folds them in 0.2 ms.
+// 8 ranks' window-1 merges: 32 ms in one launch each, 2.1 ms with a 2^10 head (2^14: 2.6, 2^17: 6.5). So a
+// short head launch of GSGPU_MERGE_HEAD pairs (default 2^10) joins the big components first, then
+// the rest follow in launches of GSGPU_MERGE_CHUNK pairs (0 = one launch).
+static uint64_t merge_head() {
+    static const uint64_t v = env_u64("GSGPU_MERGE_HEAD", 1u << 10);
+    return v;
+}
+static uint64_t merge_chunk() {
+    static const uint64_t v = env_u64("GSGPU_MERGE_CHUNK", 0);
+    return v;
+}
+// first young launch after reset: GSGPU_YOUNG_HEAD edges, doubling per launch up to the chunk
+// (0 = chunks from the start): the hubs' first touches and joins happen with few edges in flight
+static uint64_t young_head() {
+    static const uint64_t v = env_u64("GSGPU_YOUNG_HEAD", 0);
+    return v;
+}
 static uint64_t ring_from() {
     static const uint64_t v = env_u64("GSGPU_RING_FROM", 1);
     return v;
@@ -303,7 +330,17 @@ void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, siz
         uint64_t m = n - off;
         if (h->edges_since_reset < young_limit) {
             const uint64_t left = young_limit - h->edges_since_reset;
-            m = std::min(m, std::max<uint64_t>(std::min(young_chunk(), left), 1));
+            uint64_t c = young_chunk();
+            if (young_head()) {          // geometric ramp: head, 2 head, 4 head, ... up to the chunk
+                uint64_t r = young_head();
+                while (r < c && 2 * r <= h->edges_since_reset + young_head()) r *= 2;
+                c = std::min(c, r);
+            }
+            m = std::min(m, std::max<uint64_t>(std::min(c, left), 1));
+        } else if (AOS && off == 0 && merge_head()) {
+            m = std::min(m, merge_head());
+        } else if (AOS && merge_chunk()) {
+            m = std::min(m, merge_chunk());
         }
         const size_t stride = AOS ? 2 * esz : esz;
         launch_fold<IdT, AOS>(h, a + off * stride, b ? b + off * esz : nullptr, m,
@@ -917,7 +954,7 @@ int gs_cc_export_marks(gs_cc_t* h, void* pairs, uint64_t cap, uint64_t* n_out) {
     GS_HIP(hipMemsetAsync(h->dscratch, 0, sizeof(unsigned long long), h->stream));
     {
         KTimer t(h, GS_K_EXPORT);
-        klaunch(k_export_marks, dim3(grid_for((h->cap + 31) / 32, 256, 4096)), dim3(256), h->stream, t.start(), t.stop(),
+        klaunch(k_export_marks, dim3(grid_for((h->cap + 31) / 32, 256, kExportBlocks)), dim3(256), h->stream, t.start(), t.stop(),
                 h->mark, (const uint32_t*)h->parent, h->cap, (uint32_t*)out, cap, h->dscratch);
     }
     GS_HIP(hipGetLastError());

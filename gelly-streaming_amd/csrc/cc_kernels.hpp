@@ -32,11 +32,13 @@ namespace gsgpu {
 // just initialised (treated as a root; a hook on it is then decided by the CAS, which sees the
 // true word). A non-root's parent is always < its index, so px >= x covers both cases and no
 // walk ever indexes parent[kInvalid].
-__device__ __forceinline__ uint32_t find_root(uint32_t* __restrict__ parent, uint32_t x, uint32_t px) {
+// halve = false: a read-only walk (no stores into words other walks share: in a young forest the
+// halving atomics on hub ancestors serialise at the memory-side atomic unit).
+__device__ __forceinline__ uint32_t find_root(uint32_t* __restrict__ parent, uint32_t x, uint32_t px, bool halve = true) {
     if (px >= x) return x;
     uint32_t prev = x, cur = px, next;
     while (cur > (next = parent[cur])) {
-        __hip_atomic_fetch_min(&parent[prev], next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (halve) __hip_atomic_fetch_min(&parent[prev], next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         prev = cur;
         cur = next;
     }
@@ -76,7 +78,7 @@ template <bool MARK, bool STATS = false>
 __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32_t* __restrict__ mark,
                                            uint32_t* __restrict__ sbits,
                                            uint32_t u, uint32_t v, uint32_t pu, uint32_t pv,
-                                           FoldStats* st = nullptr) {
+                                           FoldStats* st = nullptr, bool halve = true) {
     if (u == v) {                                   // union(u,u): makeSet only
         if (pu == kInvalid) {
             const uint32_t old = atomicCAS(&parent[u], kInvalid, u);
@@ -97,8 +99,8 @@ __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32
         if (STATS) ++st->early;
         return;
     }
-    uint32_t ru = fu ? u : find_root(parent, u, pu);
-    uint32_t rv = fv ? v : find_root(parent, v, pv);
+    uint32_t ru = fu ? u : find_root(parent, u, pu, halve);
+    uint32_t rv = fv ? v : find_root(parent, v, pv, halve);
     while (ru != rv) {
         const bool uhi = ru > rv;
         const uint32_t hi = uhi ? ru : rv, lo = uhi ? rv : ru;
@@ -110,7 +112,7 @@ __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32
             if (old == kInvalid) {
                 set_mark(sbits, lo);
             } else if (old != lo) {                 // initialised and hooked meanwhile
-                const uint32_t r = find_root(parent, old, parent[old]);
+                const uint32_t r = find_root(parent, old, parent[old], halve);
                 if (uhi) rv = r; else ru = r;
                 continue;
             }
@@ -129,7 +131,7 @@ __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32
         if (old == kInvalid) { hf = true; continue; }   // defensive: never reached by a walk result
         // hi was hooked meanwhile: continue from its true parent (old < hi, strictly
         // decreasing, so the loop ends)
-        const uint32_t r = find_root(parent, old, parent[old]);
+        const uint32_t r = find_root(parent, old, parent[old], halve);
         if (uhi) ru = r; else rv = r;
     }
 }
@@ -165,6 +167,7 @@ struct FoldArgs {
     const uint32_t* giant;
     RangeCheck rc;
     unsigned long long* stats;   // STATS: [valid, filtered, early, hooks, casfail, inits]
+    uint32_t halve = 1;          // path halving in root walks (find_root)
 };
 
 // ---- LDS hot set (steady state) ----
@@ -287,7 +290,7 @@ __device__ __forceinline__ void union_group(const FoldArgs& f, const uint32_t (&
     }
 #pragma unroll
     for (int k = 0; k < EPT; ++k)
-        if (ok[k]) union_edge<MARK, STATS>(f.parent, f.mark, f.sbits, u[k], v[k], pu[k], pv[k], &st);
+        if (ok[k]) union_edge<MARK, STATS>(f.parent, f.mark, f.sbits, u[k], v[k], pu[k], pv[k], &st, f.halve != 0);
 }
 
 // Filter, parent gathers and unions of one thread's EPT edges (ids already range-checked;
@@ -815,31 +818,59 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_scatter(const uint32_t* _
     }
 }
 
-// Partial-summary export: (v, parent[v]) for every marked v (bitmap, 32 vertices per word),
-// marks cleared. Unordered append with one atomic per wave (prefix sum over the wave). Each word
-// is owned by one thread, so its plain clear cannot race with another workgroup's store.
+// Partial-summary export (multi-GPU CombineCC): every marked vertex v (a root hooked since the
+// last export, or a self-loop first touch) becomes the pair (v, root(v)); its mark is cleared.
+// Roots, not the parent words at hook time: the receiver's unions then all point at the few
+// component minima its own forest already holds (short walks, no hook chains to contend on).
+// Each workgroup owns a contiguous range of mark words: it counts them, takes its output range with
+// ONE atomicAdd on the shared counter (one per wave serialised ~32K same-address atomics: 400 us
+// per RMAT-26 window, tools/sim_ranks.py), then scatters tile by tile (block-wide scan). Pairs
+// past `cap` are not written and keep their marks for the next export. Each mark word is one
+// thread's, so its plain clear cannot race with another workgroup's store.
+constexpr int kExportBlocks = 1024;
 __global__ __launch_bounds__(256) void k_export_marks(uint32_t* __restrict__ mark, const uint32_t* __restrict__ parent,
                                                       uint32_t n, uint32_t* __restrict__ pairs, uint64_t cap,
                                                       unsigned long long* __restrict__ counter) {
+    __shared__ unsigned long long s_base;
+    __shared__ uint32_t s_wave[4];
     const uint32_t nwords = (n + 31) >> 5;
-    const uint32_t stride = gridDim.x * blockDim.x;
-    const int lane = threadIdx.x & 63;
-    for (uint32_t w0 = blockIdx.x * blockDim.x; w0 < nwords; w0 += stride) {
+    const uint32_t per = (nwords + gridDim.x - 1) / gridDim.x;
+    const uint32_t lo = min(blockIdx.x * per, nwords), hi = min(lo + per, nwords);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t c = 0;
+    for (uint32_t w = lo + threadIdx.x; w < hi; w += blockDim.x) c += __popc(mark[w]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+    if (lane == 0) s_wave[wave] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+        s_base = t ? atomicAdd(counter, (unsigned long long)t) : 0ull;
+    }
+    __syncthreads();
+    unsigned long long base = s_base;
+    for (uint32_t w0 = lo; w0 < hi; w0 += blockDim.x) {          // uniform over the block
         const uint32_t w = w0 + threadIdx.x;
-        uint32_t m = (w < nwords) ? mark[w] : 0u;
+        uint32_t m = (w < hi) ? mark[w] : 0u;
         const uint32_t cnt = __popc(m);
-        unsigned long long incl = cnt;
+        uint32_t incl = cnt;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
-            const unsigned long long y = __shfl_up(incl, off, 64);
+            const uint32_t y = __shfl_up(incl, off, 64);
             if (lane >= off) incl += y;
         }
-        const unsigned long long wtot = __shfl(incl, 63, 64);
-        unsigned long long wbase = 0;
-        if (lane == 0 && wtot) wbase = atomicAdd(counter, wtot);
-        wbase = __shfl(wbase, 0, 64);
+        __syncthreads();                                         // s_wave free
+        if (lane == 63) s_wave[wave] = incl;
+        __syncthreads();
+        uint32_t woff = 0, tile = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            woff += (i < wave) ? s_wave[i] : 0u;
+            tile += s_wave[i];
+        }
+        unsigned long long pos = base + woff + incl - cnt;
+        base += tile;
         if (cnt == 0) continue;
-        unsigned long long pos = wbase + incl - cnt;
         uint32_t keep = 0;
         while (m) {
             const int b = __ffs(m) - 1;
@@ -847,7 +878,7 @@ __global__ __launch_bounds__(256) void k_export_marks(uint32_t* __restrict__ mar
             const uint32_t v = (w << 5) + b;
             if (pos < cap) {
                 pairs[2 * pos] = v;
-                pairs[2 * pos + 1] = parent[v];
+                pairs[2 * pos + 1] = find_root_ro(parent, v);
             } else {
                 keep |= 1u << b;                // overflowing marks stay for the next export
             }
