@@ -57,8 +57,9 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo = host-staged, for testing the "
                          "multi-rank path with several ranks on one GPU")
-    ap.add_argument("--merge", default="tree", choices=["gather", "tree"],
-                    help="multi-rank CombineCC: gather = flat windowAll gather to rank 0 (ConnectedComponents, "
+    ap.add_argument("--merge", default="allgather", choices=["allgather", "gather", "tree"],
+                    help="multi-rank CombineCC: allgather = replicated global summary, all-pairs delta exchange "
+                         "(fastest, tools/sim_ranks.py); gather = flat windowAll gather to rank 0 (ConnectedComponents, "
                          "SummaryBulkAggregation.java:81); tree = log2(P) pairwise rounds (ConnectedComponentsTree, "
                          "SummaryTreeReduce.java:95-123)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "fold_traffic.json"),
@@ -105,11 +106,13 @@ def main():
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
-    ds = gsgpu.DisjointSet(V, id_bits=32, device=local, track_marks=(world > 1 and rank != 0), stream=stream)
+    marks = world > 1 and (a.merge == "allgather" or rank != 0)
+    ds = gsgpu.DisjointSet(V, id_bits=32, device=local, track_marks=marks, stream=stream)
     tree = None
     if world > 1:
-        from gsgpu.tree import GatherMerge, TreeMerge
-        tree = (GatherMerge if a.merge == "gather" else TreeMerge)(ds, capacity_pairs=V, device=dev)
+        from gsgpu.tree import AllgatherMerge, GatherMerge, TreeMerge
+        cls = {"allgather": AllgatherMerge, "gather": GatherMerge, "tree": TreeMerge}[a.merge]
+        tree = cls(ds, capacity_pairs=V, device=dev)
     gather = world > 1 and a.merge == "gather"
 
     def step():

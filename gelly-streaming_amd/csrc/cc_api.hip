@@ -61,6 +61,7 @@ struct gs_cc {
     hipStream_t own = nullptr, stream = nullptr;
     uint32_t* parent = nullptr;          // dense summary / label array
     uint32_t* mark = nullptr;            // export mark bitmap, 1 bit per vertex (GS_CC_TRACK_MARKS)
+    uint32_t* mark_buf = nullptr;        // the mark allocation (mark = mark_buf while marking, else null)
     uint32_t* gbits = nullptr;           // giant-component filter bitmap (1 bit per vertex)
     uint32_t* sbits = nullptr;           // seen bitmap (1 bit per vertex), set on first touch
     uint32_t* derr = nullptr;            // derr[0] deferred device error flags; derr[1..5] giant state
@@ -291,6 +292,8 @@ static uint64_t young_chunk() {
 // 8 ranks' window-1 merges: 32 ms in one launch each, 2.1 ms with a 2^10 head (2^14: 2.6, 2^17: 6.5). So a
 // short head launch of GSGPU_MERGE_HEAD pairs (default 2^10) joins the big components first, then
 // the rest follow in launches of GSGPU_MERGE_CHUNK pairs (0 = one launch).
+constexpr uint64_t kMergeBulk = 1ull << 20;   // smaller batches: one launch (a delta of a mature
+                                              // summary rarely joins big components)
 static uint64_t merge_head() {
     static const uint64_t v = env_u64("GSGPU_MERGE_HEAD", 1u << 10);
     return v;
@@ -337,7 +340,7 @@ void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, siz
                 c = std::min(c, r);
             }
             m = std::min(m, std::max<uint64_t>(std::min(c, left), 1));
-        } else if (AOS && off == 0 && merge_head()) {
+        } else if (AOS && off == 0 && merge_head() && n > kMergeBulk) {
             m = std::min(m, merge_head());
         } else if (AOS && merge_chunk()) {
             m = std::min(m, merge_chunk());
@@ -612,7 +615,8 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
     h->stream = h->own;
     if (hipMalloc(&h->parent, (size_t)h->cap * sizeof(uint32_t)) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "parent[%u] allocation failed", h->cap)); }
     if (cfg->flags & GS_CC_TRACK_MARKS) {
-        if (hipMalloc(&h->mark, mark_bytes(h->cap)) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "mark allocation failed")); }
+        if (hipMalloc(&h->mark_buf, mark_bytes(h->cap)) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "mark allocation failed")); }
+        h->mark = h->mark_buf;
     }
     if (hipMalloc(&h->gbits, mark_bytes(h->cap)) != hipSuccess || hipMalloc(&h->sbits, mark_bytes(h->cap)) != hipSuccess ||
         hipMalloc(&h->derr, 64) != hipSuccess || hipMalloc(&h->dscratch, 8 * sizeof(unsigned long long)) != hipSuccess ||
@@ -659,7 +663,7 @@ int gs_cc_destroy(gs_cc_t* h) {
     for (auto& p : h->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : h->pool) (void)hipEventDestroy(e);
     if (h->parent) (void)hipFree(h->parent);
-    if (h->mark) (void)hipFree(h->mark);
+    if (h->mark_buf) (void)hipFree(h->mark_buf);
     if (h->derr) (void)hipFree(h->derr);
     if (h->gbits) (void)hipFree(h->gbits);
     if (h->sbits) (void)hipFree(h->sbits);
@@ -682,7 +686,7 @@ int gs_cc_reset(gs_cc_t* h) {
     GS_TRY(check(h));
     DeviceGuard g(h->device);
     GS_HIP(hipMemsetAsync(h->parent, 0xFF, (size_t)h->cap * sizeof(uint32_t), h->stream));
-    if (h->mark) GS_HIP(hipMemsetAsync(h->mark, 0, mark_bytes(h->cap), h->stream));
+    if (h->mark_buf) GS_HIP(hipMemsetAsync(h->mark_buf, 0, mark_bytes(h->cap), h->stream));
     GS_HIP(hipMemsetAsync(h->gbits, 0, mark_bytes(h->cap), h->stream));
     GS_HIP(hipMemsetAsync(h->sbits, 0, mark_bytes(h->cap), h->stream));
     // giant state (cc_kernels.hpp, giant_state()): both slots no giant / gbits built for none,
@@ -938,11 +942,27 @@ int gs_cc_labels_device(gs_cc_t* h, const void** p) {
     return GS_OK;
 }
 
+static int export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long* counter) {
+    GS_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned long long), h->stream));
+    {
+        KTimer t(h, GS_K_EXPORT);
+        klaunch(k_export_marks, dim3(grid_for((h->cap + 31) / 32, 256, kExportBlocks)), dim3(256), h->stream, t.start(), t.stop(),
+                h->mark_buf, (const uint32_t*)h->parent, h->cap, (uint32_t*)out, cap, counter);
+    }
+    GS_HIP(hipGetLastError());
+    return GS_OK;
+}
+
+static int export_check(gs_cc_t* h, const char* fn) {
+    if (!h->mark_buf) return fail(GS_ERR_UNSUPPORTED, "%s: handle created without GS_CC_TRACK_MARKS", fn);
+    if (h->sparse) return fail(GS_ERR_UNSUPPORTED, "%s: sparse-id summary", fn);
+    return GS_OK;
+}
+
 int gs_cc_export_marks(gs_cc_t* h, void* pairs, uint64_t cap, uint64_t* n_out) {
     GS_TRY(check(h));
     if (!n_out) return fail(GS_ERR_INVALID, "gs_cc_export_marks: null n_out");
-    if (!h->mark) return fail(GS_ERR_UNSUPPORTED, "gs_cc_export_marks: handle created without GS_CC_TRACK_MARKS");
-    if (h->sparse) return fail(GS_ERR_UNSUPPORTED, "gs_cc_export_marks: sparse-id summary");
+    GS_TRY(export_check(h, "gs_cc_export_marks"));
     if (cap && !pairs) return fail(GS_ERR_INVALID, "gs_cc_export_marks: null output");
     DeviceGuard g(h->device);
     const bool dev = cap == 0 || is_device_pointer(pairs);
@@ -951,13 +971,7 @@ int gs_cc_export_marks(gs_cc_t* h, void* pairs, uint64_t cap, uint64_t* n_out) {
         GS_TRY(ensure_buf(&h->tmp, &h->tmp_bytes, cap * 8));
         out = h->tmp;
     }
-    GS_HIP(hipMemsetAsync(h->dscratch, 0, sizeof(unsigned long long), h->stream));
-    {
-        KTimer t(h, GS_K_EXPORT);
-        klaunch(k_export_marks, dim3(grid_for((h->cap + 31) / 32, 256, kExportBlocks)), dim3(256), h->stream, t.start(), t.stop(),
-                h->mark, (const uint32_t*)h->parent, h->cap, (uint32_t*)out, cap, h->dscratch);
-    }
-    GS_HIP(hipGetLastError());
+    GS_TRY(export_launch(h, out, cap, h->dscratch));
     GS_HIP(hipMemcpyAsync(h->hscratch, h->dscratch, 8, hipMemcpyDeviceToHost, h->stream));
     GS_TRY(sync_and_check(h));
     const uint64_t total = h->hscratch[0];
@@ -968,6 +982,24 @@ int gs_cc_export_marks(gs_cc_t* h, void* pairs, uint64_t cap, uint64_t* n_out) {
     }
     if (total > cap) return fail(GS_ERR_CAPACITY, "gs_cc_export_marks: %llu marked, capacity %llu (rest kept)",
                                  (unsigned long long)total, (unsigned long long)cap);
+    return GS_OK;
+}
+
+int gs_cc_export_marks_async(gs_cc_t* h, void* pairs, uint64_t cap, void* dev_count) {
+    GS_TRY(check(h));
+    GS_TRY(export_check(h, "gs_cc_export_marks_async"));
+    if (!dev_count || !is_device_pointer(dev_count) || (cap && (!pairs || !is_device_pointer(pairs))))
+        return fail(GS_ERR_INVALID, "gs_cc_export_marks_async: pairs and dev_count must be device pointers");
+    if (cap < h->cap) return fail(GS_ERR_CAPACITY, "gs_cc_export_marks_async: capacity %llu < vertex capacity %u",
+                                  (unsigned long long)cap, h->cap);
+    DeviceGuard g(h->device);
+    return export_launch(h, pairs, cap, static_cast<unsigned long long*>(dev_count));
+}
+
+int gs_cc_set_marking(gs_cc_t* h, int on) {
+    GS_TRY(check(h));
+    if (!h->mark_buf) return on ? fail(GS_ERR_UNSUPPORTED, "gs_cc_set_marking: handle created without GS_CC_TRACK_MARKS") : GS_OK;
+    h->mark = on ? h->mark_buf : nullptr;
     return GS_OK;
 }
 

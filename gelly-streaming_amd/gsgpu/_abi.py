@@ -37,7 +37,7 @@ EXPORTED_SYMBOLS = (
     "gs_cc_sync", "gs_cc_fold", "gs_cc_fold_pairs", "gs_cc_merge", "gs_cc_combine",
     "gs_cc_close_window", "gs_cc_stats", "gs_cc_emit_dense", "gs_cc_emit_pairs",
     "gs_cc_checksum", "gs_cc_find", "gs_cc_find_flags", "gs_cc_labels_device", "gs_cc_export_marks",
-    "gs_cc_fold_pairs32", "gs_cc_timing", "gs_cc_kernel_time", "gs_gen_rmat", "gs_gen_er", "gs_parse_edges",
+    "gs_cc_fold_pairs32", "gs_cc_export_marks_async", "gs_cc_set_marking", "gs_cc_timing", "gs_cc_kernel_time", "gs_gen_rmat", "gs_gen_er", "gs_parse_edges",
     "gs_bip_create", "gs_bip_destroy", "gs_bip_reset", "gs_bip_set_stream", "gs_bip_sync", "gs_bip_fold",
     "gs_bip_fold_pairs", "gs_bip_merge", "gs_bip_close_window", "gs_bip_status", "gs_bip_checksum",
     "gs_bip_emit_pairs",
@@ -87,6 +87,8 @@ def lib() -> ctypes.CDLL:
         "gs_cc_fold": [vp, vp, vp, u64],
         "gs_cc_fold_pairs": [vp, vp, u64],
         "gs_cc_fold_pairs32": [vp, vp, u64],
+        "gs_cc_set_marking": [vp, ctypes.c_int],
+        "gs_cc_export_marks_async": [vp, vp, u64, vp],
         "gs_cc_merge": [vp, vp],
         "gs_cc_combine": [vp, vp, P(vp)],
         "gs_cc_close_window": [vp],

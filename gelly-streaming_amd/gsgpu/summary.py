@@ -238,6 +238,16 @@ class DisjointSet:
         call("gs_cc_export_marks", self.handle, p, cap, ctypes.byref(n))
         return int(n.value)
 
+    def export_marks_async(self, out, count) -> None:
+        """export_marks enqueued on the stream; the pair count lands in the device int64 tensor
+        ``count`` (one element), no host sync."""
+        p, keep, total = _buf(out, 32, "out")
+        call("gs_cc_export_marks_async", self.handle, p, total // 2, ctypes.c_void_p(count.data_ptr()))
+
+    def set_marking(self, on: bool) -> None:
+        """Pause / resume marking (GS_CC_TRACK_MARKS): folds while paused are not exported."""
+        call("gs_cc_set_marking", self.handle, 1 if on else 0)
+
     # ---- instrumentation ----
     def timing(self, enable: bool) -> None:
         call("gs_cc_timing", self.handle, 1 if enable else 0)

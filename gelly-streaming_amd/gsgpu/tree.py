@@ -1,9 +1,18 @@
 """Multi-GPU CombineCC: per-window exchange of per-rank partial summaries.
 
-``GatherMerge`` (default for ConnectedComponents): the reference's windowAll reduce
-(SummaryBulkAggregation.java:81: every partition's partial summary goes to the one
-parallelism-1 task) as one flat gather to rank 0 — every other rank sends its window's pairs
-straight to rank 0 over its own xGMI link, all at once, and rank 0 folds them in one launch.
+Three exchanges behind one contract (``merge_window()`` after each window's fold; True on the
+rank that emitted):
+
+``AllgatherMerge`` (bench default): replicated summaries. Every rank keeps the GLOBAL summary: per
+window each rank exports its delta (the connectivity its own slice added), sends it to every
+other rank over that pair's own xGMI link (one batch of RCCL send/recv), and folds the others'
+deltas with marking paused. Every rank's filter is then the global giant component, so the
+deltas shrink to the genuinely new connectivity (RMAT-26, 8 ranks, window 64: 14K pairs per rank
+instead of 132K) and every rank's fold is as fast as a single GPU's (tools/sim_ranks.py).
+``GatherMerge``: the reference's windowAll reduce (SummaryBulkAggregation.java:81: every
+partition's partial summary goes to the one parallelism-1 task) as one flat gather to rank 0 —
+every other rank sends its window's pairs straight to rank 0 over its own xGMI link, all at once,
+and rank 0 folds them.
 ``TreeMerge`` (ConnectedComponentsTree): log2(P) pairwise rounds (SummaryTreeReduce.enhance).
 
 Restates the reference's tree reduction ``SummaryTreeReduce.enhance``
@@ -245,3 +254,127 @@ class GatherMerge:
                 for w in self.works[t]:
                     w.wait()
                 self.works[t] = []
+
+
+# A receiver folding several ranks' deltas at once: while their big components are still separate
+# (young windows) each delta must go in its own fold call, so that call's short head launch joins
+# its components before the bulk arrives (csrc/cc_api.hip, merge_head); small deltas go in one call.
+BULK_DELTA_PAIRS = 1 << 21
+
+
+def fold_deltas(summary, buf, counts) -> None:
+    """Fold the deltas laid out back to back in ``buf`` (counts[i] pairs each)."""
+    total = sum(counts)
+    if total == 0:
+        return
+    if max(counts) <= BULK_DELTA_PAIRS:
+        summary.fold_pairs(buf, total, id_bits=32)
+        return
+    off = 0
+    for c in counts:
+        if c:
+            summary.fold_pairs(buf[2 * off: 2 * (off + c)], c, id_bits=32)
+            off += c
+
+
+class AllgatherMerge:
+    """Replicated global summary on every rank; per window an all-pairs exchange of deltas.
+
+    Per window, every rank: export its marks (its slice's new connectivity relative to the global
+    summary it held) into ``sendbuf``; all-gather the counts (one small collective, one host
+    sync); one batch of send/recv: its delta to every peer, every peer's delta into one
+    contiguous buffer (on xGMI each pair of GPUs has its own link, so all P(P-1) transfers run at
+    once); fold the received deltas with marking paused (they are the others' to export, not
+    this rank's); close the window. All ranks then hold the same partition (the union of all
+    ranks' edges); rank 0 reports the emission. Correctness argument: a delta holds (v, root(v))
+    for every root the exporting rank hooked and every self-loop first touch, so it carries
+    every component join of that rank's window; joins are idempotent, so it applies to any
+    summary of the same prior partition (tests/test_tree_gloo.py).
+    The summary needs ``export_marks``, ``fold_pairs``, ``set_marking``, ``close_window`` and
+    must have been created with marks tracked (GS_CC_TRACK_MARKS) on EVERY rank.
+    """
+
+    def __init__(self, summary, capacity_pairs: int, device: torch.device, group=None):
+        self.summary = summary
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = torch.device(device)
+        self.cap = int(capacity_pairs)
+        self.stage = (dist.get_backend(group) == "gloo" and self.device.type == "cuda")
+        cdev = "cpu" if (self.stage or self.device.type == "cpu") else self.device
+        self.cnt = torch.zeros(1, dtype=torch.int64, device=cdev)
+        self.cnts = torch.zeros(self.world, dtype=torch.int64, device=cdev)
+        # device summaries export asynchronously into a device count (the collective's input
+        # under RCCL; copied to the host first under gloo)
+        self.dcnt = None
+        if self.device.type == "cuda" and hasattr(summary, "export_marks_async"):
+            self.dcnt = self.cnt if self.cnt.is_cuda else torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.sendbuf = torch.empty(2 * self.cap, dtype=torch.int32, device=self.device)
+        self.recvbuf = torch.empty(2 * max(self.cap, 1), dtype=torch.int32, device=self.device)
+        self.hsend = torch.empty(0, dtype=torch.int32)
+        self.hrecv = torch.empty(0, dtype=torch.int32)
+        self.bytes_sent = 0
+        self.bytes_recv = 0
+        # communicators up (all ranks take part) before the first partial point-to-point batch
+        dist.all_gather_into_tensor(self.cnts, self.cnt, group=self.group)
+
+    def _grank(self, r: int) -> int:
+        return r if self.group is None else dist.get_global_rank(self.group, r)
+
+    def _host(self, attr: str, n: int) -> torch.Tensor:
+        t = getattr(self, attr)
+        if t.numel() < n:
+            t = torch.empty(max(n, 2 * t.numel()), dtype=torch.int32)
+            if self.device.type == "cuda":
+                t = t.pin_memory()
+            setattr(self, attr, t)
+        return t
+
+    def merge_window(self) -> bool:
+        if self.world == 1:
+            self.summary.close_window()
+            return True
+        if self.dcnt is not None:
+            # count straight from the device into the collective: one host sync per window
+            self.summary.export_marks_async(self.sendbuf, self.dcnt)
+            if self.stage:
+                self.cnt.copy_(self.dcnt)
+            dist.all_gather_into_tensor(self.cnts, self.cnt, group=self.group)
+            counts = [int(x) for x in self.cnts.tolist()]
+            n = counts[self.rank]
+        else:
+            n = self.summary.export_marks(self.sendbuf, self.cap)
+            self.cnt.fill_(n)
+            dist.all_gather_into_tensor(self.cnts, self.cnt, group=self.group)
+            counts = [int(x) for x in self.cnts.tolist()]
+        others = [(q, counts[q]) for q in range(self.world) if q != self.rank]
+        total = sum(c for _, c in others)
+        if total > self.recvbuf.numel() // 2:
+            self.recvbuf = torch.empty(2 * total, dtype=torch.int32, device=self.device)
+        send, recv = self.sendbuf, self.recvbuf
+        if self.stage:                                   # gloo moves host tensors only
+            send = self._host("hsend", 2 * n)
+            if n:
+                send[: 2 * n].copy_(self.sendbuf[: 2 * n])
+            recv = self._host("hrecv", 2 * total)
+        ops, off = [], 0
+        for q, c in others:
+            if n:
+                ops.append(dist.P2POp(dist.isend, send[: 2 * n], self._grank(q), group=self.group))
+            if c:
+                ops.append(dist.P2POp(dist.irecv, recv[2 * off: 2 * (off + c)], self._grank(q), group=self.group))
+                off += c
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        if self.stage and total:
+            self.recvbuf[: 2 * total].copy_(recv[: 2 * total])
+        self.bytes_sent += 8 * n * (self.world - 1)
+        self.bytes_recv += 8 * total
+        if total:
+            self.summary.set_marking(False)
+            fold_deltas(self.summary, self.recvbuf, [c for _, c in others])
+            self.summary.set_marking(True)
+        self.summary.close_window()
+        return self.rank == 0

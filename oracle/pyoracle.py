@@ -334,11 +334,14 @@ class PyMarkedSummary:
         a = np.asarray(buf.cpu() if hasattr(buf, "cpu") else buf)[: 2 * n].astype(np.int64)
         self.fold(a[0::2], a[1::2])
 
+    def set_marking(self, on: bool) -> None:
+        self.track = bool(on)
+
     def export_marks(self, buf, cap: int) -> int:
         vs = np.nonzero(self.mark)[0][:cap]
         out = np.empty(2 * len(vs), dtype=np.int32)
         out[0::2] = vs
-        out[1::2] = self.parent[vs]
+        out[1::2] = [self._root(int(v)) for v in vs]           # (v, root), as k_export_marks
         self.mark[vs] = False
         if hasattr(buf, "copy_"):
             import torch

@@ -284,6 +284,7 @@ def test_tree_exchange_single_process(oracle, torch_cuda, world):
                 if role == "send":
                     m = ranks[r].export_marks(buf)
                     ranks[peer].fold_pairs(buf, m, id_bits=32)
+                    ranks[peer].sync()          # buf is reused by the next export (other stream)
                     done.add(r)
         ranks[0].close_window()
         np.testing.assert_array_equal(ranks[0].dense().astype(np.int64), want[w], err_msg="window %d" % w)
@@ -382,7 +383,7 @@ def test_cc_example_file_input(tmp_path):
 
 
 # ---------------- bench.py multi-rank path (2 ranks on one GPU, gloo-staged exchange) ----------------
-@pytest.mark.parametrize("merge", ["gather", "tree"])
+@pytest.mark.parametrize("merge", ["allgather", "gather", "tree"])
 def test_bench_two_ranks_one_gpu_verified(merge):
     import subprocess, sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

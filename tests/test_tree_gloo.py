@@ -1,5 +1,5 @@
 """CPU, multi-process: the multi-GPU CombineCC exchanges (gsgpu/tree.py: flat gather, pairwise
-tree) under gloo, world 2 and 4.
+tree, replicated all-pairs delta exchange) under gloo, world 2 and 4.
 
 Each rank folds its contiguous slice of every window into a CPU summary model with the same
 export/fold contract as the device summary (oracle/pyoracle.py: PyMarkedSummary); the ranks run
@@ -28,14 +28,15 @@ def _worker(rank, world, port, src, dst, W, cap, outdir, kind):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "gelly-streaming_amd"), os.path.join(root, "oracle")]
-    from gsgpu.tree import GatherMerge, TreeMerge
+    from gsgpu.tree import AllgatherMerge, GatherMerge, TreeMerge
     from pyoracle import PyMarkedSummary
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        summ = PyMarkedSummary(cap, track_marks=(rank != 0))
-        tm = (TreeMerge if kind == "tree" else GatherMerge)(summ, capacity_pairs=cap, device=torch.device("cpu"))
+        summ = PyMarkedSummary(cap, track_marks=(kind == "allgather" or rank != 0))
+        cls = {"tree": TreeMerge, "gather": GatherMerge, "allgather": AllgatherMerge}[kind]
+        tm = cls(summ, capacity_pairs=cap, device=torch.device("cpu"))
         emis = []
         n = len(src)
         for lo in range(0, n, W):
@@ -44,17 +45,17 @@ def _worker(rank, world, port, src, dst, W, cap, outdir, kind):
             if kind == "gather":
                 tm.before_fold()
             summ.fold(src[a:b], dst[a:b])
-            if tm.merge_window():
+            if tm.merge_window() or kind == "allgather":      # allgather: every rank is a replica
                 emis.append(summ.dense())
         if kind == "gather":
             tm.drain()
-        if rank == 0:
-            np.save(os.path.join(outdir, "emis.npy"), np.stack(emis))
+        if rank == 0 or kind == "allgather":
+            np.save(os.path.join(outdir, "emis%d.npy" % rank), np.stack(emis))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["tree", "gather"])
+@pytest.mark.parametrize("kind", ["tree", "gather", "allgather"])
 @pytest.mark.parametrize("world", [2, 4])
 def test_tree_merge_gloo_matches_oracle(tmp_path, oracle, world, kind):
     s, d = oracle.gen_rmat(0, 6000, 10, 21)
@@ -62,8 +63,9 @@ def test_tree_merge_gloo_matches_oracle(tmp_path, oracle, world, kind):
     s = np.concatenate([s, [1000, 1001]]); d = np.concatenate([d, [1000, 1001]])
     cap, W = 1024, 1000
     mp.spawn(_worker, args=(world, _free_port(), s, d, W, cap, str(tmp_path), kind), nprocs=world, join=True)
-    got = np.load(tmp_path / "emis.npy")
     from pyoracle import EMIT_DENSE
     want = oracle.run(s, d, W, partitions=world, emit=EMIT_DENSE, label_cap=cap)["labels"]
-    assert got.shape == want.shape
-    np.testing.assert_array_equal(got, want)
+    for r in range(world if kind == "allgather" else 1):
+        got = np.load(tmp_path / ("emis%d.npy" % r))
+        assert got.shape == want.shape
+        np.testing.assert_array_equal(got, want, err_msg="rank %d" % r)

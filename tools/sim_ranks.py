@@ -4,7 +4,9 @@ step is timed with HIP events. Measures what a multi-GPU run cannot show from a 
 payload (pairs) each exchange moves per window and the merge folds on the receiving ranks; the
 xGMI transfer time is modelled as bytes / 150 GB/s per link.
 
-usage (GPU box): python tools/sim_ranks.py P windows [scheme ...]   schemes: gather tree
+usage (GPU box): python tools/sim_ranks.py P windows [scheme ...]   schemes: gather tree allgather
+(allgather: every rank keeps the global summary; per window each rank's delta goes to every other
+rank over its own link and every rank folds the others' deltas with marking paused)
 """
 import os, sys, time
 import torch
@@ -12,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "gelly-streaming_amd")]
 import gsgpu
 from gsgpu import gen
-from gsgpu.tree import tree_schedule
+from gsgpu.tree import fold_deltas, tree_schedule
 from gsgpu._abi import GS_K_FOLD, GS_K_COMPRESS
 
 P = int(sys.argv[1]) if len(sys.argv) > 1 else 8
@@ -45,7 +47,10 @@ _wa.close(); _wb.close()
 torch.cuda.synchronize()
 
 for scheme in schemes:
-    ranks = [gsgpu.DisjointSet(V, id_bits=32, track_marks=(r != 0), stream=torch.cuda.current_stream()) for r in range(P)]
+    ag = scheme == "allgather"       # replicated summaries: every rank folds every other rank's delta
+    ranks = [gsgpu.DisjointSet(V, id_bits=32, track_marks=(ag or r != 0), stream=torch.cuda.current_stream()) for r in range(P)]
+    if ag:
+        dbufs = [torch.empty(2 * V, dtype=torch.int32, device="cuda") for _ in range(P)]
     scheds = [tree_schedule(r, P) for r in range(P)]
     print("== %s P=%d scale=%d W/rank=2^%d" % (scheme, P, scale, W.bit_length() - 1), flush=True)
     tot = dict(fold=0.0, close=0.0, crit=0.0, xfer=0.0, merge=0.0, pairs=0)
@@ -56,7 +61,29 @@ for scheme in schemes:
             _, t = timed(lambda: ranks[r].fold(s, d))
             fold_us.append(t)
         merge_us, xfer_us, npairs = 0.0, 0.0, []
-        if scheme == "gather":
+        if ag:
+            tex = []
+            cnt_dev = torch.zeros(P, dtype=torch.int64, device="cuda")
+            for r in range(P):
+                _, te = timed(lambda: ranks[r].export_marks_async(dbufs[r], cnt_dev[r:r + 1]))
+                tex.append(te)
+            ns = [int(x) for x in cnt_dev.tolist()]
+            npairs = ns
+            xfer_us = max(tex) + 8 * max(ns) / LINK * 1e6     # all pairs of links at once
+            mt = []
+            for r in range(P):
+                parts = [dbufs[q][:2 * ns[q]] for q in range(P) if q != r and ns[q]]
+                tot_n = sum(ns) - ns[r]
+                if parts:
+                    torch.cat(parts, out=buf[:2 * tot_n])
+                ranks[r].set_marking(False)
+                _, tf = timed(lambda: fold_deltas(ranks[r], buf, [ns[q] for q in range(P) if q != r]))
+                ranks[r].set_marking(True)
+                mt.append(tf)
+            merge_us = max(mt)
+            if os.environ.get("SIM_VERBOSE") and w < 3:
+                print("   w%d deltas %s merge %s" % (w + 1, ns, ["%.0f" % x for x in mt]), flush=True)
+        elif scheme == "gather":
             per = []
             for r in range(1, P):
                 n, te = timed(lambda: ranks[r].export_marks(buf))
@@ -81,7 +108,7 @@ for scheme in schemes:
         for r in range(P):
             _, t = timed(lambda: ranks[r].close_window())
             close_us.append(t)
-        crit = max(fold_us) + xfer_us + merge_us + close_us[0]
+        crit = max(fold_us) + xfer_us + merge_us + (max(close_us) if ag else close_us[0])
         tot["fold"] += max(fold_us); tot["close"] += close_us[0]; tot["crit"] += crit
         tot["xfer"] += xfer_us; tot["merge"] += merge_us; tot["pairs"] += sum(npairs)
         print("w%3d fold max %6.0f us (r0 %6.0f)  pairs %8d (max %7d)  xfer %6.0f  merge folds %6.0f  close r0 %5.0f  "
