@@ -29,7 +29,7 @@ import torch.distributed as dist  # noqa: E402
 
 import gsgpu  # noqa: E402
 from gsgpu import gen  # noqa: E402
-from gsgpu._abi import GS_K_COMPRESS, GS_K_FOLD  # noqa: E402
+from gsgpu._abi import GS_K_COMPRESS, GS_K_EXPORT, GS_K_FOLD, GS_K_MERGE  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "streaming CC edges/sec (RMAT-26) at 1/2/4/8 MI355X + % of HBM roofline"
@@ -147,6 +147,8 @@ def main():
     elapsed = t1 - t0
     fold_ms, fold_n = ds.kernel_time(GS_K_FOLD)
     comp_ms, comp_n = ds.kernel_time(GS_K_COMPRESS)
+    merge_ms, _ = ds.kernel_time(GS_K_MERGE)
+    export_ms, _ = ds.kernel_time(GS_K_EXPORT)
     ds.timing(False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -242,6 +244,15 @@ def main():
             "final_vertices": nv,
             "final_components": nc,
         }
+        if world > 1:                                # rank 0's side of the exchange
+            line["exchange"] = {
+                "merge": a.merge,
+                "merge_fold_ms_per_window": merge_ms / max(folds, 1),
+                "export_ms_per_window": export_ms / max(folds, 1),
+                "bytes_sent_per_window": tree.bytes_sent / max(a.warmup + a.steps, 1) / nwin,
+                "bytes_recv_per_window": tree.bytes_recv / max(a.warmup + a.steps, 1) / nwin,
+                "wall_ms_per_window": elapsed / a.steps / nwin * 1e3,
+            }
         if verify is not None:
             line["verify"] = verify
         if latency is not None:

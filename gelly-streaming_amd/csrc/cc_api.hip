@@ -88,6 +88,7 @@ struct gs_cc {
     bool minkey_valid = false;
     // instrumentation
     bool timing = false;
+    int fold_timer = GS_K_FOLD;          // GS_K_MERGE while folding an exported partial summary
     struct Pend { int k; hipEvent_t a, b; };
     std::vector<Pend> pending;
     std::vector<hipEvent_t> pool;
@@ -230,7 +231,7 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
     f.halve = AOS ? merge_halve() : young ? young_halve() : 1u;
     const bool vec = std::is_same<IdT, uint32_t>::value && !AOS &&
                      ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
-    KTimer t(h, GS_K_FOLD);
+    KTimer t(h, h->fold_timer);
 #define GS_LAUNCH_FOLD(MARKV, VECV, EPTV, STV)                                                                       \
     klaunch((k_fold<IdT, AOS, MARKV, VECV, EPTV, STV>), dim3(grid), dim3(kFoldThreads), h->stream, t.start(), t.stop(), \
             (const IdT*)a, (const IdT*)b, f)
@@ -262,7 +263,7 @@ void launch_fold_ring(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t
     }
     const HotArgs hot{h->hot, h->hot_bits, h->hot_cand};
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
-    KTimer t(h, GS_K_FOLD);
+    KTimer t(h, h->fold_timer);
     const bool st = h->dstats != nullptr;
     const dim3 grid(grid_for(n / 4, kHotThreads, (unsigned)std::max(h->cus, 1)));
     if (h->mark) {
@@ -368,7 +369,7 @@ void launch_fold_sparse(gs_cc_t* h, const int64_t* a, const int64_t* b, uint64_t
             m = std::min(m, std::max<uint64_t>(std::min(kYoungChunk, young_limit - h->edges_since_reset), 1));
         FoldArgs f{m, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
         const unsigned grid = grid_for((m + 1) / 2, 256, 16384);
-        KTimer t(h, GS_K_FOLD);
+        KTimer t(h, h->fold_timer);
         const int64_t* pa = a + (aos ? 2 * off : off);
         const int64_t* pb = aos ? nullptr : b + off;
         if (aos) {
@@ -738,7 +739,10 @@ int gs_cc_fold_pairs(gs_cc_t* h, const void* pairs, uint64_t n) {
 
 int gs_cc_fold_pairs32(gs_cc_t* h, const void* pairs, uint64_t n) {
     GS_TRY(check(h));
-    return fold_impl(h, pairs, nullptr, n, true, 32);
+    h->fold_timer = GS_K_MERGE;          // a partial summary: timed as CombineCC, not UpdateCC
+    const int rc = fold_impl(h, pairs, nullptr, n, true, 32);
+    h->fold_timer = GS_K_FOLD;
+    return rc;
 }
 
 int gs_cc_merge(gs_cc_t* into, gs_cc_t* from) {

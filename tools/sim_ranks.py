@@ -68,6 +68,8 @@ for scheme in schemes:
                 _, te = timed(lambda: ranks[r].export_marks_async(dbufs[r], cnt_dev[r:r + 1]))
                 tex.append(te)
             ns = [int(x) for x in cnt_dev.tolist()]
+            if os.environ.get("SIM_VERBOSE") and w in (0, 15, 63):
+                print("   w%d export wall us %s" % (w + 1, ["%.0f" % x for x in tex]), flush=True)
             npairs = ns
             xfer_us = max(tex) + 8 * max(ns) / LINK * 1e6     # all pairs of links at once
             mt = []
