@@ -73,6 +73,7 @@ struct gs_cc {
     size_t tmp_bytes = 0;
     bool compressed = true;
     uint64_t edges_since_reset = 0;      // drives the young-forest launch split (fold_impl)
+    uint64_t ring_launches = 0;          // ring fold launches since reset (hot-set admission cadence)
     uint64_t closes = 0;                 // compressions since reset (giant re-sampled every kPickEvery)
     unsigned long long* dstats = nullptr;    // GSGPU_FOLD_STATS=1: per-window fold counters
     uint2* hot = nullptr;                // LDS hot set master copy (kHotBuckets uint2), steady folds
@@ -129,7 +130,8 @@ static bool timing_markers() {
 // Times one span of launches of kernel class k (HIP events on the launch stream). Launch the
 // span's first kernel with start() and its last with stop() through klaunch().
 // the current giant-state slot (cc_kernels.hpp): derr[1 + 2 * (closes & 1)] = giant, [+1] = built;
-// close c reads slot c & 1 and writes slot (c + 1) & 1; derr[5] = hot set owner
+// close c reads slot c & 1 and writes slot (c + 1) & 1; derr[5] = hot set owner, derr[6] = hot
+// set admission budget
 inline uint32_t* giant_state(gs_cc_t* h) { return h->derr + 1 + 2 * (h->closes & 1); }
 
 struct KTimer {
@@ -261,7 +263,18 @@ void launch_fold_ring(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t
         (void)hipMalloc(&h->dstats, 8 * sizeof(unsigned long long));
         (void)hipMemsetAsync(h->dstats, 0, 8 * sizeof(unsigned long long), h->stream);
     }
-    const HotArgs hot{h->hot, h->hot_bits, h->hot_cand};
+    HotArgs hot{h->hot, h->hot_bits, h->hot_cand};
+    // A/B knobs: GSGPU_HOT_SAMPLE (edges of each launch offered for admission), GSGPU_HOT_PROBE
+    static const uint64_t sample = env_u64("GSGPU_HOT_SAMPLE", kHotSampleEdges);
+    static const uint32_t probe = (uint32_t)env_u64("GSGPU_HOT_PROBE", 1);
+    // admission: while the device budget lasts (cc_kernels.hpp), plus every GSGPU_HOT_ADMIT_EVERY-th
+    // launch (kHotAdmitEvery; 1 = every launch)
+    static const uint64_t every = std::max<uint64_t>(env_u64("GSGPU_HOT_ADMIT_EVERY", kHotAdmitEvery), 1);
+    hot.sample_edges = sample;
+    hot.budget = h->derr + 6;
+    hot.periodic = (h->ring_launches % every == every - 1) ? 1u : 0u;
+    ++h->ring_launches;
+    hot.probe = probe;
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
     KTimer t(h, h->fold_timer);
     const bool st = h->dstats != nullptr;
@@ -693,6 +706,10 @@ int gs_cc_reset(gs_cc_t* h) {
     // giant state (cc_kernels.hpp, giant_state()): both slots no giant / gbits built for none,
     // hot set owner none
     GS_HIP(hipMemsetAsync(h->derr + 1, 0xFF, 5 * sizeof(uint32_t), h->stream));
+    {
+        static const uint32_t budget = kHotAdmitLaunches;     // hot-set admission budget: derr[6]
+        GS_HIP(hipMemcpyAsync(h->derr + 6, &budget, sizeof(uint32_t), hipMemcpyHostToDevice, h->stream));
+    }
     if (h->hot) GS_HIP(hipMemsetAsync(h->hot, 0, kHotBuckets * sizeof(uint2), h->stream));
     if (h->hot_cand) GS_HIP(hipMemsetAsync(h->hot_cand, 0xFF, sizeof(uint32_t) << kHotCandBits, h->stream));
     if (h->sparse) {
@@ -705,6 +722,7 @@ int gs_cc_reset(gs_cc_t* h) {
     h->minkey_valid = false;
     h->edges_since_reset = 0;
     h->closes = 0;
+    h->ring_launches = 0;
     return GS_OK;
 }
 

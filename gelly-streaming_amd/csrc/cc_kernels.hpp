@@ -234,7 +234,18 @@ struct HotArgs {
     uint2* table;       // global master copy (kHotBuckets uint2), nullptr = no hot set
     uint32_t bits;      // B: every id < 2^B
     uint32_t* cand;     // 2^kHotCandBits candidate slots
+    uint64_t sample_edges = kHotSampleEdges;   // admission offers endpoints of a launch's first edges
+    uint32_t probe = 1;                        // 0: no LDS probes (A/B experiments)
+    uint32_t* budget = nullptr;                // admitting launches left (device word, see below)
+    uint32_t periodic = 0;                     // the host's periodic refresh: admit in this launch
 };
+
+// Admission cadence. Offering a launch's first 2^18 edges costs ~28 us per RMAT-26 window (the
+// candidate table's atomics); the hubs are stable, so a launch admits only while *budget > 0
+// (kHotAdmitLaunches after reset or after k_compress clears the set for a new giant) or when the
+// host's periodic refresh (every kHotAdmitEvery ring launches) asks: steady window 266 -> 240 us.
+constexpr uint32_t kHotAdmitLaunches = 8;
+constexpr uint32_t kHotAdmitEvery = 16;
 
 __device__ __forceinline__ void hot_admit(const HotArgs& hot, uint32_t v) {
     uint32_t* slot = &hot.cand[(uint32_t)(splitmix64(v) >> (64 - kHotCandBits))];
@@ -252,14 +263,15 @@ __device__ __forceinline__ void filter_group(const FoldArgs& f, const uint32_t (
     uint32_t wu[EPT], wv[EPT];
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
-        hu[k] = HOT && hot_probe(tab, u[k], hot.bits);
-        hv[k] = HOT && hot_probe(tab, v[k], hot.bits);
+        hu[k] = HOT && hot.probe && hot_probe(tab, u[k], hot.bits);
+        hv[k] = HOT && hot.probe && hot_probe(tab, v[k], hot.bits);
     }
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
         wu[k] = hu[k] ? ~0u : f.gbits[u[k] >> 5];
         wv[k] = hv[k] ? ~0u : f.gbits[v[k] >> 5];
     }
+
     if (HOT && STATS) {
         uint32_t nh = 0;
 #pragma unroll
@@ -415,7 +427,12 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const uint32_t* __res
     if (filt) {
         for (uint32_t i = threadIdx.x; i < kHotBuckets; i += blockDim.x) tab[i] = hot.table[i];
     }
+    // admitting launch? (read before workgroup 0's decrement may land: a workgroup that reads the
+    // decremented budget only skips this launch's admission, which is a heuristic anyway)
+    const uint32_t budget = hot.budget ? *hot.budget : 1u;
+    const uint64_t sample_edges = (hot.periodic || budget) ? hot.sample_edges : 0;
     __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0 && hot.budget && budget) *hot.budget = budget - 1;
     const int lane = threadIdx.x & 63;
     uint2* const ring = rings[threadIdx.x >> 6];
     uint32_t cnt = 0;                                // wave-uniform ring fill
@@ -442,7 +459,7 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const uint32_t* __res
             if (bad) atomicOr(f.rc.err, 1u);
         }
         if (STATS) for (int k = 0; k < 4; ++k) nvalid += ok[k];
-        if (filt) filter_group<STATS, 4, true>(f, u, v, ok, tab, hot, g * 4 < kHotSampleEdges);
+        if (filt) filter_group<STATS, 4, true>(f, u, v, ok, tab, hot, g * 4 < sample_edges);
         const uint32_t c = (uint32_t)ok[0] + ok[1] + ok[2] + ok[3];
         if (STATS) nkept += c;
         uint32_t incl = c;
@@ -613,6 +630,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
     const uint32_t g = s_g;
     if (s_clear && hot) {                            // workgroup 0 only: the hot set belonged to another component
         for (uint32_t i = threadIdx.x; i < kHotBuckets; i += blockDim.x) hot[i] = make_uint2(0u, 0u);
+        if (threadIdx.x == 0) owner[1] = kHotAdmitLaunches;    // refill: the admission budget
     }
     const int lane = threadIdx.x & 63;
     if (s_inc) {                                     // one bitmap word (32 vertices) per thread
