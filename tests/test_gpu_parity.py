@@ -290,6 +290,59 @@ def test_tree_exchange_single_process(oracle, torch_cuda, world):
         np.testing.assert_array_equal(ranks[0].dense().astype(np.int64), want[w], err_msg="window %d" % w)
 
 
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_replicated_exchange_single_process(oracle, torch_cuda, world):
+    """AllgatherMerge's protocol replayed with device handles on this GPU: every rank folds its
+    slice, exports its delta asynchronously (count in device memory), folds every other rank's
+    delta with marking paused, closes; EVERY replica's emission must equal the oracle's."""
+    torch = torch_cuda
+    from gsgpu.tree import fold_deltas
+    scale, n, W = 13, 200000, 20000
+    cap = 1 << scale
+    s, d = oracle.gen_rmat(0, n, scale, 9)
+    s = np.concatenate([s, [cap - 1, cap - 2]]); d = np.concatenate([d, [cap - 1, cap - 2]])
+    n = s.size
+    want = oracle.run(s, d, W, partitions=world, emit=EMIT_DENSE, label_cap=cap)["labels"]
+    cur = torch.cuda.current_stream()
+    ranks = [DisjointSet(cap, id_bits=32, track_marks=True, stream=cur) for _ in range(world)]
+    bufs = [torch.empty(2 * cap, dtype=torch.int32, device="cuda") for _ in range(world)]
+    cnt = torch.zeros(world, dtype=torch.int64, device="cuda")
+    recv = torch.empty(2 * cap * world, dtype=torch.int32, device="cuda")
+    ts = torch.from_numpy(s.astype(np.int32)).cuda()
+    td = torch.from_numpy(d.astype(np.int32)).cuda()
+    for w, lo in enumerate(range(0, n, W)):
+        ln = min(W, n - lo)
+        for r in range(world):
+            a, b = lo + (ln * r) // world, lo + (ln * (r + 1)) // world
+            ranks[r].fold(ts[a:b], td[a:b])
+            ranks[r].export_marks_async(bufs[r], cnt[r:r + 1])
+        ns = [int(x) for x in cnt.tolist()]
+        for r in range(world):
+            others = [q for q in range(world) if q != r]
+            tot = sum(ns[q] for q in others)
+            if tot:
+                torch.cat([bufs[q][:2 * ns[q]] for q in others], out=recv[:2 * tot])
+            ranks[r].set_marking(False)
+            fold_deltas(ranks[r], recv, [ns[q] for q in others])
+            ranks[r].set_marking(True)
+            ranks[r].close_window()
+        for r in range(world):
+            np.testing.assert_array_equal(ranks[r].dense().astype(np.int64), want[w], err_msg="window %d rank %d" % (w, r))
+    # folds while marking is paused leave nothing to export
+    ranks[0].reset()
+    e = lambda *x: torch.tensor(x, dtype=torch.int32, device="cuda")
+    ranks[0].set_marking(False)
+    ranks[0].fold(e(1, 7), e(2, 7))              # a join and a self-loop, unmarked
+    ranks[0].set_marking(True)
+    assert ranks[0].export_marks(bufs[0]) == 0
+    ranks[0].fold(e(3, 2), e(4, 9))              # 4 hooked under 3; 9 joins 1's component
+    m = ranks[0].export_marks(bufs[0])
+    got = sorted(map(tuple, bufs[0][:2 * m].view(-1, 2).cpu().numpy().tolist()))
+    assert got == [(4, 3), (9, 1)]
+    with pytest.raises(GsError):
+        DisjointSet(cap, id_bits=32).set_marking(True)       # no marks tracked
+
+
 # ---------------- full-size properties (independent torch checker) ----------------
 def _torch_min_labels(torch, src, dst, V):
     """Independent min-label CC on the GPU with torch ops (hook-to-min + pointer jumping)."""
