@@ -275,6 +275,8 @@ void launch_fold_ring(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t
     hot.periodic = (h->ring_launches % every == every - 1) ? 1u : 0u;
     ++h->ring_launches;
     hot.probe = probe;
+    static const bool five_ok = env_u64("GSGPU_HOT_FIVE", 1) != 0;
+    hot.five = (five_ok && h->hot_bits <= kHotBucketBits + 12) ? 1u : 0u;
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
     KTimer t(h, h->fold_timer);
     const bool st = h->dstats != nullptr;
