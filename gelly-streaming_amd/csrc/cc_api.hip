@@ -277,6 +277,8 @@ void launch_fold_ring(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t
     hot.probe = probe;
     static const bool five_ok = env_u64("GSGPU_HOT_FIVE", 1) != 0;
     hot.five = (five_ok && h->hot_bits <= kHotBucketBits + 12) ? 1u : 0u;
+    static const uint32_t thresh = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(env_u64("GSGPU_HOT_THRESH", 3), 2), 63);
+    hot.thresh = thresh;
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
     KTimer t(h, h->fold_timer);
     const bool st = h->dstats != nullptr;
@@ -709,7 +711,7 @@ int gs_cc_reset(gs_cc_t* h) {
     // hot set owner none
     GS_HIP(hipMemsetAsync(h->derr + 1, 0xFF, 5 * sizeof(uint32_t), h->stream));
     {
-        static const uint32_t budget = kHotAdmitLaunches;     // hot-set admission budget: derr[6]
+        static const uint32_t budget = (uint32_t)env_u64("GSGPU_HOT_BUDGET", kHotAdmitLaunches);   // derr[6]
         GS_HIP(hipMemcpyAsync(h->derr + 6, &budget, sizeof(uint32_t), hipMemcpyHostToDevice, h->stream));
     }
     if (h->hot) GS_HIP(hipMemsetAsync(h->hot, 0, kHotBuckets * sizeof(uint2), h->stream));

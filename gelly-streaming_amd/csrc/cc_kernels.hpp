@@ -268,6 +268,8 @@ struct HotArgs {
     uint32_t* budget = nullptr;                // admitting launches left (device word, see below)
     uint32_t periodic = 0;                     // the host's periodic refresh: admit in this launch
     uint32_t five = 0;                         // slot format: 5 x 12 bits (B <= 26) instead of 4 x 16
+    uint32_t thresh = 2;                       // sightings before admission (> 2 needs B <= 26;
+                                               // the host passes 3: steady window 233 -> 229 us)
 };
 
 // Admission cadence. Offering a launch's first 2^18 edges costs ~28 us per RMAT-26 window (the
@@ -279,7 +281,18 @@ constexpr uint32_t kHotAdmitEvery = 16;
 
 __device__ __forceinline__ void hot_admit(const HotArgs& hot, uint32_t v) {
     uint32_t* slot = &hot.cand[(uint32_t)(splitmix64(v) >> (64 - kHotCandBits))];
-    if (__hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == v) hot_insert(hot.table, v, hot.bits, hot.five != 0);
+    const uint32_t x = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (hot.thresh > 2 && hot.bits <= 26) {          // slot = id << 6 | sightings
+        if ((x >> 6) == v) {
+            const uint32_t c = (x & 63u) + 1;
+            if (c >= hot.thresh) hot_insert(hot.table, v, hot.bits, hot.five != 0);
+            else __hip_atomic_store(slot, (v << 6) | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(slot, (v << 6) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+    if (x == v) hot_insert(hot.table, v, hot.bits, hot.five != 0);
     else __hip_atomic_store(slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
