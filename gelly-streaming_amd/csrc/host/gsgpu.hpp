@@ -118,6 +118,19 @@ public:
         l.resize(got);
     }
 
+    // Merger checkpoint (ListCheckpointed, SummaryAggregation.java:127-135): the summary as its
+    // canonical (vertex, label) pairs; restore = reset + union(v, label) for every pair
+    void snapshot(std::vector<K>& v, std::vector<K>& l) { pairs(v, l); }
+    void restore(const std::vector<K>& v, const std::vector<K>& l) {
+        if (v.size() != l.size()) throw GsError(GS_ERR_INVALID, "restore: vertices / labels differ in length");
+        reset();
+        if (v.empty()) return;
+        std::vector<K> inter(2 * v.size());
+        for (size_t i = 0; i < v.size(); ++i) { inter[2 * i] = v[i]; inter[2 * i + 1] = l[i]; }
+        check(gs_cc_fold_pairs(h_, inter.data(), v.size()), "gs_cc_fold_pairs");
+        check(gs_cc_close_window(h_), "gs_cc_close_window");
+    }
+
     // toString (:133-150): {root=[members...], ...}, roots and members ascending
     std::string toString() {
         std::vector<K> v, l;

@@ -90,6 +90,20 @@ class SummaryBulkAggregation:
         self.window_edges = window_edges
         self.mode = mode
         self.sparse = sparse          # None: sparse ids (GS_CC_SPARSE_IDS) iff some id is < 0 or >= 2^32 - 1
+        self._summary: Optional[DisjointSet] = None      # the Merger's cumulative summary
+        self._restored = None                            # restoreState's snapshot, for the next run
+
+    # ---- Merger checkpointing (ListCheckpointed<S>, SummaryAggregation.java:127-135) ----
+    def snapshotState(self, checkpointId: int = 0, timestamp: int = 0) -> list:
+        """Collections.singletonList(summary): the cumulative summary as canonical
+        (vertices, labels); an empty list before the first emission (summary == initialVal)."""
+        if self._summary is None:
+            return []
+        return [self._summary.snapshot()]
+
+    def restoreState(self, state: list) -> None:
+        """summary = list.get(0): the next run() starts its Merger from this snapshot."""
+        self._restored = state[0] if state else None
 
     def _use_sparse(self, stream: SimpleEdgeStream) -> bool:
         if self.sparse is not None:
@@ -98,6 +112,9 @@ class SummaryBulkAggregation:
             return False
         lo = min(int(stream.src.min()), int(stream.dst.min()))
         hi = max(int(stream.src.max()), int(stream.dst.max()))
+        if self._restored is not None and len(self._restored[0]):
+            rv = np.asarray(self._restored[0], dtype=np.int64)
+            lo, hi = min(lo, int(rv.min())), max(hi, int(rv.max()))
         return lo < 0 or hi >= 0xFFFFFFFF
 
     def _capacity(self, stream: SimpleEdgeStream) -> int:
@@ -115,6 +132,13 @@ class SummaryBulkAggregation:
     def run(self, stream: SimpleEdgeStream) -> Iterator[DisjointSet]:
         self._sparse_run = self._use_sparse(stream)
         cap = self._capacity(stream)
+        if self._restored is not None and len(self._restored[0]) and not self.vertex_capacity:
+            rv = np.asarray(self._restored[0], dtype=np.int64)
+            if self._sparse_run:                  # distinct ids of the stream and the snapshot
+                ids = [rv] + ([stream.src, stream.dst] if len(stream) else [])
+                cap = int(np.unique(np.concatenate(ids)).size)
+            else:
+                cap = max(cap, int(rv.max()) + 1)
         wins = stream.windows(self.time_millis, self.window_edges)
         if self.mode == "fused":
             yield from self._run_fused(stream, wins, cap)
@@ -123,6 +147,9 @@ class SummaryBulkAggregation:
 
     def _run_fused(self, stream, wins, cap) -> Iterator[DisjointSet]:
         summary = self._new(cap)
+        if self._restored is not None:
+            summary.restore(*self._restored)
+        self._summary = summary
         try:
             for w in wins:
                 if self.transient_state:
@@ -131,12 +158,16 @@ class SummaryBulkAggregation:
                 summary.close_window()
                 yield summary                      # Merger: collector.collect(summary)
         finally:
+            self._summary = None
             summary.close()
 
     def _run_reference(self, stream, wins, cap) -> Iterator[DisjointSet]:
         P = self.parallelism
         pool = [self._new(cap) for _ in range(P + 1)]
         summary: Optional[DisjointSet] = None     # Merger.summary = initialVal (empty)
+        if self._restored is not None:            # restoreState: the Merger resumes from it
+            summary = pool[P]
+            summary.restore(*self._restored)
         try:
             for w in wins:
                 lo, ln = w.start, w.stop - w.start
@@ -155,8 +186,10 @@ class SummaryBulkAggregation:
                 else:
                     summary = self.combine_fun.reduce(acc, summary)
                 summary.close_window()
+                self._summary = summary
                 yield summary
         finally:
+            self._summary = None
             for d in pool:
                 d.close()
 

@@ -224,6 +224,28 @@ class DisjointSet:
              l.ctypes.data_as(ctypes.c_void_p), nv, ctypes.byref(cnt))
         return v[:cnt.value].astype(np.int64), l[:cnt.value].astype(np.int64)
 
+    # ---- checkpoint / resume (Merger implements ListCheckpointed, SummaryAggregation.java:127-135) ----
+    def snapshot(self) -> Tuple[np.ndarray, np.ndarray]:
+        """The summary as its canonical (vertex, label) pairs, sorted by vertex: everything the
+        reference's snapshotState serialises (the DisjointSet's matches, here canonicalised)."""
+        return self.pairs()
+
+    def restore(self, vertices, labels) -> None:
+        """restoreState: this summary becomes the snapshotted one (reset, then union(v, label)
+        for every pair: the same vertex set and components, hence the same emission)."""
+        v = np.asarray(vertices, dtype=np.int64)
+        l = np.asarray(labels, dtype=np.int64)
+        if v.shape != l.shape:
+            raise ValueError("restore: %d vertices, %d labels" % (v.size, l.size))
+        self.reset()
+        if v.size == 0:
+            return
+        inter = np.empty(2 * v.size, dtype=np.int64)
+        inter[0::2] = v
+        inter[1::2] = l
+        self.fold_pairs(inter, v.size)
+        self.close_window()
+
     def labels_device_ptr(self) -> int:
         p = ctypes.c_void_p()
         call("gs_cc_labels_device", self.handle, ctypes.byref(p))

@@ -111,6 +111,52 @@ def test_streams_golden(case, mode, bits):
     assert w == case["labels"].shape[0]
 
 
+# ---------------- Merger checkpoint / resume (ListCheckpointed, SummaryAggregation.java:127-135) ----------------
+@pytest.mark.parametrize("bits", [32, 64])
+@pytest.mark.parametrize("mode", ["fused", "reference"])
+@pytest.mark.parametrize("case", _streams()[:3], ids=lambda c: c["name"])
+def test_merger_checkpoint_resume(case, mode, bits):
+    """Run k windows, snapshotState, restore into a NEW operator and run the rest of the stream:
+    every later emission equals the uninterrupted pipeline's (the golden labels)."""
+    W = case["window_edges"]
+    nwin = case["labels"].shape[0]
+    k = max(1, nwin // 2)
+    kw = dict(window_edges=W, parallelism=case["partitions"], mode=mode, id_bits=bits, vertex_capacity=case["cap"])
+    cc = ConnectedComponents(1000, **kw)
+    for w, ds in enumerate(SimpleEdgeStream(case["src"][:k * W], case["dst"][:k * W]).aggregate(cc)):
+        if w == k - 1:
+            state = cc.snapshotState(1, 0)
+    assert len(state) == 1
+    cc2 = ConnectedComponents(1000, **kw)
+    cc2.restoreState(state)
+    w = k
+    for ds in SimpleEdgeStream(case["src"][k * W:], case["dst"][k * W:]).aggregate(cc2):
+        np.testing.assert_array_equal(ds.dense().astype(np.int64), case["labels"][w], err_msg="window %d" % w)
+        w += 1
+    assert w == nwin
+
+
+def test_snapshot_restore_sparse_ids(oracle):
+    """DisjointSet.snapshot / restore with ids across the whole long range (GS_CC_SPARSE_IDS)."""
+    rng = np.random.default_rng(7)
+    ids = rng.integers(-(1 << 62), 1 << 62, size=3000, dtype=np.int64)
+    ids[:3] = [-1, np.iinfo(np.int64).min, np.iinfo(np.int64).max]
+    src = ids[rng.integers(0, ids.size, 8000)]
+    dst = ids[rng.integers(0, ids.size, 8000)]
+    a = DisjointSet(ids.size, id_bits=64, sparse=True)
+    a.fold(src[:5000], dst[:5000])
+    a.close_window()
+    snap = a.snapshot()
+    b = DisjointSet(ids.size, id_bits=64, sparse=True)
+    b.restore(*snap)
+    assert b.toString() == a.toString()
+    a.fold(src[5000:], dst[5000:]); b.fold(src[5000:], dst[5000:])
+    va, la = a.pairs(); vb, lb = b.pairs()
+    np.testing.assert_array_equal(va, vb)
+    np.testing.assert_array_equal(la, lb)
+    a.close(); b.close()
+
+
 # ---------------- larger random streams vs the C oracle ----------------
 @pytest.mark.parametrize("gen,scale,n,W", [("rmat", 16, 1 << 20, 1 << 16), ("er", 17, 1 << 19, 100003),
                                            ("rmat", 12, 300000, 4096)])
