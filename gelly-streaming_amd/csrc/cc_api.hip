@@ -221,16 +221,30 @@ static int young_ept() {
 static bool young_halve() { static const bool v = env_u64("GSGPU_YOUNG_HALVE", 1) != 0; return v; }
 static bool merge_halve() { static const bool v = env_u64("GSGPU_MERGE_HALVE", 1) != 0; return v; }
 
+// young forest as ONE launch with a dynamic chunk counter (k_fold f.work; GSGPU_YOUNG_PERSIST=0:
+// launches of young_chunk() edges), GSGPU_YOUNG_BPC workgroups per CU (edges in flight = CUs x
+// BPC x 256 x EPT). RMAT-26 window 1: 64 launches 1746 us (+ 63 launch gaps of ~6 us), one
+// launch with 2 workgroups per CU 1403 us; 4 per CU 2265 us (more edges in flight, more hub
+// contention).
+static bool young_persist() { static const bool v = env_u64("GSGPU_YOUNG_PERSIST", 1) != 0; return v; }
+static unsigned young_bpc() { static const unsigned v = (unsigned)std::max<uint64_t>(env_u64("GSGPU_YOUNG_BPC", 2), 1); return v; }
+
 template <typename IdT, bool AOS>
 void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool young = false) {
     const int ept = (young && young_ept()) ? young_ept() : fold_ept();
-    const unsigned grid = grid_for((n + ept - 1) / ept, kFoldThreads, 16384);
+    const bool persist = young && young_persist() && h->cus > 0;
+    const unsigned grid = persist ? (unsigned)std::min<uint64_t>((uint64_t)h->cus * young_bpc(), grid_for((n + ept - 1) / ept, kFoldThreads, 1u << 20))
+                                  : grid_for((n + ept - 1) / ept, kFoldThreads, 16384);
     if (fold_stats_on() && !h->dstats) {
         (void)hipMalloc(&h->dstats, 8 * sizeof(unsigned long long));
         (void)hipMemsetAsync(h->dstats, 0, 8 * sizeof(unsigned long long), h->stream);
     }
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
     f.halve = AOS ? merge_halve() : young ? young_halve() : 1u;
+    if (persist) {
+        f.work = reinterpret_cast<unsigned long long*>(h->derr + 8);
+        (void)hipMemsetAsync(f.work, 0, sizeof(unsigned long long), h->stream);
+    }
     const bool vec = std::is_same<IdT, uint32_t>::value && !AOS &&
                      ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
     KTimer t(h, h->fold_timer);
@@ -351,7 +365,7 @@ void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, siz
         uint64_t m = n - off;
         if (h->edges_since_reset < young_limit) {
             const uint64_t left = young_limit - h->edges_since_reset;
-            uint64_t c = young_chunk();
+            uint64_t c = young_persist() ? left : young_chunk();
             if (young_head()) {          // geometric ramp: head, 2 head, 4 head, ... up to the chunk
                 uint64_t r = young_head();
                 while (r < c && 2 * r <= h->edges_since_reset + young_head()) r *= 2;
@@ -475,7 +489,10 @@ int compress_impl(gs_cc_t* h) {
             klaunch(k_pick_giant, dim3(1), dim3(1024), h->stream, t.start(), nullptr, (const uint32_t*)h->parent, h->cap,
                     in, (int)force);
         ++h->closes;
-        klaunch(k_compress, dim3(grid_for(h->cap, 1024, 16384)), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
+        // 2048 workgroups: the incremental close is a 2M-word bitmap scan; 16384 cost 140 us more
+        // per 64-window step (tools/sweep_env.sh)
+        static const unsigned cgrid = (unsigned)std::max<uint64_t>(env_u64("GSGPU_COMPRESS_GRID", 2048), 1);
+        klaunch(k_compress, dim3(grid_for(h->cap, 1024, cgrid)), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
                 h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot);
     }
     GS_HIP(hipGetLastError());

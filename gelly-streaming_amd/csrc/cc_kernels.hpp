@@ -168,6 +168,7 @@ struct FoldArgs {
     RangeCheck rc;
     unsigned long long* stats;   // STATS: [valid, filtered, early, hooks, casfail, inits]
     uint32_t halve = 1;          // path halving in root walks (find_root)
+    unsigned long long* work = nullptr;   // k_fold: dynamic chunk counter (young forest), or null
 };
 
 // ---- LDS hot set (steady state) ----
@@ -368,10 +369,61 @@ __device__ __forceinline__ void fold_group(const FoldArgs& f, bool filt, uint32_
     }
 }
 
-// UpdateCC over a batch. Each thread takes 4 consecutive edges per pass: endpoint reads are
+// One thread's EPT edges starting at edge g * EPT: load, range-check, filter, union.
+template <typename IdT, bool AOS, bool MARK, bool VEC, int EPT, bool STATS>
+__device__ __forceinline__ void fold_edges_at(const IdT* __restrict__ a, const IdT* __restrict__ b, const FoldArgs& f,
+                                              bool filt, uint64_t g, FoldStats& st) {
+    const uint64_t n = f.n;
+    const uint64_t e0 = g * EPT;
+    uint32_t u[EPT], v[EPT];
+    bool ok[EPT];
+    bool bad = false;
+    if (VEC && e0 + EPT <= n) {
+#pragma unroll
+        for (int q = 0; q < EPT / 4; ++q) {
+            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a) + g * (EPT / 4) + q);
+            const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b) + g * (EPT / 4) + q);
+            u[4 * q + 0] = x.x; u[4 * q + 1] = x.y; u[4 * q + 2] = x.z; u[4 * q + 3] = x.w;
+            v[4 * q + 0] = y.x; v[4 * q + 1] = y.y; v[4 * q + 2] = y.z; v[4 * q + 3] = y.w;
+        }
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            ok[k] = u[k] < f.rc.cap && v[k] < f.rc.cap;
+            bad |= !ok[k];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const uint64_t e = e0 + k;
+            IdT x = 0, y = 0;
+            if (e < n) {
+                if (AOS) {
+                    x = __builtin_nontemporal_load(&a[2 * e]);
+                    y = __builtin_nontemporal_load(&a[2 * e + 1]);
+                } else {
+                    x = __builtin_nontemporal_load(&a[e]);
+                    y = __builtin_nontemporal_load(&b[e]);
+                }
+            }
+            const bool in = e < n;
+            const bool good = in && id_ok<IdT>(x, f.rc.cap) && id_ok<IdT>(y, f.rc.cap);
+            bad |= in && !good;
+            ok[k] = good;
+            u[k] = static_cast<uint32_t>(x);
+            v[k] = static_cast<uint32_t>(y);
+        }
+    }
+    if (bad) atomicOr(f.rc.err, 1u);
+    fold_group<MARK, STATS, EPT>(f, filt, u, v, ok, st);
+}
+
+// UpdateCC over a batch. Each thread takes EPT consecutive edges per pass: endpoint reads are
 // coalesced and nontemporal (the edge stream is read once and must not evict parent[] / gbits
-// from L2 / Infinity Cache), 16 B per lane when VEC; the filter and parent[] gathers of the 4
+// from L2 / Infinity Cache), 16 B per lane when VEC; the filter and parent[] gathers of the
 // edges are issued back to back before any dependent step; then the unions run.
+// f.work != nullptr (young forest, one launch per batch): workgroups take the next blockDim
+// groups from the counter *f.work in stream order, so about grid x blockDim x EPT edges are in
+// flight at any time (what bounds the hub contention) without a launch boundary per chunk.
 template <typename IdT, bool AOS, bool MARK, bool VEC, int EPT = kEdgesPerThread, bool STATS = false>
 __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a, const IdT* __restrict__ b,
                                                        FoldArgs f) {
@@ -379,49 +431,21 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
     const bool filt = *f.giant != kInvalid;          // wave-uniform
     FoldStats st;
     const uint64_t groups = (n + EPT - 1) / EPT;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += stride) {
-        const uint64_t e0 = g * EPT;
-        uint32_t u[EPT], v[EPT];
-        bool ok[EPT];
-        bool bad = false;
-        if (VEC && e0 + EPT <= n) {
-#pragma unroll
-            for (int q = 0; q < EPT / 4; ++q) {
-                const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a) + g * (EPT / 4) + q);
-                const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b) + g * (EPT / 4) + q);
-                u[4 * q + 0] = x.x; u[4 * q + 1] = x.y; u[4 * q + 2] = x.z; u[4 * q + 3] = x.w;
-                v[4 * q + 0] = y.x; v[4 * q + 1] = y.y; v[4 * q + 2] = y.z; v[4 * q + 3] = y.w;
-            }
-#pragma unroll
-            for (int k = 0; k < EPT; ++k) {
-                ok[k] = u[k] < f.rc.cap && v[k] < f.rc.cap;
-                bad |= !ok[k];
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < EPT; ++k) {
-                const uint64_t e = e0 + k;
-                IdT x = 0, y = 0;
-                if (e < n) {
-                    if (AOS) {
-                        x = __builtin_nontemporal_load(&a[2 * e]);
-                        y = __builtin_nontemporal_load(&a[2 * e + 1]);
-                    } else {
-                        x = __builtin_nontemporal_load(&a[e]);
-                        y = __builtin_nontemporal_load(&b[e]);
-                    }
-                }
-                const bool in = e < n;
-                const bool good = in && id_ok<IdT>(x, f.rc.cap) && id_ok<IdT>(y, f.rc.cap);
-                bad |= in && !good;
-                ok[k] = good;
-                u[k] = static_cast<uint32_t>(x);
-                v[k] = static_cast<uint32_t>(y);
-            }
+    if (f.work) {
+        __shared__ unsigned long long s_base;
+        for (;;) {
+            if (threadIdx.x == 0) s_base = atomicAdd(f.work, (unsigned long long)blockDim.x);
+            __syncthreads();
+            const uint64_t base = s_base;
+            __syncthreads();
+            if (base >= groups) break;
+            const uint64_t g = base + threadIdx.x;
+            if (g < groups) fold_edges_at<IdT, AOS, MARK, VEC, EPT, STATS>(a, b, f, filt, g, st);
         }
-        if (bad) atomicOr(f.rc.err, 1u);
-        fold_group<MARK, STATS, EPT>(f, filt, u, v, ok, st);
+    } else {
+        const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+        for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += stride)
+            fold_edges_at<IdT, AOS, MARK, VEC, EPT, STATS>(a, b, f, filt, g, st);
     }
     if (STATS) {
         atomicAdd(&f.stats[2], (unsigned long long)st.early);
