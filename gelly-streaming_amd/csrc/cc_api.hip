@@ -89,6 +89,7 @@ struct gs_cc {
     bool minkey_valid = false;
     // instrumentation
     bool timing = false;
+    uint32_t timing_mask = ~0u;          // kernels timed while timing (bit GS_K_*)
     int fold_timer = GS_K_FOLD;          // GS_K_MERGE while folding an exported partial summary
     struct Pend { int k; hipEvent_t a, b; };
     std::vector<Pend> pending;
@@ -137,7 +138,7 @@ inline uint32_t* giant_state(gs_cc_t* h) { return h->derr + 1 + 2 * (h->closes &
 struct KTimer {
     gs_cc_t* h; int k; hipEvent_t a = nullptr, b = nullptr; bool markers = false;
     KTimer(gs_cc_t* h_, int k_) : h(h_), k(k_) {
-        if (!h->timing) return;
+        if (!h->timing || !(h->timing_mask & (1u << k))) return;
         a = get_event(h);
         b = get_event(h);
         markers = timing_markers();
@@ -1051,6 +1052,7 @@ int gs_cc_timing(gs_cc_t* h, int enable) {
     DeviceGuard g(h->device);
     GS_TRY(resolve_timing(h));
     h->timing = enable != 0;
+    h->timing_mask = (enable & GS_TIMING_MASK) ? ((uint32_t)enable & 0xFFu) : ~0u;
     for (int k = 0; k < GS_K_COUNT; ++k) { h->total_ms[k] = 0; h->launches[k] = 0; }
     return GS_OK;
 }

@@ -26,6 +26,7 @@ GS_CC_TRACK_MARKS = 1
 GS_CC_SPARSE_IDS = 2
 
 GS_K_FOLD, GS_K_COMPRESS, GS_K_MERGE, GS_K_EXPORT = 0, 1, 2, 3
+GS_TIMING_MASK = 0x100
 
 _ERRNAMES = {GS_ERR_INVALID: "INVALID", GS_ERR_HIP: "HIP", GS_ERR_RANGE: "RANGE",
              GS_ERR_NOMEM: "NOMEM", GS_ERR_STATE: "STATE", GS_ERR_UNSUPPORTED: "UNSUPPORTED",

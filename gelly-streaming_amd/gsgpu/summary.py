@@ -271,8 +271,9 @@ class DisjointSet:
         call("gs_cc_set_marking", self.handle, 1 if on else 0)
 
     # ---- instrumentation ----
-    def timing(self, enable: bool) -> None:
-        call("gs_cc_timing", self.handle, 1 if enable else 0)
+    def timing(self, enable) -> None:
+        """True / False, or GS_TIMING_MASK | (1 << GS_K_*) ...: time only those kernels."""
+        call("gs_cc_timing", self.handle, int(enable) if not isinstance(enable, bool) else (1 if enable else 0))
 
     def kernel_time(self, kernel: int) -> Tuple[float, int]:
         ms, n = ctypes.c_double(), U64()

@@ -144,6 +144,9 @@ int gs_cc_set_marking(gs_cc_t* h, int on);
 /* ---- instrumentation ----
  * kernel ids: 0 fold, 1 compress (close_window), 2 merge, 3 export. */
 enum { GS_K_FOLD = 0, GS_K_COMPRESS = 1, GS_K_MERGE = 2, GS_K_EXPORT = 3, GS_K_COUNT = 4 };
+/* enable = 0: off; 1: every kernel; GS_TIMING_MASK | (1 << GS_K_x) | ...: only those kernels
+ * carry timing events (a timed launch costs ~3 us more dispatch time). Totals reset. */
+enum { GS_TIMING_MASK = 0x100 };
 int gs_cc_timing(gs_cc_t* h, int enable);
 int gs_cc_kernel_time(gs_cc_t* h, int kernel, double* total_ms, uint64_t* launches);
 
