@@ -79,6 +79,9 @@ struct gs_cc {
     uint2* hot = nullptr;                // LDS hot set master copy (kHotBuckets uint2), steady folds
     uint32_t hot_bits = 0;               // ids < 2^hot_bits
     uint32_t* hot_cand = nullptr;        // hot-set admission candidates (2^kHotCandBits ids)
+    uint32_t* warm = nullptr;            // warm set (2^warm_bits words, L2-resident), steady folds
+    uint32_t warm_bits = 0;
+    uint32_t* wcnt = nullptr;            // warm build counters (16-bit, 2^(hot_bits-1) words)
     int cus = 0;                         // compute units: k_fold_ring grid
     // GS_CC_SPARSE_IDS: id -> slot table; cap (above) = slots = 2^hbits + 1
     bool sparse = false;
@@ -132,7 +135,7 @@ static bool timing_markers() {
 // span's first kernel with start() and its last with stop() through klaunch().
 // the current giant-state slot (cc_kernels.hpp): derr[1 + 2 * (closes & 1)] = giant, [+1] = built;
 // close c reads slot c & 1 and writes slot (c + 1) & 1; derr[5] = hot set owner, derr[6] = hot
-// set admission budget
+// set admission budget, derr[7] = warm set valid
 inline uint32_t* giant_state(gs_cc_t* h) { return h->derr + 1 + 2 * (h->closes & 1); }
 
 struct KTimer {
@@ -294,16 +297,45 @@ void launch_fold_ring(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t
     hot.five = (five_ok && h->hot_bits <= kHotBucketBits + 12) ? 1u : 0u;
     static const uint32_t thresh = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(env_u64("GSGPU_HOT_THRESH", 3), 2), 63);
     hot.thresh = thresh;
+    // warm set: built (counted in this launch, then k_warm_build) at ring launch GSGPU_WARM_AT
+    // after reset and every GSGPU_WARM_EVERY-th after it, each time only if the set is not valid
+    // for the current giant (device-gated); GSGPU_WARM=0 turns it off, GSGPU_WARM_SAMPLE = edges
+    // counted
+    static const uint64_t warm_at = env_u64("GSGPU_WARM_AT", 3);
+    static const uint64_t warm_every = std::max<uint64_t>(env_u64("GSGPU_WARM_EVERY", 16), 1);
+    static const uint64_t warm_sample = std::min<uint64_t>(env_u64("GSGPU_WARM_SAMPLE", 1ull << 23), 1ull << 24);
+    const uint64_t launch_no = h->ring_launches - 1;
+    const bool build = h->warm && launch_no >= warm_at && (launch_no - warm_at) % warm_every == 0;
+    hot.warm = h->warm;
+    hot.warm_bits = h->warm_bits;
+    hot.warm_valid = h->derr + 7;
+    hot.wcnt = build ? h->wcnt : nullptr;
+    hot.count_edges = build ? warm_sample : 0;
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
     KTimer t(h, h->fold_timer);
     const bool st = h->dstats != nullptr;
     const dim3 grid(grid_for(n / 4, kHotThreads, (unsigned)std::max(h->cus, 1)));
+    hipEvent_t stop = build ? nullptr : t.stop();
     if (h->mark) {
-        if (st) klaunch(k_fold_ring<true, true>, grid, dim3(kHotThreads), h->stream, t.start(), t.stop(), a, b, f, hot);
-        else klaunch(k_fold_ring<true, false>, grid, dim3(kHotThreads), h->stream, t.start(), t.stop(), a, b, f, hot);
+        if (st) klaunch(k_fold_ring<true, true>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
+        else klaunch(k_fold_ring<true, false>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
     } else {
-        if (st) klaunch(k_fold_ring<false, true>, grid, dim3(kHotThreads), h->stream, t.start(), t.stop(), a, b, f, hot);
-        else klaunch(k_fold_ring<false, false>, grid, dim3(kHotThreads), h->stream, t.start(), t.stop(), a, b, f, hot);
+        if (st) klaunch(k_fold_ring<false, true>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
+        else klaunch(k_fold_ring<false, false>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
+    }
+    if (build) {
+        // hottest band first: a full bucket then drops the colder ids (counts from 2^23 sampled edges)
+        static const uint32_t bands[] = {0xFFFFFFFFu, 32u, 8u, 3u, 2u};
+        const uint32_t B = h->hot_bits;
+        const uint32_t wwords = 1u << h->warm_bits;
+        const uint32_t cwords = (uint32_t)((((uint64_t)1 << B) + 1) / 2);
+        klaunch(k_warm_clear, dim3(grid_for(wwords, 256, 2048)), dim3(256), h->stream, nullptr, nullptr, h->warm, wwords,
+                (const uint32_t*)(h->derr + 7));
+        const int nb = (int)(sizeof(bands) / sizeof(bands[0])) - 1;
+        for (int i = 0; i < nb; ++i)
+            klaunch(k_warm_build, dim3(grid_for(cwords, 256, 8192)), dim3(256), h->stream, nullptr, nullptr, h->wcnt, cwords,
+                    h->warm, B, h->warm_bits, bands[i + 1], bands[i], (const uint2*)h->hot, hot.five, (const uint32_t*)h->gbits, h->derr + 7, (int)(i == nb - 1));
+        klaunch(k_warm_done, dim3(1), dim3(1), h->stream, nullptr, t.stop(), h->derr + 7);
     }
 }
 
@@ -471,8 +503,8 @@ void report_fold_stats(gs_cc_t* h) {
     unsigned long long c[8];
     if (hipMemcpyAsync(c, h->dstats, sizeof(c), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
         hipStreamSynchronize(h->stream) != hipSuccess) return;
-    fprintf(stderr, "[gsgpu fold-stats] valid=%llu filtered=%llu early=%llu hooks=%llu casfail=%llu inits=%llu hot_hits=%llu\n",
-            c[0], c[1], c[2], c[3], c[4], c[5], c[6]);
+    fprintf(stderr, "[gsgpu fold-stats] valid=%llu filtered=%llu early=%llu hooks=%llu casfail=%llu inits=%llu hot_hits=%llu warm_hits=%llu\n",
+            c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]);
     (void)hipMemsetAsync(h->dstats, 0, sizeof(c), h->stream);
 }
 
@@ -681,6 +713,24 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
                 h->hot_cand = nullptr;
             }
             h->hot_bits = bits;
+            // warm set: only where gbits outgrows an XCD's 4 MiB L2 (ids >= 2^25; GSGPU_WARM_MIN_BITS
+            // for tests), its table L2-resident and at most 1/8 of gbits (GSGPU_WARM_BUCKETS = log2
+            // buckets of 4 B, at most 2^19 = 2 MiB; 8-bit slots need at least 2^(B-8))
+            static const bool warm_on = env_u64("GSGPU_WARM", 1) != 0;
+            static const uint32_t wmin = (uint32_t)env_u64("GSGPU_WARM_MIN_BITS", 25);
+            static const uint32_t wmax = (uint32_t)std::min<uint64_t>(env_u64("GSGPU_WARM_BUCKETS", 18), 19);
+            h->warm_bits = std::min<uint32_t>(wmax, bits - 6);
+            if (h->hot && warm_on && bits >= wmin && bits <= h->warm_bits + 8) {
+                const size_t cbytes = (size_t)((((uint64_t)1 << bits) + 1) / 2) * 4;
+                if (hipMalloc(&h->warm, (size_t)4 << h->warm_bits) != hipSuccess ||
+                    hipMalloc(&h->wcnt, cbytes) != hipSuccess || hipMemsetAsync(h->wcnt, 0, cbytes, h->stream) != hipSuccess) {
+                    (void)hipGetLastError();
+                    if (h->warm) (void)hipFree(h->warm);
+                    if (h->wcnt) (void)hipFree(h->wcnt);
+                    h->warm = nullptr;
+                    h->wcnt = nullptr;
+                }
+            }
         }
     }
     if (hipMemsetAsync(h->derr, 0, 4, h->stream) != hipSuccess) return bail(fail(GS_ERR_HIP, "memset failed"));
@@ -706,6 +756,8 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->dstats) (void)hipFree(h->dstats);
     if (h->hot) (void)hipFree(h->hot);
     if (h->hot_cand) (void)hipFree(h->hot_cand);
+    if (h->warm) (void)hipFree(h->warm);
+    if (h->wcnt) (void)hipFree(h->wcnt);
     if (h->keys) (void)hipFree(h->keys);
     if (h->minkey) (void)hipFree(h->minkey);
     if (h->nkeys) (void)hipFree(h->nkeys);
@@ -732,6 +784,7 @@ int gs_cc_reset(gs_cc_t* h) {
         static const uint32_t budget = (uint32_t)env_u64("GSGPU_HOT_BUDGET", kHotAdmitLaunches);   // derr[6]
         GS_HIP(hipMemcpyAsync(h->derr + 6, &budget, sizeof(uint32_t), hipMemcpyHostToDevice, h->stream));
     }
+    GS_HIP(hipMemsetAsync(h->derr + 7, 0, sizeof(uint32_t), h->stream));      // warm set: not built
     if (h->hot) GS_HIP(hipMemsetAsync(h->hot, 0, kHotBuckets * sizeof(uint2), h->stream));
     if (h->hot_cand) GS_HIP(hipMemsetAsync(h->hot_cand, 0xFF, sizeof(uint32_t) << kHotCandBits, h->stream));
     if (h->sparse) {

@@ -271,7 +271,58 @@ struct HotArgs {
     uint32_t five = 0;                         // slot format: 5 x 12 bits (B <= 26) instead of 4 x 16
     uint32_t thresh = 2;                       // sightings before admission (> 2 needs B <= 26;
                                                // the host passes 3: steady window 233 -> 229 us)
+    uint32_t* warm = nullptr;                  // warm set (2^warm_bits words), nullptr = none
+    uint32_t warm_bits = 0;                    // log2(warm buckets), B - 8 <= warm_bits <= B
+    const uint32_t* warm_valid = nullptr;      // device word: warm set built for the current giant
+    uint32_t* wcnt = nullptr;                  // endpoint counters for the next warm build
+    uint64_t count_edges = 0;                  // count this launch's first edges (if !*warm_valid)
 };
+
+// ---- warm set (L2-resident second tier) ----
+// Ids ranked ~80K..2M by frequency answer ~45 % of an RMAT-26 window's lookups (top 80K: 38 %,
+// top 2M: 82 %), but do not fit LDS. The warm set holds them in a global table small enough to
+// stay in every XCD's 4 MiB L2 next to the bitmap lines (2 MiB at 2^26 ids), one 4-B word per
+// probe: 2^wb buckets x 4 slots of 8 bits, h = v * kWarmMul mod 2^B (odd multiplier: a
+// bijection), bucket = h >> (B - wb), slot value = (h mod 2^(B - wb)) + 1; exact like the hot set. An LDS miss
+// probes it before gbits, so a warm hit costs an L2 hit instead of (half the time) an
+// Infinity-Cache line fill. Built from endpoint counts (16-bit, two per word) of one ring launch's
+// first count_edges edges (LDS misses confirmed in the giant), hottest first (k_warm_build);
+// valid (hot.warm_valid) while the giant is the same component, like the hot set.
+constexpr uint32_t kWarmMul = 0x85EBCA6Bu;
+// wb = log2(buckets); remainders of B - wb <= 8 bits, slot value r = rem + 1 in [1, 256]: the one
+// value that does not fit a byte (256: 1 id in 256 when B - wb = 8) never enters nor matches.
+__device__ __forceinline__ uint32_t warm_hash(uint32_t v, uint32_t B) { return (v * kWarmMul) & ((1u << B) - 1); }
+__device__ __forceinline__ bool warm_probe(const uint32_t* __restrict__ warm, uint32_t v, uint32_t B, uint32_t wb) {
+    const uint32_t h = warm_hash(v, B);
+    const uint32_t rb = B - wb;
+    const uint32_t r = (h & ((1u << rb) - 1)) + 1;
+    const uint32_t x = warm[h >> rb] ^ (r * 0x01010101u);
+    return r <= 0xFFu && ((x - 0x01010101u) & ~x & 0x80808080u) != 0;    // a byte equal to r
+}
+__device__ inline void warm_insert(uint32_t* __restrict__ warm, uint32_t v, uint32_t B, uint32_t wb) {
+    const uint32_t h = warm_hash(v, B);
+    const uint32_t rb = B - wb;
+    const uint32_t r = (h & ((1u << rb) - 1)) + 1;
+    if (r > 0xFFu) return;
+    uint32_t* p = warm + (h >> rb);
+    uint32_t x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int attempt = 0; attempt < 8; ++attempt) {
+        int empty = -1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t fk = (x >> (8 * k)) & 0xFFu;
+            if (fk == r) return;
+            if (fk == 0 && empty < 0) empty = k;
+        }
+        if (empty < 0) return;                               // bucket full
+        const uint32_t old = atomicCAS(p, x, x | (r << (8 * empty)));
+        if (old == x) return;
+        x = old;
+    }
+}
+__device__ __forceinline__ void warm_count(uint32_t* __restrict__ wcnt, uint32_t v) {
+    atomicAdd(&wcnt[v >> 1], 1u << ((v & 1u) << 4));
+}
 
 // Admission cadence. Offering a launch's first 2^18 edges costs ~28 us per RMAT-26 window (the
 // candidate table's atomics); the hubs are stable, so a launch admits only while *budget > 0
@@ -300,33 +351,57 @@ __device__ __forceinline__ void hot_admit(const HotArgs& hot, uint32_t v) {
 // Filter of one thread's EPT edges (ids already range-checked and zeroed where !ok): ok[k]
 // becomes false for an edge whose endpoints are both in the giant component. HOT: probe the LDS
 // hot set `tab` before gbits, and (insert) offer the gbits-confirmed endpoints for admission.
+// warm: probe the warm set for LDS misses first; count: add the LDS misses found in the giant to
+// the warm build's counters.
 template <bool STATS, int EPT, bool HOT>
 __device__ __forceinline__ void filter_group(const FoldArgs& f, const uint32_t (&u)[EPT], const uint32_t (&v)[EPT],
-                                             bool (&ok)[EPT], const uint2* tab, const HotArgs& hot, bool insert) {
-    bool hu[EPT], hv[EPT];
+                                             bool (&ok)[EPT], const uint2* tab, const HotArgs& hot, bool insert,
+                                             bool warm = false, bool count = false) {
+    bool hu[EPT], hv[EPT];       // LDS hot-set hits
+    bool mu[EPT], mv[EPT];       // known giant members without a gbits load (LDS or warm hits)
     uint32_t wu[EPT], wv[EPT];
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
         hu[k] = HOT && hot.probe && hot_probe(tab, u[k], hot.bits, hot.five != 0);
         hv[k] = HOT && hot.probe && hot_probe(tab, v[k], hot.bits, hot.five != 0);
+        mu[k] = hu[k];
+        mv[k] = hv[k];
+    }
+    if (HOT && warm) {
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            mu[k] = hu[k] || warm_probe(hot.warm, u[k], hot.bits, hot.warm_bits);
+            mv[k] = hv[k] || warm_probe(hot.warm, v[k], hot.bits, hot.warm_bits);
+        }
     }
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
-        wu[k] = hu[k] ? ~0u : f.gbits[u[k] >> 5];
-        wv[k] = hv[k] ? ~0u : f.gbits[v[k] >> 5];
+        wu[k] = mu[k] ? ~0u : f.gbits[u[k] >> 5];
+        wv[k] = mv[k] ? ~0u : f.gbits[v[k] >> 5];
     }
 
     if (HOT && STATS) {
-        uint32_t nh = 0;
+        uint32_t nh = 0, nw = 0;
 #pragma unroll
-        for (int k = 0; k < EPT; ++k) nh += (ok[k] && hu[k]) + (ok[k] && hv[k]);
+        for (int k = 0; k < EPT; ++k) {
+            nh += (ok[k] && hu[k]) + (ok[k] && hv[k]);
+            nw += (ok[k] && mu[k] && !hu[k]) + (ok[k] && mv[k] && !hv[k]);
+        }
         if (nh) atomicAdd(&f.stats[6], (unsigned long long)nh);
+        if (nw) atomicAdd(&f.stats[7], (unsigned long long)nw);
     }
     if (HOT && insert) {
 #pragma unroll
         for (int k = 0; k < EPT; ++k) {
             if (ok[k] && !hu[k] && ((wu[k] >> (u[k] & 31)) & 1u)) hot_admit(hot, u[k]);
             if (ok[k] && !hv[k] && ((wv[k] >> (v[k] & 31)) & 1u)) hot_admit(hot, v[k]);
+        }
+    }
+    if (HOT && count) {
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            if (ok[k] && !hu[k] && ((wu[k] >> (u[k] & 31)) & 1u)) warm_count(hot.wcnt, u[k]);
+            if (ok[k] && !hv[k] && ((wv[k] >> (v[k] & 31)) & 1u)) warm_count(hot.wcnt, v[k]);
         }
     }
 #pragma unroll
@@ -498,6 +573,8 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const uint32_t* __res
     // decremented budget only skips this launch's admission, which is a heuristic anyway)
     const uint32_t budget = hot.budget ? *hot.budget : 1u;
     const uint64_t sample_edges = (hot.periodic || budget) ? hot.sample_edges : 0;
+    const bool warm_ok = filt && hot.warm && *hot.warm_valid != 0;                        // uniform
+    const uint64_t count_edges = (filt && hot.wcnt && hot.warm_valid && *hot.warm_valid == 0) ? hot.count_edges : 0;
     __syncthreads();
     if (blockIdx.x == 0 && threadIdx.x == 0 && hot.budget && budget) *hot.budget = budget - 1;
     const int lane = threadIdx.x & 63;
@@ -526,7 +603,7 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const uint32_t* __res
             if (bad) atomicOr(f.rc.err, 1u);
         }
         if (STATS) for (int k = 0; k < 4; ++k) nvalid += ok[k];
-        if (filt) filter_group<STATS, 4, true>(f, u, v, ok, tab, hot, g * 4 < sample_edges);
+        if (filt) filter_group<STATS, 4, true>(f, u, v, ok, tab, hot, g * 4 < sample_edges, warm_ok, g * 4 < count_edges);
         const uint32_t c = (uint32_t)ok[0] + ok[1] + ok[2] + ok[3];
         if (STATS) nkept += c;
         uint32_t incl = c;
@@ -562,6 +639,36 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const uint32_t* __res
         atomicAdd(&f.stats[5], (unsigned long long)st.inits);
     }
 }
+
+// Warm build pass: every id whose count c (16-bit counters, two per word) lies in [lo, hi), that
+// gbits holds and that is not already in the hot set enters the warm set; passes run hottest band first so that full
+// buckets keep the hotter ids. The first pass (clear) zeroes the table first; the last (done)
+// zeroes the counters for the next build and marks the set valid. No-op while the set is valid.
+__global__ __launch_bounds__(256) void k_warm_clear(uint32_t* __restrict__ warm, uint32_t words, const uint32_t* __restrict__ valid) {
+    if (*valid) return;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < words; i += gridDim.x * blockDim.x) warm[i] = 0u;
+}
+__global__ __launch_bounds__(256) void k_warm_build(uint32_t* __restrict__ wcnt, uint32_t nwords, uint32_t* __restrict__ warm,
+                                                    uint32_t B, uint32_t wb, uint32_t lo, uint32_t hi, const uint2* __restrict__ hot,
+                                                    uint32_t five, const uint32_t* __restrict__ gbits,
+                                                    uint32_t* __restrict__ valid, int done) {
+    if (*valid) return;                              // uniform (set by the last pass, after every read)
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += gridDim.x * blockDim.x) {
+        const uint32_t c = wcnt[i];
+        if (!c) continue;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t ck = (c >> (16 * k)) & 0xFFFFu;
+            const uint32_t v = 2 * i + k;
+            // gbits (the last close's giant, a subset of the current one): whatever the counts
+            // say, only a giant member can enter
+            if (ck >= lo && ck < hi && ((gbits[v >> 5] >> (v & 31)) & 1u) && !(hot && hot_probe(hot, v, B, five != 0)))
+                warm_insert(warm, v, B, wb);
+        }
+        if (done) wcnt[i] = 0u;
+    }
+}
+__global__ void k_warm_done(uint32_t* __restrict__ valid) { *valid = 1u; }
 
 // DisjointSet.merge(other) with other given as a dense parent array: union(v, other[v]) for
 // every v in other (DisjointSet.java:127-131 iterates other.getMatches()).
@@ -697,7 +804,10 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
     const uint32_t g = s_g;
     if (s_clear && hot) {                            // workgroup 0 only: the hot set belonged to another component
         for (uint32_t i = threadIdx.x; i < kHotBuckets; i += blockDim.x) hot[i] = make_uint2(0u, 0u);
-        if (threadIdx.x == 0) owner[1] = kHotAdmitLaunches;    // refill: the admission budget
+        if (threadIdx.x == 0) {
+            owner[1] = kHotAdmitLaunches;            // refill: the admission budget
+            owner[2] = 0;                            // the warm set belonged to it too (rebuilt later)
+        }
     }
     const int lane = threadIdx.x & 63;
     if (s_inc) {                                     // one bitmap word (32 vertices) per thread
@@ -912,18 +1022,35 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_scatter(const uint32_t* _
 // per RMAT-26 window, tools/sim_ranks.py), then scatters tile by tile (block-wide scan). Pairs
 // past `cap` are not written and keep their marks for the next export. Each mark word is one
 // thread's, so its plain clear cannot race with another workgroup's store.
+// Each lane reads 4 mark words at once (16 B): a workgroup's range is 2 passes of 256 quads at
+// RMAT-26 instead of 8 dependent passes of 256 words (the scan and the root walks of one pass
+// wait on its loads).
 constexpr int kExportBlocks = 1024;
+__device__ __forceinline__ uint4 load_mark_quad(const uint32_t* mark, uint32_t q, uint32_t nwords) {
+    const uint32_t w = q << 2;
+    if (w + 3 < nwords) return reinterpret_cast<const uint4*>(mark)[q];
+    uint4 r;
+    r.x = w < nwords ? mark[w] : 0u;
+    r.y = w + 1 < nwords ? mark[w + 1] : 0u;
+    r.z = w + 2 < nwords ? mark[w + 2] : 0u;
+    r.w = 0u;
+    return r;
+}
 __global__ __launch_bounds__(256) void k_export_marks(uint32_t* __restrict__ mark, const uint32_t* __restrict__ parent,
                                                       uint32_t n, uint32_t* __restrict__ pairs, uint64_t cap,
                                                       unsigned long long* __restrict__ counter) {
     __shared__ unsigned long long s_base;
     __shared__ uint32_t s_wave[4];
     const uint32_t nwords = (n + 31) >> 5;
-    const uint32_t per = (nwords + gridDim.x - 1) / gridDim.x;
-    const uint32_t lo = min(blockIdx.x * per, nwords), hi = min(lo + per, nwords);
+    const uint32_t nquads = (nwords + 3) >> 2;
+    const uint32_t per = (nquads + gridDim.x - 1) / gridDim.x;
+    const uint32_t lo = min(blockIdx.x * per, nquads), hi = min(lo + per, nquads);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t c = 0;
-    for (uint32_t w = lo + threadIdx.x; w < hi; w += blockDim.x) c += __popc(mark[w]);
+    for (uint32_t q = lo + threadIdx.x; q < hi; q += blockDim.x) {
+        const uint4 m = load_mark_quad(mark, q, nwords);
+        c += __popc(m.x) + __popc(m.y) + __popc(m.z) + __popc(m.w);
+    }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
     if (lane == 0) s_wave[wave] = c;
@@ -934,10 +1061,11 @@ __global__ __launch_bounds__(256) void k_export_marks(uint32_t* __restrict__ mar
     }
     __syncthreads();
     unsigned long long base = s_base;
-    for (uint32_t w0 = lo; w0 < hi; w0 += blockDim.x) {          // uniform over the block
-        const uint32_t w = w0 + threadIdx.x;
-        uint32_t m = (w < hi) ? mark[w] : 0u;
-        const uint32_t cnt = __popc(m);
+    if (s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3] == 0) return;   // nothing marked here (uniform)
+    for (uint32_t q0 = lo; q0 < hi; q0 += blockDim.x) {          // uniform over the block
+        const uint32_t q = q0 + threadIdx.x;
+        const uint4 m4 = (q < hi) ? load_mark_quad(mark, q, nwords) : make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t cnt = __popc(m4.x) + __popc(m4.y) + __popc(m4.z) + __popc(m4.w);
         uint32_t incl = cnt;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
@@ -956,20 +1084,27 @@ __global__ __launch_bounds__(256) void k_export_marks(uint32_t* __restrict__ mar
         unsigned long long pos = base + woff + incl - cnt;
         base += tile;
         if (cnt == 0) continue;
-        uint32_t keep = 0;
-        while (m) {
-            const int b = __ffs(m) - 1;
-            m &= m - 1;
-            const uint32_t v = (w << 5) + b;
-            if (pos < cap) {
-                pairs[2 * pos] = v;
-                pairs[2 * pos + 1] = find_root_ro(parent, v);
-            } else {
-                keep |= 1u << b;                // overflowing marks stay for the next export
+        const uint32_t mw[4] = {m4.x, m4.y, m4.z, m4.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t m = mw[k];
+            if (!m) continue;
+            const uint32_t w = (q << 2) + k;
+            uint32_t keep = 0;
+            while (m) {
+                const int b = __ffs(m) - 1;
+                m &= m - 1;
+                const uint32_t v = (w << 5) + b;
+                if (pos < cap) {
+                    pairs[2 * pos] = v;
+                    pairs[2 * pos + 1] = find_root_ro(parent, v);
+                } else {
+                    keep |= 1u << b;                // overflowing marks stay for the next export
+                }
+                ++pos;
             }
-            ++pos;
+            mark[w] = keep;
         }
-        mark[w] = keep;
     }
 }
 

@@ -4,9 +4,9 @@ Three exchanges behind one contract (``merge_window()`` after each window's fold
 rank that emitted):
 
 ``AllgatherMerge`` (bench default): replicated summaries. Every rank keeps the GLOBAL summary: per
-window each rank exports its delta (the connectivity its own slice added), sends it to every
-other rank over that pair's own xGMI link (one batch of RCCL send/recv), and folds the others'
-deltas with marking paused. Every rank's filter is then the global giant component, so the
+window each rank exports its delta (the connectivity its own slice added), the deltas are
+all-gathered (one RCCL all-gather of slots padded to the largest delta; on xGMI every pair of
+GPUs has its own link), and each rank folds the others' deltas with marking paused. Every rank's filter is then the global giant component, so the
 deltas shrink to the genuinely new connectivity (RMAT-26, 8 ranks, window 64: 14K pairs per rank
 instead of 132K) and every rank's fold is as fast as a single GPU's (tools/sim_ranks.py).
 ``GatherMerge``: the reference's windowAll reduce (SummaryBulkAggregation.java:81: every
@@ -278,18 +278,22 @@ def fold_deltas(summary, buf, counts) -> None:
 
 
 class AllgatherMerge:
-    """Replicated global summary on every rank; per window an all-pairs exchange of deltas.
+    """Replicated global summary on every rank; per window an all-gather of deltas.
 
     Per window, every rank: export its marks (its slice's new connectivity relative to the global
     summary it held) into ``sendbuf``; all-gather the counts (one small collective, one host
-    sync); one batch of send/recv: its delta to every peer, every peer's delta into one
-    contiguous buffer (on xGMI each pair of GPUs has its own link, so all P(P-1) transfers run at
-    once); fold the received deltas with marking paused (they are the others' to export, not
-    this rank's); close the window. All ranks then hold the same partition (the union of all
-    ranks' edges); rank 0 reports the emission. Correctness argument: a delta holds (v, root(v))
-    for every root the exporting rank hooked and every self-loop first touch, so it carries
-    every component join of that rank's window; joins are idempotent, so it applies to any
-    summary of the same prior partition (tests/test_tree_gloo.py).
+    sync); pad its delta to the largest count m with copies of its first pair (a repeated union
+    is a no-op) and all-gather the padded deltas (one collective: P slots of m pairs each, over
+    every pair of GPUs' own xGMI link at once); fold the other ranks' slots with marking paused
+    (they are the others' to export, not this rank's); close the window. All ranks then hold the
+    same partition (the union of all ranks' edges); rank 0 reports the emission.
+    One collective call instead of a batch of 2(P-1) send/recv ops keeps the host's share of the
+    per-window critical path (the GPU idles from the count sync until the payload is enqueued)
+    to one launch.
+    Correctness argument: a delta holds (v, root(v)) for every root the exporting rank hooked and
+    every self-loop first touch, so it carries every component join of that rank's window; joins
+    are idempotent, so it applies to any summary of the same prior partition
+    (tests/test_tree_gloo.py).
     The summary needs ``export_marks``, ``fold_pairs``, ``set_marking``, ``close_window`` and
     must have been created with marks tracked (GS_CC_TRACK_MARKS) on EVERY rank.
     """
@@ -311,16 +315,13 @@ class AllgatherMerge:
         if self.device.type == "cuda" and hasattr(summary, "export_marks_async"):
             self.dcnt = self.cnt if self.cnt.is_cuda else torch.zeros(1, dtype=torch.int64, device=self.device)
         self.sendbuf = torch.empty(2 * self.cap, dtype=torch.int32, device=self.device)
-        self.recvbuf = torch.empty(2 * max(self.cap, 1), dtype=torch.int32, device=self.device)
+        self.recvbuf = torch.empty(2 * self.world, dtype=torch.int32, device=self.device)   # grows
         self.hsend = torch.empty(0, dtype=torch.int32)
         self.hrecv = torch.empty(0, dtype=torch.int32)
         self.bytes_sent = 0
         self.bytes_recv = 0
-        # communicators up (all ranks take part) before the first partial point-to-point batch
+        # communicator up (all ranks take part) before the first window
         dist.all_gather_into_tensor(self.cnts, self.cnt, group=self.group)
-
-    def _grank(self, r: int) -> int:
-        return r if self.group is None else dist.get_global_rank(self.group, r)
 
     def _host(self, attr: str, n: int) -> torch.Tensor:
         t = getattr(self, attr)
@@ -331,50 +332,65 @@ class AllgatherMerge:
             setattr(self, attr, t)
         return t
 
-    def merge_window(self) -> bool:
-        if self.world == 1:
-            self.summary.close_window()
-            return True
+    def _counts(self) -> List[int]:
         if self.dcnt is not None:
             # count straight from the device into the collective: one host sync per window
             self.summary.export_marks_async(self.sendbuf, self.dcnt)
             if self.stage:
                 self.cnt.copy_(self.dcnt)
-            dist.all_gather_into_tensor(self.cnts, self.cnt, group=self.group)
-            counts = [int(x) for x in self.cnts.tolist()]
-            n = counts[self.rank]
         else:
-            n = self.summary.export_marks(self.sendbuf, self.cap)
-            self.cnt.fill_(n)
-            dist.all_gather_into_tensor(self.cnts, self.cnt, group=self.group)
-            counts = [int(x) for x in self.cnts.tolist()]
-        others = [(q, counts[q]) for q in range(self.world) if q != self.rank]
-        total = sum(c for _, c in others)
-        if total > self.recvbuf.numel() // 2:
-            self.recvbuf = torch.empty(2 * total, dtype=torch.int32, device=self.device)
-        send, recv = self.sendbuf, self.recvbuf
-        if self.stage:                                   # gloo moves host tensors only
-            send = self._host("hsend", 2 * n)
-            if n:
-                send[: 2 * n].copy_(self.sendbuf[: 2 * n])
-            recv = self._host("hrecv", 2 * total)
-        ops, off = [], 0
-        for q, c in others:
-            if n:
-                ops.append(dist.P2POp(dist.isend, send[: 2 * n], self._grank(q), group=self.group))
-            if c:
-                ops.append(dist.P2POp(dist.irecv, recv[2 * off: 2 * (off + c)], self._grank(q), group=self.group))
-                off += c
-        if ops:
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
-        if self.stage and total:
-            self.recvbuf[: 2 * total].copy_(recv[: 2 * total])
-        self.bytes_sent += 8 * n * (self.world - 1)
-        self.bytes_recv += 8 * total
-        if total:
+            self.cnt.fill_(self.summary.export_marks(self.sendbuf, self.cap))
+        dist.all_gather_into_tensor(self.cnts, self.cnt, group=self.group)
+        return [int(x) for x in self.cnts.tolist()]
+
+    def merge_window(self) -> bool:
+        if self.world == 1:
+            self.summary.close_window()
+            return True
+        counts = self._counts()
+        n, m, P = counts[self.rank], max(counts), self.world
+        if m:
+            if 0 < n < m:                                  # pad with copies of the first pair
+                self.sendbuf[2 * n: 2 * m].view(-1, 2).copy_(self.sendbuf[0:2].view(1, 2).expand(m - n, 2))
+            if self.recvbuf.numel() < 2 * P * m:
+                self.recvbuf = torch.empty(2 * P * m, dtype=torch.int32, device=self.device)
+            send, recv = self.sendbuf[: 2 * m], self.recvbuf[: 2 * P * m]
+            if self.stage:                                 # gloo moves host tensors only
+                hs = self._host("hsend", 2 * m)[: 2 * m]
+                hs.copy_(send)
+                hr = self._host("hrecv", 2 * P * m)[: 2 * P * m]
+                dist.all_gather_into_tensor(hr, hs, group=self.group)
+                recv.copy_(hr)
+            else:
+                dist.all_gather_into_tensor(recv, send, group=self.group)
+            self.bytes_sent += 8 * m * (P - 1)
+            self.bytes_recv += 8 * m * (P - 1)
             self.summary.set_marking(False)
-            fold_deltas(self.summary, self.recvbuf, [c for _, c in others])
+            fold_slots(self.summary, recv, m, [0 if q == self.rank else c for q, c in enumerate(counts)])
             self.summary.set_marking(True)
         self.summary.close_window()
         return self.rank == 0
+
+
+def fold_slots(summary, buf, m: int, counts) -> None:
+    """Fold deltas laid out in slots of m pairs (slot q: counts[q] real pairs, then copies of its
+    first pair). Runs of non-empty slots go in one call; while the deltas are big (young windows,
+    components not yet joined) each slot goes in its own call with its exact count, so that
+    call's short head launch joins its components before the bulk (see fold_deltas)."""
+    if max(counts) > BULK_DELTA_PAIRS:
+        for q, c in enumerate(counts):
+            if c:
+                summary.fold_pairs(buf[2 * q * m: 2 * (q * m + c)], c, id_bits=32)
+        return
+    q, P = 0, len(counts)
+    while q < P:
+        if counts[q] == 0:
+            q += 1
+            continue
+        e = q
+        while e + 1 < P and counts[e + 1]:
+            e += 1
+        # slots q..e: the last one needs only its real pairs
+        npairs = (e - q) * m + counts[e]
+        summary.fold_pairs(buf[2 * q * m: 2 * (q * m + npairs)], npairs, id_bits=32)
+        q = e + 1

@@ -336,13 +336,14 @@ def test_tree_exchange_single_process(oracle, torch_cuda, world):
         np.testing.assert_array_equal(ranks[0].dense().astype(np.int64), want[w], err_msg="window %d" % w)
 
 
+@pytest.mark.parametrize("slots", [False, True], ids=["deltas", "padded_slots"])
 @pytest.mark.parametrize("world", [2, 3, 4])
-def test_replicated_exchange_single_process(oracle, torch_cuda, world):
+def test_replicated_exchange_single_process(oracle, torch_cuda, world, slots):
     """AllgatherMerge's protocol replayed with device handles on this GPU: every rank folds its
     slice, exports its delta asynchronously (count in device memory), folds every other rank's
     delta with marking paused, closes; EVERY replica's emission must equal the oracle's."""
     torch = torch_cuda
-    from gsgpu.tree import fold_deltas
+    from gsgpu.tree import fold_deltas, fold_slots
     scale, n, W = 13, 200000, 20000
     cap = 1 << scale
     s, d = oracle.gen_rmat(0, n, scale, 9)
@@ -363,13 +364,23 @@ def test_replicated_exchange_single_process(oracle, torch_cuda, world):
             ranks[r].fold(ts[a:b], td[a:b])
             ranks[r].export_marks_async(bufs[r], cnt[r:r + 1])
         ns = [int(x) for x in cnt.tolist()]
+        m = max(ns)
+        if slots and m:                 # AllgatherMerge's layout: slots of m pairs, padded
+            for q in range(world):
+                if 0 < ns[q] < m:
+                    bufs[q][2 * ns[q]: 2 * m].view(-1, 2).copy_(bufs[q][0:2].view(1, 2).expand(m - ns[q], 2))
+            torch.cat([bufs[q][:2 * m] for q in range(world)], out=recv[:2 * m * world])
         for r in range(world):
             others = [q for q in range(world) if q != r]
             tot = sum(ns[q] for q in others)
-            if tot:
+            if tot and not slots:
                 torch.cat([bufs[q][:2 * ns[q]] for q in others], out=recv[:2 * tot])
             ranks[r].set_marking(False)
-            fold_deltas(ranks[r], recv, [ns[q] for q in others])
+            if slots:
+                if m:
+                    fold_slots(ranks[r], recv, m, [0 if q == r else ns[q] for q in range(world)])
+            else:
+                fold_deltas(ranks[r], recv, [ns[q] for q in others])
             ranks[r].set_marking(True)
             ranks[r].close_window()
         for r in range(world):
@@ -499,10 +510,14 @@ def test_bench_two_ranks_one_gpu_verified(merge):
 
 # ---------------- opt-in fold variants, end to end against the independent torch CC ----------------
 @pytest.mark.parametrize("env", [{"GSGPU_FOLD_MODE": "plain"}, {"GSGPU_FOLD_MODE": "ring"},
+                                 {"GSGPU_WARM": "0"}, {"GSGPU_WARM_MIN_BITS": "25"},
+                                 {"GSGPU_WARM_BUCKETS": "14", "GSGPU_WARM_AT": "1", "GSGPU_WARM_EVERY": "2"},
+                                 {"GSGPU_WARM_SAMPLE": "16777216", "GSGPU_FOLD_STATS": "1"},
                                  {"GSGPU_FOLD_MODE": "ring", "GSGPU_FOLD_STATS": "1"},
                                  {"GSGPU_FOLD_MODE": "plain", "GSGPU_FOLD_STATS": "1"},
                                  {"GSGPU_FOLD_MODE": "plain", "GSGPU_FOLD_EPT": "8"}, {"GSGPU_TIMING": "marker"}],
-                         ids=["plain", "ring", "ring_stats", "plain_stats", "plain_ept8", "marker_timing"])
+                         ids=["plain", "ring", "warm_off", "warm_production_default", "warm_tiny_table",
+                              "warm_big_sample_stats", "ring_stats", "plain_stats", "plain_ept8", "marker_timing"])
 def test_fold_variants_verified(env):
     import subprocess, sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -69,3 +69,37 @@ def test_tree_merge_gloo_matches_oracle(tmp_path, oracle, world, kind):
         got = np.load(tmp_path / ("emis%d.npy" % r))
         assert got.shape == want.shape
         np.testing.assert_array_equal(got, want, err_msg="rank %d" % r)
+
+
+@pytest.mark.parametrize("bulk", [False, True])
+def test_fold_slots_covers_real_pairs_only(monkeypatch, bulk):
+    """AllgatherMerge's padded slots: every real pair is folded, no empty (garbage) slot is, and
+    padding is only ever a copy of its own slot's first pair."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "gelly-streaming_amd")]
+    from gsgpu import tree
+    if bulk:
+        monkeypatch.setattr(tree, "BULK_DELTA_PAIRS", 2)
+    m, counts = 4, [3, 0, 4, 1, 0, 2]
+    buf = torch.full((2 * m * len(counts),), -7, dtype=torch.int32)     # -7: garbage
+    real = set()
+    for q, c in enumerate(counts):
+        for i in range(m if c else 0):
+            j = i if i < c else 0                                         # padding = first pair
+            buf[2 * (q * m + i)] = 100 * q + j
+            buf[2 * (q * m + i) + 1] = 100 * q + j + 50
+        real |= {(100 * q + j, 100 * q + j + 50) for j in range(c)}
+
+    class Rec:
+        def __init__(self):
+            self.got = set()
+
+        def fold_pairs(self, b, n, id_bits=32):
+            p = b[: 2 * n].view(-1, 2).tolist()
+            assert len(p) == n
+            self.got |= {tuple(x) for x in p}
+
+    r = Rec()
+    tree.fold_slots(r, buf, m, counts)
+    assert r.got == real

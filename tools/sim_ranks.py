@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "gelly-streaming_amd")]
 import gsgpu
 from gsgpu import gen
-from gsgpu.tree import fold_deltas, tree_schedule
+from gsgpu.tree import fold_slots, tree_schedule
 from gsgpu._abi import GS_K_FOLD, GS_K_COMPRESS
 
 P = int(sys.argv[1]) if len(sys.argv) > 1 else 8
@@ -51,6 +51,7 @@ for scheme in schemes:
     ranks = [gsgpu.DisjointSet(V, id_bits=32, track_marks=(ag or r != 0), stream=torch.cuda.current_stream()) for r in range(P)]
     if ag:
         dbufs = [torch.empty(2 * V, dtype=torch.int32, device="cuda") for _ in range(P)]
+        rbuf = [torch.empty(2, dtype=torch.int32, device="cuda")]
     scheds = [tree_schedule(r, P) for r in range(P)]
     print("== %s P=%d scale=%d W/rank=2^%d" % (scheme, P, scale, W.bit_length() - 1), flush=True)
     tot = dict(fold=0.0, close=0.0, crit=0.0, xfer=0.0, merge=0.0, pairs=0)
@@ -71,15 +72,20 @@ for scheme in schemes:
             if os.environ.get("SIM_VERBOSE") and w in (0, 15, 63):
                 print("   w%d export wall us %s" % (w + 1, ["%.0f" % x for x in tex]), flush=True)
             npairs = ns
-            xfer_us = max(tex) + 8 * max(ns) / LINK * 1e6     # all pairs of links at once
+            m = max(ns)
+            xfer_us = max(tex) + 8 * m / LINK * 1e6           # all pairs of links at once
+            # AllgatherMerge's layout: P slots of m pairs, each padded with copies of its first pair
+            for q in range(P):
+                if 0 < ns[q] < m:
+                    dbufs[q][2 * ns[q]: 2 * m].view(-1, 2).copy_(dbufs[q][0:2].view(1, 2).expand(m - ns[q], 2))
+            if m:
+                if rbuf[0].numel() < 2 * P * m:
+                    rbuf[0] = torch.empty(2 * P * m, dtype=torch.int32, device="cuda")
+                torch.cat([dbufs[q][:2 * m] for q in range(P)], out=rbuf[0][:2 * P * m])
             mt = []
             for r in range(P):
-                parts = [dbufs[q][:2 * ns[q]] for q in range(P) if q != r and ns[q]]
-                tot_n = sum(ns) - ns[r]
-                if parts:
-                    torch.cat(parts, out=buf[:2 * tot_n])
                 ranks[r].set_marking(False)
-                _, tf = timed(lambda: fold_deltas(ranks[r], buf, [ns[q] for q in range(P) if q != r]))
+                _, tf = timed(lambda: fold_slots(ranks[r], rbuf[0], m, [0 if q == r else ns[q] for q in range(P)]) if m else None)
                 ranks[r].set_marking(True)
                 mt.append(tf)
             merge_us = max(mt)
