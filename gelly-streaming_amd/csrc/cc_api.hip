@@ -265,15 +265,24 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
 }
 
 // Steady-state fold (mature forest, aligned device uint32 SoA), GSGPU_FOLD_MODE:
-//   ring  (default) k_fold_ring: LDS hot set + survivor rings, one persistent launch
-//   plain k_fold, as for young windows (the A/B baseline)
-enum FoldMode { kFoldPlain = 0, kFoldRing = 1 };
+//   auto  (default) ring once gbits outgrows an XCD's 4 MiB L2 (ids >= 2^25), else plain: with
+//         gbits L2-resident the hot set's 128 KiB LDS fill per workgroup costs more than it saves
+//         (RMAT-20 2^20-edge windows: ring 83 us, plain 61 us; ER 2^24: 141 vs 126 us)
+//   ring  k_fold_ring: LDS hot set (+ warm set) + survivor rings, one persistent launch
+//   plain k_fold, as for young windows
+enum FoldMode { kFoldPlain = 0, kFoldRing = 1, kFoldAuto = 2 };
 static int fold_mode() {
     static const int m = [] {
         const char* e = getenv("GSGPU_FOLD_MODE");
-        return (e && !strcmp(e, "plain")) ? (int)kFoldPlain : (int)kFoldRing;
+        if (e && !strcmp(e, "plain")) return (int)kFoldPlain;
+        if (e && !strcmp(e, "ring")) return (int)kFoldRing;
+        return (int)kFoldAuto;
     }();
     return m;
+}
+static bool use_ring(const gs_cc_t* h) {
+    const int m = fold_mode();
+    return m == kFoldRing || (m == kFoldAuto && h->hot_bits >= 25);
 }
 
 void launch_fold_ring(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t n) {
@@ -382,7 +391,7 @@ template <typename IdT, bool AOS>
 void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, size_t esz) {
     const uint64_t young_limit = h->cap / 4;
     // mature forest (past the young limit), aligned device uint32 SoA: the steady ring fold
-    if (std::is_same<IdT, uint32_t>::value && !AOS && h->hot && fold_mode() == kFoldRing &&
+    if (std::is_same<IdT, uint32_t>::value && !AOS && h->hot && use_ring(h) &&
         h->edges_since_reset >= ring_from() * young_limit && n >= 4 &&
         ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0) {
         const uint64_t done = n & ~(uint64_t)3;

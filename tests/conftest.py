@@ -11,6 +11,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # oracle comparison of a >= 2^20-id stream goes through it. tests/test_gpu_parity.py runs the
 # production default (and GSGPU_WARM=0) in subprocesses.
 os.environ.setdefault("GSGPU_WARM_MIN_BITS", "20")
+# Likewise the steady ring fold (LDS hot set) runs from 2^20 ids in tests (production: from 2^25;
+# the auto choice is run by the fold-variant subprocesses).
+os.environ.setdefault("GSGPU_FOLD_MODE", "ring")
 for p in (ROOT, os.path.join(ROOT, "gelly-streaming_amd"), os.path.join(ROOT, "oracle")):
     if p not in sys.path:
         sys.path.insert(0, p)

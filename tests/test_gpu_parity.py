@@ -509,14 +509,14 @@ def test_bench_two_ranks_one_gpu_verified(merge):
 
 
 # ---------------- opt-in fold variants, end to end against the independent torch CC ----------------
-@pytest.mark.parametrize("env", [{"GSGPU_FOLD_MODE": "plain"}, {"GSGPU_FOLD_MODE": "ring"},
+@pytest.mark.parametrize("env", [{"GSGPU_FOLD_MODE": "plain"}, {"GSGPU_FOLD_MODE": "ring"}, {"GSGPU_FOLD_MODE": "auto"},
                                  {"GSGPU_WARM": "0"}, {"GSGPU_WARM_MIN_BITS": "25"},
                                  {"GSGPU_WARM_BUCKETS": "14", "GSGPU_WARM_AT": "1", "GSGPU_WARM_EVERY": "2"},
                                  {"GSGPU_WARM_SAMPLE": "16777216", "GSGPU_FOLD_STATS": "1"},
                                  {"GSGPU_FOLD_MODE": "ring", "GSGPU_FOLD_STATS": "1"},
                                  {"GSGPU_FOLD_MODE": "plain", "GSGPU_FOLD_STATS": "1"},
                                  {"GSGPU_FOLD_MODE": "plain", "GSGPU_FOLD_EPT": "8"}, {"GSGPU_TIMING": "marker"}],
-                         ids=["plain", "ring", "warm_off", "warm_production_default", "warm_tiny_table",
+                         ids=["plain", "ring", "auto", "warm_off", "warm_production_default", "warm_tiny_table",
                               "warm_big_sample_stats", "ring_stats", "plain_stats", "plain_ept8", "marker_timing"])
 def test_fold_variants_verified(env):
     import subprocess, sys
