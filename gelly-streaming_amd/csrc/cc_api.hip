@@ -387,6 +387,20 @@ static uint64_t ring_from() {
     return v;
 }
 
+// GSGPU_YOUNG_SPLIT=S (0 = off), GSGPU_YOUNG_SPLITS=k: inside the young forest, close internally
+// (compress + giant pick: no emission, labels stay canonical) after S, 2S, .. 2^(k-1) S edges
+// since reset, so the rest of the young window folds with the giant filter on
+static uint64_t young_split() { static const uint64_t v = env_u64("GSGPU_YOUNG_SPLIT", 0); return v; }
+static uint64_t young_splits() { static const uint64_t v = env_u64("GSGPU_YOUNG_SPLITS", 1); return v; }
+static uint64_t next_young_split(uint64_t done) {
+    uint64_t s = young_split();
+    for (uint64_t i = 0; s && i < young_splits(); ++i, s *= 2)
+        if (done < s) return s;
+    return 0;
+}
+
+int compress_impl(gs_cc_t* h);
+
 template <typename IdT, bool AOS>
 void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, size_t esz) {
     const uint64_t young_limit = h->cap / 4;
@@ -414,6 +428,10 @@ void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, siz
                 c = std::min(c, r);
             }
             m = std::min(m, std::max<uint64_t>(std::min(c, left), 1));
+            if (!AOS && !h->sparse) {
+                const uint64_t sp = next_young_split(h->edges_since_reset);
+                if (sp) m = std::min(m, sp - h->edges_since_reset);
+            }
         } else if (AOS && off == 0 && merge_head() && n > kMergeBulk) {
             m = std::min(m, merge_head());
         } else if (AOS && merge_chunk()) {
@@ -422,8 +440,14 @@ void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, siz
         const size_t stride = AOS ? 2 * esz : esz;
         launch_fold<IdT, AOS>(h, a + off * stride, b ? b + off * esz : nullptr, m,
                               h->edges_since_reset < young_limit);
+        const uint64_t sp = (!AOS && !h->sparse && h->edges_since_reset < young_limit) ? next_young_split(h->edges_since_reset) : 0;
         h->edges_since_reset += m;
         off += m;
+        if (sp && h->edges_since_reset == sp && off < n) {
+            h->compressed = false;
+            (void)compress_impl(h);
+            h->compressed = false;
+        }
     }
 }
 
