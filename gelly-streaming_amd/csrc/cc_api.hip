@@ -62,6 +62,7 @@ struct gs_cc {
     uint32_t* parent = nullptr;          // dense summary / label array
     uint32_t* mark = nullptr;            // export mark bitmap, 1 bit per vertex (GS_CC_TRACK_MARKS)
     uint32_t* mark_buf = nullptr;        // the mark allocation (mark = mark_buf while marking, else null)
+    uint32_t* export_bcnt = nullptr;     // per-workgroup mark counts of an export (kExportBlocks words)
     uint32_t* gbits = nullptr;           // giant-component filter bitmap (1 bit per vertex)
     uint32_t* sbits = nullptr;           // seen bitmap (1 bit per vertex), set on first touch
     uint32_t* derr = nullptr;            // derr[0] deferred device error flags; derr[1..5] giant state
@@ -387,13 +388,20 @@ static uint64_t ring_from() {
     return v;
 }
 
-// GSGPU_YOUNG_SPLIT=S (0 = off), GSGPU_YOUNG_SPLITS=k: inside the young forest, close internally
-// (compress + giant pick: no emission, labels stay canonical) after S, 2S, .. 2^(k-1) S edges
-// since reset, so the rest of the young window folds with the giant filter on
-static uint64_t young_split() { static const uint64_t v = env_u64("GSGPU_YOUNG_SPLIT", 0); return v; }
+// GSGPU_YOUNG_SPLIT=S, GSGPU_YOUNG_SPLITS=k: inside the young forest, close internally (compress
+// + giant pick: no emission, labels stay canonical) after S, 2S, .. 2^(k-1) S edges since reset,
+// so the rest of the young window folds with the giant filter on. Default: one split at
+// capacity / 16 edges where gbits outgrows L2 (ids >= 2^25; 0 = off). RMAT-26 window 1:
+// 1487 -> 1297 us for one extra full close (+118 us); splits at 2^21 or 2^23, or 3-5 doubling
+// splits, gained less (tools/young_split_sweep.sh)
+static uint64_t young_split(const gs_cc_t* h) {
+    static const uint64_t v = env_u64("GSGPU_YOUNG_SPLIT", ~0ull);
+    if (v != ~0ull) return v;
+    return h->cap >= (1u << 25) ? h->cap / 16 : 0;
+}
 static uint64_t young_splits() { static const uint64_t v = env_u64("GSGPU_YOUNG_SPLITS", 1); return v; }
-static uint64_t next_young_split(uint64_t done) {
-    uint64_t s = young_split();
+static uint64_t next_young_split(const gs_cc_t* h, uint64_t done) {
+    uint64_t s = young_split(h);
     for (uint64_t i = 0; s && i < young_splits(); ++i, s *= 2)
         if (done < s) return s;
     return 0;
@@ -429,7 +437,7 @@ void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, siz
             }
             m = std::min(m, std::max<uint64_t>(std::min(c, left), 1));
             if (!AOS && !h->sparse) {
-                const uint64_t sp = next_young_split(h->edges_since_reset);
+                const uint64_t sp = next_young_split(h, h->edges_since_reset);
                 if (sp) m = std::min(m, sp - h->edges_since_reset);
             }
         } else if (AOS && off == 0 && merge_head() && n > kMergeBulk) {
@@ -440,7 +448,7 @@ void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, siz
         const size_t stride = AOS ? 2 * esz : esz;
         launch_fold<IdT, AOS>(h, a + off * stride, b ? b + off * esz : nullptr, m,
                               h->edges_since_reset < young_limit);
-        const uint64_t sp = (!AOS && !h->sparse && h->edges_since_reset < young_limit) ? next_young_split(h->edges_since_reset) : 0;
+        const uint64_t sp = (!AOS && !h->sparse && h->edges_since_reset < young_limit) ? next_young_split(h, h->edges_since_reset) : 0;
         h->edges_since_reset += m;
         off += m;
         if (sp && h->edges_since_reset == sp && off < n) {
@@ -717,6 +725,7 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
     if (hipMalloc(&h->parent, (size_t)h->cap * sizeof(uint32_t)) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "parent[%u] allocation failed", h->cap)); }
     if (cfg->flags & GS_CC_TRACK_MARKS) {
         if (hipMalloc(&h->mark_buf, mark_bytes(h->cap)) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "mark allocation failed")); }
+        if (hipMalloc(&h->export_bcnt, kExportBlocks * sizeof(uint32_t)) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "export count allocation failed")); }
         h->mark = h->mark_buf;
     }
     if (hipMalloc(&h->gbits, mark_bytes(h->cap)) != hipSuccess || hipMalloc(&h->sbits, mark_bytes(h->cap)) != hipSuccess ||
@@ -783,6 +792,7 @@ int gs_cc_destroy(gs_cc_t* h) {
     for (auto e : h->pool) (void)hipEventDestroy(e);
     if (h->parent) (void)hipFree(h->parent);
     if (h->mark_buf) (void)hipFree(h->mark_buf);
+    if (h->export_bcnt) (void)hipFree(h->export_bcnt);
     if (h->derr) (void)hipFree(h->derr);
     if (h->gbits) (void)hipFree(h->gbits);
     if (h->sbits) (void)hipFree(h->sbits);
@@ -1073,11 +1083,15 @@ int gs_cc_labels_device(gs_cc_t* h, const void** p) {
 }
 
 static int export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long* counter) {
-    GS_HIP(hipMemsetAsync(counter, 0, sizeof(unsigned long long), h->stream));
+    // one workgroup per contiguous range of mark words: GSGPU_EXPORT_BLOCKS (<= kExportBlocks)
+    static const unsigned eb = (unsigned)std::min<uint64_t>(std::max<uint64_t>(env_u64("GSGPU_EXPORT_BLOCKS", kExportBlocks), 1), kExportBlocks);
+    const dim3 grid(grid_for((h->cap + 31) / 32, 256, eb));
     {
         KTimer t(h, GS_K_EXPORT);
-        klaunch(k_export_marks, dim3(grid_for((h->cap + 31) / 32, 256, kExportBlocks)), dim3(256), h->stream, t.start(), t.stop(),
-                h->mark_buf, (const uint32_t*)h->parent, h->cap, (uint32_t*)out, cap, counter);
+        klaunch(k_export_count, grid, dim3(256), h->stream, t.start(), nullptr,
+                (const uint32_t*)h->mark_buf, h->cap, h->export_bcnt);
+        klaunch(k_export_marks, grid, dim3(256), h->stream, nullptr, t.stop(),
+                h->mark_buf, (const uint32_t*)h->parent, h->cap, (uint32_t*)out, cap, (const uint32_t*)h->export_bcnt, counter);
     }
     GS_HIP(hipGetLastError());
     return GS_OK;
