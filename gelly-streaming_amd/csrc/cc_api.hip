@@ -343,7 +343,7 @@ void launch_fold_ring(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t
                 (const uint32_t*)(h->derr + 7));
         const int nb = (int)(sizeof(bands) / sizeof(bands[0])) - 1;
         for (int i = 0; i < nb; ++i)
-            klaunch(k_warm_build, dim3(grid_for(cwords, 256, 8192)), dim3(256), h->stream, nullptr, nullptr, h->wcnt, cwords,
+            klaunch(k_warm_build, dim3(grid_for(cwords / 4 + 1, 256, 8192)), dim3(256), h->stream, nullptr, nullptr, h->wcnt, cwords,
                     h->warm, B, h->warm_bits, bands[i + 1], bands[i], (const uint2*)h->hot, hot.five, (const uint32_t*)h->gbits, h->derr + 7, (int)(i == nb - 1));
         klaunch(k_warm_done, dim3(1), dim3(1), h->stream, nullptr, t.stop(), h->derr + 7);
     }

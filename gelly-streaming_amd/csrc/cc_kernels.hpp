@@ -653,15 +653,36 @@ __global__ __launch_bounds__(256) void k_warm_build(uint32_t* __restrict__ wcnt,
                                                     uint32_t five, const uint32_t* __restrict__ gbits,
                                                     uint32_t* __restrict__ valid, int done) {
     if (*valid) return;                              // uniform (set by the last pass, after every read)
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += gridDim.x * blockDim.x) {
+    // 16 B of counters per lane (scalar 4-B reads: 61 us per pass over 128 MiB); most vectors are
+    // zero (2^23 sampled edges touch a fraction of 2^26 ids) and cost only the read
+    const uint32_t nvec = nwords / 4;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nvec; q += stride) {
+        u32x4 c4 = reinterpret_cast<const u32x4*>(wcnt)[q];
+        if ((c4.x | c4.y | c4.z | c4.w) == 0u) continue;
+        const uint32_t cw[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t c = cw[j];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t ck = (c >> (16 * k)) & 0xFFFFu;
+                const uint32_t v = 2 * (4 * q + j) + k;
+                // gbits (the last close's giant, a subset of the current one): whatever the counts
+                // say, only a giant member can enter
+                if (ck >= lo && ck < hi && ((gbits[v >> 5] >> (v & 31)) & 1u) && !(hot && hot_probe(hot, v, B, five != 0)))
+                    warm_insert(warm, v, B, wb);
+            }
+        }
+        if (done) reinterpret_cast<u32x4*>(wcnt)[q] = u32x4{0u, 0u, 0u, 0u};
+    }
+    for (uint32_t i = 4 * nvec + blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += stride) {   // tail words
         const uint32_t c = wcnt[i];
         if (!c) continue;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const uint32_t ck = (c >> (16 * k)) & 0xFFFFu;
             const uint32_t v = 2 * i + k;
-            // gbits (the last close's giant, a subset of the current one): whatever the counts
-            // say, only a giant member can enter
             if (ck >= lo && ck < hi && ((gbits[v >> 5] >> (v & 31)) & 1u) && !(hot && hot_probe(hot, v, B, five != 0)))
                 warm_insert(warm, v, B, wb);
         }
@@ -815,20 +836,35 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
         for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += gridDim.x * blockDim.x) {
             uint32_t cand = sbits[w] & ~gbits[w];
             uint32_t add = 0;
+            // up to 8 stragglers at a time, their parent and grandparent reads issued back to
+            // back (one at a time: a young Erdos-Renyi window's close, ~32 stragglers per word,
+            // spent 121 us per 2^24 ids in dependent loads)
             while (cand) {
-                const int b = __ffs(cand) - 1;
-                cand &= cand - 1;
-                const uint32_t v = (w << 5) + b;
-                const uint32_t p = parent[v];
-                uint32_t lab = p;
-                if (p != v) {
-                    const uint32_t gp = parent[p];
-                    if (gp != p) {
-                        lab = find_root_ro(parent, gp);
+                uint32_t vb[8], p[8], gp[8];
+                int m = 0;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    vb[k] = cand ? (uint32_t)(__ffs(cand) - 1) : 32u;
+                    if (cand) { cand &= cand - 1; ++m; }
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) p[k] = (k < m) ? parent[(w << 5) + vb[k]] : 0u;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t v = (w << 5) + vb[k];
+                    gp[k] = (k < m && p[k] != v) ? parent[p[k]] : p[k];
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    if (k >= m) continue;
+                    const uint32_t v = (w << 5) + vb[k];
+                    uint32_t lab = p[k];
+                    if (p[k] != v && gp[k] != p[k]) {
+                        lab = find_root_ro(parent, gp[k]);
                         parent[v] = lab;
                     }
+                    add |= (lab == g) ? (1u << vb[k]) : 0u;
                 }
-                add |= (lab == g) ? (1u << b) : 0u;
             }
             if (add) gbits[w] |= add;
         }
