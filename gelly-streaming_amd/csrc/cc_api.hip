@@ -335,13 +335,21 @@ void launch_fold_ring(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t
     }
     if (build) {
         // hottest band first: a full bucket then drops the colder ids (counts from 2^23 sampled edges)
-        static const uint32_t bands[] = {0xFFFFFFFFu, 32u, 8u, 3u, 2u};
+        // GSGPU_WARM_BANDS (A/B): number of band passes, 4 by default (3: [2, 8) in one pass, 2: [8, inf) +
+        // [2, 8): 0.17 ms per step slower, the bands' priority is worth more than their passes; 5, 6: finer)
+        static const uint32_t bands4[] = {0xFFFFFFFFu, 32u, 8u, 3u, 2u};
+        static const uint32_t bands3[] = {0xFFFFFFFFu, 32u, 8u, 2u};
+        static const uint32_t bands2[] = {0xFFFFFFFFu, 8u, 2u};
+        static const uint32_t bands5[] = {0xFFFFFFFFu, 64u, 16u, 8u, 3u, 2u};
+        static const uint32_t bands6[] = {0xFFFFFFFFu, 64u, 24u, 12u, 6u, 3u, 2u};
+        static const uint64_t nbands = env_u64("GSGPU_WARM_BANDS", 4);
+        const uint32_t* bands = nbands == 2 ? bands2 : nbands == 3 ? bands3 : nbands == 5 ? bands5 : nbands == 6 ? bands6 : bands4;
         const uint32_t B = h->hot_bits;
         const uint32_t wwords = 1u << h->warm_bits;
         const uint32_t cwords = (uint32_t)((((uint64_t)1 << B) + 1) / 2);
         klaunch(k_warm_clear, dim3(grid_for(wwords, 256, 2048)), dim3(256), h->stream, nullptr, nullptr, h->warm, wwords,
                 (const uint32_t*)(h->derr + 7));
-        const int nb = (int)(sizeof(bands) / sizeof(bands[0])) - 1;
+        const int nb = (nbands >= 2 && nbands <= 6) ? (int)nbands : 4;
         for (int i = 0; i < nb; ++i)
             klaunch(k_warm_build, dim3(grid_for(cwords / 4 + 1, 256, 8192)), dim3(256), h->stream, nullptr, nullptr, h->wcnt, cwords,
                     h->warm, B, h->warm_bits, bands[i + 1], bands[i], (const uint2*)h->hot, hot.five, (const uint32_t*)h->gbits, h->derr + 7, (int)(i == nb - 1));
