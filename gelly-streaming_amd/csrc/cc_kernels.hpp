@@ -329,7 +329,9 @@ __device__ __forceinline__ void warm_count(uint32_t* __restrict__ wcnt, uint32_t
 // (kHotAdmitLaunches after reset or after k_compress clears the set for a new giant) or when the
 // host's periodic refresh (every kHotAdmitEvery ring launches) asks: steady window 266 -> 240 us.
 constexpr uint32_t kHotAdmitLaunches = 8;
-constexpr uint32_t kHotAdmitEvery = 16;
+// every 64th (was 16th): 0.4-0.8 % faster per step on RMAT-26 (tools/knob_sweep2.sh: 16 / 32 / 64 /
+// never = 18.77 / 18.68 / 18.65 / 18.61 ms); a refresh is kept for streams whose hubs drift
+constexpr uint32_t kHotAdmitEvery = 64;
 
 __device__ __forceinline__ void hot_admit(const HotArgs& hot, uint32_t v) {
     uint32_t* slot = &hot.cand[(uint32_t)(splitmix64(v) >> (64 - kHotCandBits))];
