@@ -574,7 +574,12 @@ int compress_impl(gs_cc_t* h) {
         // 2048 workgroups: the incremental close is a 2M-word bitmap scan; 16384 cost 140 us more
         // per 64-window step (tools/sweep_env.sh)
         static const unsigned cgrid = (unsigned)std::max<uint64_t>(env_u64("GSGPU_COMPRESS_GRID", 2048), 1);
-        klaunch(k_compress, dim3(grid_for(h->cap, 1024, cgrid)), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
+        // closes of the young forest (<= capacity/4 edges since reset) are mostly full passes
+        // (a 4-B read per vertex + grandparent gathers): GSGPU_COMPRESS_GRID_YOUNG (A/B; 8192-65536
+        // gave the same close sum per 64-window step as 2048, tools/close_grid_sweep.sh)
+        static const unsigned ygrid = (unsigned)std::max<uint64_t>(env_u64("GSGPU_COMPRESS_GRID_YOUNG", 2048), 1);
+        const bool young = h->edges_since_reset <= (uint64_t)h->cap / 4;
+        klaunch(k_compress, dim3(grid_for(h->cap, 1024, young ? ygrid : cgrid)), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
                 h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot);
     }
     GS_HIP(hipGetLastError());
