@@ -307,6 +307,8 @@ void launch_fold_ring(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t
     hot.five = (five_ok && h->hot_bits <= kHotBucketBits + 12) ? 1u : 0u;
     static const uint32_t thresh = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(env_u64("GSGPU_HOT_THRESH", 3), 2), 63);
     hot.thresh = thresh;
+    static const uint32_t gflag = (uint32_t)env_u64("GSGPU_RING_GFLAG", 1);   // A/B: union_group_g
+    hot.gflag = gflag;
     // warm set: built (counted in this launch, then k_warm_build) at ring launch GSGPU_WARM_AT
     // after reset and every GSGPU_WARM_EVERY-th after it, each time only if the set is not valid
     // for the current giant (device-gated); GSGPU_WARM=0 turns it off, GSGPU_WARM_SAMPLE = edges

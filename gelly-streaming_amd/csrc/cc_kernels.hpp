@@ -276,6 +276,7 @@ struct HotArgs {
     const uint32_t* warm_valid = nullptr;      // device word: warm set built for the current giant
     uint32_t* wcnt = nullptr;                  // endpoint counters for the next warm build
     uint64_t count_edges = 0;                  // count this launch's first edges (if !*warm_valid)
+    uint32_t gflag = 1;                        // survivors' giant flags stand in for parent reads
 };
 
 // ---- warm set (L2-resident second tier) ----
@@ -358,7 +359,7 @@ __device__ __forceinline__ void hot_admit(const HotArgs& hot, uint32_t v) {
 template <bool STATS, int EPT, bool HOT>
 __device__ __forceinline__ void filter_group(const FoldArgs& f, const uint32_t (&u)[EPT], const uint32_t (&v)[EPT],
                                              bool (&ok)[EPT], const uint2* tab, const HotArgs& hot, bool insert,
-                                             bool warm = false, bool count = false) {
+                                             bool warm, bool count, uint32_t (&gflag)[EPT]) {
     bool hu[EPT], hv[EPT];       // LDS hot-set hits
     bool mu[EPT], mv[EPT];       // known giant members without a gbits load (LDS or warm hits)
     uint32_t wu[EPT], wv[EPT];
@@ -407,8 +408,10 @@ __device__ __forceinline__ void filter_group(const FoldArgs& f, const uint32_t (
         }
     }
 #pragma unroll
-    for (int k = 0; k < EPT; ++k)
-        ok[k] = ok[k] && !((wu[k] >> (u[k] & 31)) & (wv[k] >> (v[k] & 31)) & 1u);
+    for (int k = 0; k < EPT; ++k) {
+        gflag[k] = ((wu[k] >> (u[k] & 31)) & 1u) | (((wv[k] >> (v[k] & 31)) & 1u) << 1);
+        ok[k] = ok[k] && gflag[k] != 3u;
+    }
 }
 
 // Parent gathers and unions of the edges with ok[k] (all issued before any dependent step).
@@ -426,6 +429,27 @@ __device__ __forceinline__ void union_group(const FoldArgs& f, const uint32_t (&
         if (ok[k]) union_edge<MARK, STATS>(f.parent, f.mark, f.sbits, u[k], v[k], pu[k], pv[k], &st, f.halve != 0);
 }
 
+// As union_group, for survivors whose giant flags are known (bit 0: u in the giant, bit 1: v): a
+// giant member x was relabelled to the giant root gR by the last close and is no root (gR is), so
+// its parent word can only have moved to an ancestor of gR since; gR stands in for the parent[x]
+// read (the walk goes on from gR, halving with fetch_min, and the hook CAS decides as for any
+// stale read). Saves one random parent[] gather per survivor with one endpoint in the giant
+// (most survivors of windows 2-12: a first-touched vertex joining the giant).
+template <bool MARK, bool STATS, int EPT>
+__device__ __forceinline__ void union_group_g(const FoldArgs& f, const uint32_t (&u)[EPT], const uint32_t (&v)[EPT],
+                                              const bool (&ok)[EPT], const uint32_t (&gflag)[EPT], uint32_t gR,
+                                              FoldStats& st) {
+    uint32_t pu[EPT], pv[EPT];
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        pu[k] = !ok[k] ? 0u : (gflag[k] & 1u) ? gR : f.parent[u[k]];
+        pv[k] = !ok[k] ? 0u : (gflag[k] & 2u) ? gR : f.parent[v[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < EPT; ++k)
+        if (ok[k]) union_edge<MARK, STATS>(f.parent, f.mark, f.sbits, u[k], v[k], pu[k], pv[k], &st, f.halve != 0);
+}
+
 // Filter, parent gathers and unions of one thread's EPT edges (ids already range-checked;
 // ok[k] false = nothing to do for edge k).
 template <bool MARK, bool STATS, int EPT>
@@ -437,7 +461,8 @@ __device__ __forceinline__ void fold_group(const FoldArgs& f, bool filt, uint32_
     }
     uint32_t nvalid = 0, nfilt = 0;
     if (STATS) for (int k = 0; k < EPT; ++k) nvalid += ok[k];
-    if (filt) filter_group<STATS, EPT, false>(f, u, v, ok, nullptr, HotArgs{nullptr, 0, nullptr}, false);
+    uint32_t gflag[EPT];
+    if (filt) filter_group<STATS, EPT, false>(f, u, v, ok, nullptr, HotArgs{nullptr, 0, nullptr}, false, false, false, gflag);
     union_group<MARK, STATS, EPT>(f, u, v, ok, st);
     if (STATS) {
         for (int k = 0; k < EPT; ++k) nfilt += ok[k];
@@ -541,8 +566,11 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
 // full waves instead of a few lanes of a filter pass (unions inline in the filter pass: 280 us
 // per steady RMAT-26 window; survivors queued for a second launch: 252 + 18-107 us; ring: 259 us).
 constexpr int kRingCap = 128;                       // pairs per wave: 16 waves x 1 KiB of LDS
+// Ring entries carry the survivor's giant flags in bit 31 of each id (ids < 2^31 when gR != kInvalid,
+// see k_fold_ring).
 template <bool MARK, bool STATS>
-__device__ __forceinline__ void ring_flush(const FoldArgs& f, uint2* ring, uint32_t& cnt, uint32_t keep, FoldStats& st) {
+__device__ __forceinline__ void ring_flush(const FoldArgs& f, uint2* ring, uint32_t& cnt, uint32_t keep, FoldStats& st,
+                                           uint32_t gR) {
     const int lane = threadIdx.x & 63;
     // the ring is written and read by different lanes of this wave: order those LDS accesses
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -552,9 +580,10 @@ __device__ __forceinline__ void ring_flush(const FoldArgs& f, uint2* ring, uint3
         const uint32_t at = cnt - take;
         const bool ok1 = (uint32_t)lane < take;
         const uint2 e = ok1 ? ring[at + lane] : make_uint2(0u, 0u);
-        const uint32_t u[1] = {e.x}, v[1] = {e.y};
+        const uint32_t u[1] = {e.x & 0x7FFFFFFFu}, v[1] = {e.y & 0x7FFFFFFFu};
+        const uint32_t gf[1] = {(e.x >> 31) | ((e.y >> 31) << 1)};
         const bool ok[1] = {ok1};
-        union_group<MARK, STATS, 1>(f, u, v, ok, st);
+        union_group_g<MARK, STATS, 1>(f, u, v, ok, gf, gR, st);
         cnt = at;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -571,6 +600,10 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const uint32_t* __res
     if (filt) {
         for (uint32_t i = threadIdx.x; i < kHotBuckets; i += blockDim.x) tab[i] = hot.table[i];
     }
+    // the root gbits were built for (= the giant's label at the last close); survivors' giant
+    // flags use it in place of a parent[] read (union_group_g). Off (kInvalid) without a filter,
+    // for ids >= 2^31 (the ring's flag bit), or with GSGPU_RING_GFLAG=0 (hot.gflag)
+    const uint32_t gR = (filt && hot.gflag && f.rc.cap <= 0x80000000u) ? f.giant[1] : kInvalid;
     // admitting launch? (read before workgroup 0's decrement may land: a workgroup that reads the
     // decremented budget only skips this launch's admission, which is a heuristic anyway)
     const uint32_t budget = hot.budget ? *hot.budget : 1u;
@@ -590,6 +623,7 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const uint32_t* __res
         const uint64_t g = g0 + lane;
         uint32_t u[4] = {0, 0, 0, 0}, v[4] = {0, 0, 0, 0};
         bool ok[4] = {false, false, false, false};
+        uint32_t gf[4] = {0u, 0u, 0u, 0u};
         if (g < groups) {
             const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a) + g);
             const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b) + g);
@@ -605,7 +639,11 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const uint32_t* __res
             if (bad) atomicOr(f.rc.err, 1u);
         }
         if (STATS) for (int k = 0; k < 4; ++k) nvalid += ok[k];
-        if (filt) filter_group<STATS, 4, true>(f, u, v, ok, tab, hot, g * 4 < sample_edges, warm_ok, g * 4 < count_edges);
+        if (filt) filter_group<STATS, 4, true>(f, u, v, ok, tab, hot, g * 4 < sample_edges, warm_ok, g * 4 < count_edges, gf);
+        if (gR == kInvalid) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) gf[k] = 0u;
+        }
         const uint32_t c = (uint32_t)ok[0] + ok[1] + ok[2] + ok[3];
         if (STATS) nkept += c;
         uint32_t incl = c;
@@ -617,21 +655,21 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const uint32_t* __res
         const uint32_t wtot = __shfl(incl, 63, 64);
         if (wtot == 0) continue;                     // uniform
         if (wtot > kRingCap / 2) {                   // young window: union in place
-            union_group<MARK, STATS, 4>(f, u, v, ok, st);
+            union_group_g<MARK, STATS, 4>(f, u, v, ok, gf, gR, st);
             continue;
         }
-        if (cnt + wtot > kRingCap) ring_flush<MARK, STATS>(f, ring, cnt, kRingCap - wtot, st);
+        if (cnt + wtot > kRingCap) ring_flush<MARK, STATS>(f, ring, cnt, kRingCap - wtot, st, gR);
         uint32_t pos = cnt + incl - c;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (!ok[k]) continue;
-            ring[pos] = make_uint2(u[k], v[k]);
+            ring[pos] = make_uint2(u[k] | ((gf[k] & 1u) << 31), v[k] | ((gf[k] >> 1) << 31));
             ++pos;
         }
         cnt += wtot;
-        if (cnt >= 64) ring_flush<MARK, STATS>(f, ring, cnt, cnt - 64, st);
+        if (cnt >= 64) ring_flush<MARK, STATS>(f, ring, cnt, cnt - 64, st, gR);
     }
-    ring_flush<MARK, STATS>(f, ring, cnt, 0, st);
+    ring_flush<MARK, STATS>(f, ring, cnt, 0, st, gR);
     if (STATS) {
         atomicAdd(&f.stats[0], nvalid);
         atomicAdd(&f.stats[1], nvalid - nkept);

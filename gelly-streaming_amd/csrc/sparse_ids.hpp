@@ -88,7 +88,8 @@ __global__ __launch_bounds__(256) void k_fold_sparse(const int64_t* __restrict__
                 if (!ok[k]) { u[k] = 0; v[k] = 0; }
             }
         }
-        if (filt) filter_group<false, 2, false>(f, u, v, ok, nullptr, HotArgs{nullptr, 0, nullptr}, false);
+        uint32_t gflag[2];
+        if (filt) filter_group<false, 2, false>(f, u, v, ok, nullptr, HotArgs{nullptr, 0, nullptr}, false, false, false, gflag);
         union_group<MARK, false, 2>(f, u, v, ok, st);
     }
 }
