@@ -434,7 +434,11 @@ __device__ __forceinline__ void union_group(const FoldArgs& f, const uint32_t (&
 // its parent word can only have moved to an ancestor of gR since; gR stands in for the parent[x]
 // read (the walk goes on from gR, halving with fetch_min, and the hook CAS decides as for any
 // stale read). Saves one random parent[] gather per survivor with one endpoint in the giant
-// (most survivors of windows 2-12: a first-touched vertex joining the giant).
+// (most survivors of windows 2-12: a first-touched vertex joining the giant). Ring fold only:
+// in the young forest the giant root gR is hooked again and again, and every walk from a stand-in
+// gR then halves a shared word (x = a hub, or gR's own word when the walk starts at gR):
+// one same-address atomic per edge, window 1 1.3 -> 2.7 ms; taking gR itself for a root instead
+// fails every hook CAS on gR's word once it is hooked (14 ms). tools/gflag_check.sh
 template <bool MARK, bool STATS, int EPT>
 __device__ __forceinline__ void union_group_g(const FoldArgs& f, const uint32_t (&u)[EPT], const uint32_t (&v)[EPT],
                                               const bool (&ok)[EPT], const uint32_t (&gflag)[EPT], uint32_t gR,
