@@ -124,14 +124,6 @@ hipEvent_t get_event(gs_cc_t* h) {
     return e;
 }
 
-// GSGPU_TIMING=marker: separate hipEventRecord marker packets around each timed launch (each
-// one is a barrier packet: ~10 us of idle GPU per marker on gfx950, profiles/r01_v3). Default:
-// the events ride on the kernel dispatch itself (hipExtLaunchKernelGGL start/stop events).
-static bool timing_markers() {
-    static const bool on = [] { const char* e = getenv("GSGPU_TIMING"); return e && !strcmp(e, "marker"); }();
-    return on;
-}
-
 // Times one span of launches of kernel class k (HIP events on the launch stream). Launch the
 // span's first kernel with start() and its last with stop() through klaunch().
 // the current giant-state slot (cc_kernels.hpp): derr[1 + 2 * (closes & 1)] = giant, [+1] = built;
@@ -139,21 +131,20 @@ static bool timing_markers() {
 // set admission budget, derr[7] = warm set valid
 inline uint32_t* giant_state(gs_cc_t* h) { return h->derr + 1 + 2 * (h->closes & 1); }
 
+// The events ride on the kernel dispatches themselves (hipExtLaunchKernelGGL start/stop events):
+// separate hipEventRecord marker packets are barrier packets, ~10 us of idle GPU each on gfx950
+// (profiles/r01_v3).
 struct KTimer {
-    gs_cc_t* h; int k; hipEvent_t a = nullptr, b = nullptr; bool markers = false;
+    gs_cc_t* h; int k; hipEvent_t a = nullptr, b = nullptr;
     KTimer(gs_cc_t* h_, int k_) : h(h_), k(k_) {
         if (!h->timing || !(h->timing_mask & (1u << k))) return;
         a = get_event(h);
         b = get_event(h);
-        markers = timing_markers();
-        if (markers) (void)hipEventRecord(a, h->stream);
     }
-    hipEvent_t start() const { return markers ? nullptr : a; }
-    hipEvent_t stop() const { return markers ? nullptr : b; }
+    hipEvent_t start() const { return a; }
+    hipEvent_t stop() const { return b; }
     ~KTimer() {
-        if (!a) return;
-        if (markers) (void)hipEventRecord(b, h->stream);
-        h->pending.push_back({k, a, b});
+        if (a) h->pending.push_back({k, a, b});
     }
 };
 
@@ -194,58 +185,84 @@ int sync_and_check(gs_cc_t* h) {
     return GS_OK;
 }
 
-// edges per thread of the fold (4 or 8; GSGPU_FOLD_EPT for experiments, read once)
-static int fold_ept() {
-    static const int ept = [] {
-        const char* e = getenv("GSGPU_FOLD_EPT");
-        return (e && atoi(e) == 8) ? 8 : 4;
-    }();
-    return ept;
+// ---- tuning constants (MI355X, RMAT-26 EF16, 2^24-edge windows unless noted) ----
+// Young forest (fewer than capacity/4 edges folded since reset): ONE launch of k_fold with a
+// dynamic chunk counter, kYoungBlocksPerCu workgroups per CU, kYoungEpt edges per thread (edges in
+// flight = CUs x 2 x 256 x 2 is what bounds the hub contention): window 1 64 launches of 2^18
+// edges 1746 us, one launch 2/CU 1403 us, 4/CU 2265 us; EPT 4 -> 2: 1873 -> 1715 us.
+constexpr int kYoungEpt = 2;
+constexpr unsigned kYoungBlocksPerCu = 2;
+// Folding a partial summary (AOS pairs: fold_pairs / the multi-GPU merge): the pairs (v, R) of one
+// component all name its root R; while R's component is not yet joined to the receiver's, every
+// pair in flight CASes the same word (RMAT-26 window-1 deltas: 5-14 ms for 6M pairs). A head
+// launch of kMergeHead pairs makes the big joins first (8 ranks' window-1 merges: 32 ms in one
+// launch each, 2.1 ms with a 2^10 head; 2^14: 2.6, 2^17: 6.5), then the rest in one launch.
+constexpr uint64_t kMergeHead = 1u << 10;
+constexpr uint64_t kMergeBulk = 1ull << 20;   // smaller batches: one launch (a delta of a mature
+                                              // summary rarely joins big components)
+// k_compress grid: the incremental close is a bitmap scan; 16384 workgroups cost 140 us more per
+// 64-window step than 2048 (young closes: 8192-65536 gave the same sum as 2048)
+constexpr unsigned kCompressGrid = 2048;
+// Steady ring fold and its warm set from ids >= 2^kRingMinBits (gbits outgrows an XCD's 4 MiB L2):
+// with gbits L2-resident the hot set's 128 KiB LDS fill per workgroup costs more than it saves
+// (RMAT-20 2^20-edge windows: ring 83 us, plain 61 us; ER 2^24: 141 vs 126 us).
+constexpr uint32_t kRingMinBits = 25;
+// warm set: counted in ring launch kWarmAt after reset (kWarmSample edges) and re-checked every
+// kWarmEvery-th launch (rebuilt only when invalid for the current giant); 4 band passes, hottest
+// first (2 bands: +0.17 ms per step; 2^24-edge samples: more hits, no faster once the count is paid)
+constexpr uint64_t kWarmAt = 3, kWarmEvery = 16, kWarmSample = 1ull << 23;
+constexpr uint32_t kWarmBucketsMaxBits = 18;        // 2^18 x 4 B = 1 MiB table at RMAT-26
+constexpr uint32_t kWarmBands[] = {0xFFFFFFFFu, 32u, 8u, 3u, 2u};
+constexpr uint32_t kHotThresh = 3;                  // sightings before hot-set admission (233 -> 229 us)
+// Young split: inside the young forest, close internally (compress + giant pick: no emission,
+// labels stay canonical) after capacity/16 edges, so the rest of the young window folds with the
+// giant filter on (RMAT-26 window 1: 1487 -> 1297 us for one extra full close of 118 us; splits
+// at 2^21 or 2^23, or 3-5 doubling splits, gained less). Only where gbits outgrows L2.
+constexpr uint32_t kYoungSplitDiv = 16;
+
+// ---- debug variables (read once per process; none is needed in production) ----
+//   GSGPU_FOLD_STATS=1       per-window fold counters on stderr (STATS kernel variants; same results)
+//   GSGPU_FOLD_MODE=plain|ring|auto   force the steady fold variant (parity tests of each variant)
+//   GSGPU_RING_MIN_BITS=B    ring fold + warm set from ids >= 2^B instead of 2^25 (tests at small sizes)
+//   GSGPU_YOUNG_SPLIT=S      young split after S edges instead of capacity/16 (0 = off; tests)
+enum FoldMode { kFoldPlain = 0, kFoldRing = 1, kFoldAuto = 2 };
+struct DebugEnv {
+    bool fold_stats = false;
+    int fold_mode = kFoldAuto;
+    uint32_t ring_min_bits = kRingMinBits;
+    uint64_t young_split = ~0ull;                   // ~0: the production rule
+    DebugEnv() {
+        const char* e = getenv("GSGPU_FOLD_STATS");
+        fold_stats = e && atoi(e) != 0;
+        e = getenv("GSGPU_FOLD_MODE");
+        if (e && !strcmp(e, "plain")) fold_mode = kFoldPlain;
+        if (e && !strcmp(e, "ring")) fold_mode = kFoldRing;
+        e = getenv("GSGPU_RING_MIN_BITS");
+        if (e && *e) ring_min_bits = (uint32_t)strtoul(e, nullptr, 0);
+        e = getenv("GSGPU_YOUNG_SPLIT");
+        if (e && *e) young_split = strtoull(e, nullptr, 0);
+    }
+};
+static const DebugEnv& dbg() {
+    static const DebugEnv d;
+    return d;
 }
 
-static bool fold_stats_on() {
-    static const bool on = [] { const char* e = getenv("GSGPU_FOLD_STATS"); return e && atoi(e) != 0; }();
-    return on;
-}
-
-// young-forest knobs (read once; tools/sweep_young.sh): GSGPU_YOUNG_EPT (edges per thread in young
-// launches: 2 by default, 1/4/8), GSGPU_YOUNG_CHUNK (edges per young launch, 2^18), GSGPU_RING_FROM
-// (the ring fold starts once edges_since_reset >= RING_FROM * capacity / 4; 1). RMAT-26 windows
-// 1-12: EPT 4 -> 2 took window 1 from 1873 to 1715 us; starting the ring (and the hot set's
-// admission) one window earlier saved 140 us over windows 2-12; larger chunks were slower.
-static uint64_t env_u64(const char* name, uint64_t dflt) {
-    const char* e = getenv(name);
-    return (e && *e) ? strtoull(e, nullptr, 0) : dflt;
-}
-static int young_ept() {
-    static const int v = [] { const uint64_t x = env_u64("GSGPU_YOUNG_EPT", 2); return (x == 1 || x == 2 || x == 4 || x == 8) ? (int)x : 0; }();
-    return v;
-}
-
-// path halving in young / merge launches: GSGPU_YOUNG_HALVE, GSGPU_MERGE_HALVE (1 = on)
-static bool young_halve() { static const bool v = env_u64("GSGPU_YOUNG_HALVE", 1) != 0; return v; }
-static bool merge_halve() { static const bool v = env_u64("GSGPU_MERGE_HALVE", 1) != 0; return v; }
-
-// young forest as ONE launch with a dynamic chunk counter (k_fold f.work; GSGPU_YOUNG_PERSIST=0:
-// launches of young_chunk() edges), GSGPU_YOUNG_BPC workgroups per CU (edges in flight = CUs x
-// BPC x 256 x EPT). RMAT-26 window 1: 64 launches 1746 us (+ 63 launch gaps of ~6 us), one
-// launch with 2 workgroups per CU 1403 us; 4 per CU 2265 us (more edges in flight, more hub
-// contention).
-static bool young_persist() { static const bool v = env_u64("GSGPU_YOUNG_PERSIST", 1) != 0; return v; }
-static unsigned young_bpc() { static const unsigned v = (unsigned)std::max<uint64_t>(env_u64("GSGPU_YOUNG_BPC", 2), 1); return v; }
-
-template <typename IdT, bool AOS>
-void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool young = false) {
-    const int ept = (young && young_ept()) ? young_ept() : fold_ept();
-    const bool persist = young && young_persist() && h->cus > 0;
-    const unsigned grid = persist ? (unsigned)std::min<uint64_t>((uint64_t)h->cus * young_bpc(), grid_for((n + ept - 1) / ept, kFoldThreads, 1u << 20))
-                                  : grid_for((n + ept - 1) / ept, kFoldThreads, 16384);
-    if (fold_stats_on() && !h->dstats) {
+static void ensure_stats(gs_cc_t* h) {
+    if (dbg().fold_stats && !h->dstats) {
         (void)hipMalloc(&h->dstats, 8 * sizeof(unsigned long long));
         (void)hipMemsetAsync(h->dstats, 0, 8 * sizeof(unsigned long long), h->stream);
     }
+}
+
+template <typename IdT, bool AOS>
+void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool young = false) {
+    const int ept = young ? kYoungEpt : kEdgesPerThread;
+    const bool persist = young && h->cus > 0;
+    const unsigned grid = persist ? (unsigned)std::min<uint64_t>((uint64_t)h->cus * kYoungBlocksPerCu, grid_for((n + ept - 1) / ept, kFoldThreads, 1u << 20))
+                                  : grid_for((n + ept - 1) / ept, kFoldThreads, 16384);
+    ensure_stats(h);
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
-    f.halve = AOS ? merge_halve() : young ? young_halve() : 1u;
     if (persist) {
         f.work = reinterpret_cast<unsigned long long*>(h->derr + 8);
         (void)hipMemsetAsync(f.work, 0, sizeof(unsigned long long), h->stream);
@@ -257,72 +274,40 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
     klaunch((k_fold<IdT, AOS, MARKV, VECV, EPTV, STV>), dim3(grid), dim3(kFoldThreads), h->stream, t.start(), t.stop(), \
             (const IdT*)a, (const IdT*)b, f)
     if (h->dstats) { if (h->mark) GS_LAUNCH_FOLD(true, false, 4, true); else GS_LAUNCH_FOLD(false, false, 4, true); }
-    else if (ept == 1) { if (h->mark) GS_LAUNCH_FOLD(true, false, 1, false); else GS_LAUNCH_FOLD(false, false, 1, false); }
-    else if (ept == 2) { if (h->mark) GS_LAUNCH_FOLD(true, false, 2, false); else GS_LAUNCH_FOLD(false, false, 2, false); }
-    else if (vec && ept == 8) { if (h->mark) GS_LAUNCH_FOLD(true, true, 8, false); else GS_LAUNCH_FOLD(false, true, 8, false); }
+    else if (ept == kYoungEpt) { if (h->mark) GS_LAUNCH_FOLD(true, false, kYoungEpt, false); else GS_LAUNCH_FOLD(false, false, kYoungEpt, false); }
     else if (h->mark) { if (vec) GS_LAUNCH_FOLD(true, true, 4, false); else GS_LAUNCH_FOLD(true, false, 4, false); }
     else { if (vec) GS_LAUNCH_FOLD(false, true, 4, false); else GS_LAUNCH_FOLD(false, false, 4, false); }
 #undef GS_LAUNCH_FOLD
 }
 
-// Steady-state fold (mature forest, aligned device uint32 SoA), GSGPU_FOLD_MODE:
-//   auto  (default) ring once gbits outgrows an XCD's 4 MiB L2 (ids >= 2^25), else plain: with
-//         gbits L2-resident the hot set's 128 KiB LDS fill per workgroup costs more than it saves
-//         (RMAT-20 2^20-edge windows: ring 83 us, plain 61 us; ER 2^24: 141 vs 126 us)
-//   ring  k_fold_ring: LDS hot set (+ warm set) + survivor rings, one persistent launch
-//   plain k_fold, as for young windows
-enum FoldMode { kFoldPlain = 0, kFoldRing = 1, kFoldAuto = 2 };
-static int fold_mode() {
-    static const int m = [] {
-        const char* e = getenv("GSGPU_FOLD_MODE");
-        if (e && !strcmp(e, "plain")) return (int)kFoldPlain;
-        if (e && !strcmp(e, "ring")) return (int)kFoldRing;
-        return (int)kFoldAuto;
-    }();
-    return m;
-}
+// Steady-state fold (mature forest, aligned device uint32 SoA): k_fold_ring (LDS hot set + warm set
+// + survivor rings, one persistent launch) once gbits outgrows an XCD's L2, else k_fold as for
+// young windows (GSGPU_FOLD_MODE forces either)
 static bool use_ring(const gs_cc_t* h) {
-    const int m = fold_mode();
-    return m == kFoldRing || (m == kFoldAuto && h->hot_bits >= 25);
+    const int m = dbg().fold_mode;
+    return m == kFoldRing || (m == kFoldAuto && h->hot_bits >= dbg().ring_min_bits);
 }
 
 void launch_fold_ring(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t n) {
-    if (fold_stats_on() && !h->dstats) {
-        (void)hipMalloc(&h->dstats, 8 * sizeof(unsigned long long));
-        (void)hipMemsetAsync(h->dstats, 0, 8 * sizeof(unsigned long long), h->stream);
-    }
+    ensure_stats(h);
     HotArgs hot{h->hot, h->hot_bits, h->hot_cand};
-    // A/B knobs: GSGPU_HOT_SAMPLE (edges of each launch offered for admission), GSGPU_HOT_PROBE
-    static const uint64_t sample = env_u64("GSGPU_HOT_SAMPLE", kHotSampleEdges);
-    static const uint32_t probe = (uint32_t)env_u64("GSGPU_HOT_PROBE", 1);
-    // admission: while the device budget lasts (cc_kernels.hpp), plus every GSGPU_HOT_ADMIT_EVERY-th
-    // launch (kHotAdmitEvery; 1 = every launch)
-    static const uint64_t every = std::max<uint64_t>(env_u64("GSGPU_HOT_ADMIT_EVERY", kHotAdmitEvery), 1);
-    hot.sample_edges = sample;
+    // admission: while the device budget lasts (cc_kernels.hpp), plus every kHotAdmitEvery-th launch
+    hot.sample_edges = kHotSampleEdges;
     hot.budget = h->derr + 6;
-    hot.periodic = (h->ring_launches % every == every - 1) ? 1u : 0u;
+    hot.periodic = (h->ring_launches % kHotAdmitEvery == kHotAdmitEvery - 1) ? 1u : 0u;
     ++h->ring_launches;
-    hot.probe = probe;
-    static const bool five_ok = env_u64("GSGPU_HOT_FIVE", 1) != 0;
-    hot.five = (five_ok && h->hot_bits <= kHotBucketBits + 12) ? 1u : 0u;
-    static const uint32_t thresh = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(env_u64("GSGPU_HOT_THRESH", 3), 2), 63);
-    hot.thresh = thresh;
-    static const uint32_t gflag = (uint32_t)env_u64("GSGPU_RING_GFLAG", 1);   // A/B: union_group_g
-    hot.gflag = gflag;
-    // warm set: built (counted in this launch, then k_warm_build) at ring launch GSGPU_WARM_AT
-    // after reset and every GSGPU_WARM_EVERY-th after it, each time only if the set is not valid
-    // for the current giant (device-gated); GSGPU_WARM=0 turns it off, GSGPU_WARM_SAMPLE = edges
-    // counted
-    static const uint64_t warm_at = env_u64("GSGPU_WARM_AT", 3);
-    static const uint64_t warm_every = std::max<uint64_t>(env_u64("GSGPU_WARM_EVERY", 16), 1);
-    static const uint64_t warm_sample = std::min<uint64_t>(env_u64("GSGPU_WARM_SAMPLE", 1ull << 23), 1ull << 24);
+    hot.five = (h->hot_bits <= kHotBucketBits + 12) ? 1u : 0u;
+    hot.thresh = kHotThresh;
+    // warm set: counted in this launch, then built by k_warm_build, at ring launch kWarmAt after
+    // reset and every kWarmEvery-th after it, each time only if the set is not valid for the
+    // current giant (device-gated)
     const uint64_t launch_no = h->ring_launches - 1;
-    const bool build = h->warm && launch_no >= warm_at && (launch_no - warm_at) % warm_every == 0;
+    const bool build = h->warm && launch_no >= kWarmAt && (launch_no - kWarmAt) % kWarmEvery == 0;
     hot.warm = h->warm;
     hot.warm_bits = h->warm_bits;
     hot.warm_valid = h->derr + 7;
     hot.wcnt = build ? h->wcnt : nullptr;
-    hot.count_edges = build ? warm_sample : 0;
+    hot.count_edges = build ? kWarmSample : 0;
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
     KTimer t(h, h->fold_timer);
     const bool st = h->dstats != nullptr;
@@ -336,95 +321,39 @@ void launch_fold_ring(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t
         else klaunch(k_fold_ring<false, false>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
     }
     if (build) {
-        // hottest band first: a full bucket then drops the colder ids (counts from 2^23 sampled edges)
-        // GSGPU_WARM_BANDS (A/B): number of band passes, 4 by default (3: [2, 8) in one pass, 2: [8, inf) +
-        // [2, 8): 0.17 ms per step slower, the bands' priority is worth more than their passes; 5, 6: finer)
-        static const uint32_t bands4[] = {0xFFFFFFFFu, 32u, 8u, 3u, 2u};
-        static const uint32_t bands3[] = {0xFFFFFFFFu, 32u, 8u, 2u};
-        static const uint32_t bands2[] = {0xFFFFFFFFu, 8u, 2u};
-        static const uint32_t bands5[] = {0xFFFFFFFFu, 64u, 16u, 8u, 3u, 2u};
-        static const uint32_t bands6[] = {0xFFFFFFFFu, 64u, 24u, 12u, 6u, 3u, 2u};
-        static const uint64_t nbands = env_u64("GSGPU_WARM_BANDS", 4);
-        const uint32_t* bands = nbands == 2 ? bands2 : nbands == 3 ? bands3 : nbands == 5 ? bands5 : nbands == 6 ? bands6 : bands4;
+        // hottest band first: a full bucket then drops the colder ids
         const uint32_t B = h->hot_bits;
         const uint32_t wwords = 1u << h->warm_bits;
         const uint32_t cwords = (uint32_t)((((uint64_t)1 << B) + 1) / 2);
         klaunch(k_warm_clear, dim3(grid_for(wwords, 256, 2048)), dim3(256), h->stream, nullptr, nullptr, h->warm, wwords,
                 (const uint32_t*)(h->derr + 7));
-        const int nb = (nbands >= 2 && nbands <= 6) ? (int)nbands : 4;
+        constexpr int nb = (int)(sizeof(kWarmBands) / sizeof(kWarmBands[0])) - 1;
         for (int i = 0; i < nb; ++i)
             klaunch(k_warm_build, dim3(grid_for(cwords / 4 + 1, 256, 8192)), dim3(256), h->stream, nullptr, nullptr, h->wcnt, cwords,
-                    h->warm, B, h->warm_bits, bands[i + 1], bands[i], (const uint2*)h->hot, hot.five, (const uint32_t*)h->gbits, h->derr + 7, (int)(i == nb - 1));
+                    h->warm, B, h->warm_bits, kWarmBands[i + 1], kWarmBands[i], (const uint2*)h->hot, hot.five, (const uint32_t*)h->gbits, h->derr + 7, (int)(i == nb - 1));
         klaunch(k_warm_done, dim3(1), dim3(1), h->stream, nullptr, t.stop(), h->derr + 7);
     }
 }
 
-// Young-forest launch split: while fewer than capacity/4 edges have been folded since reset,
-// the forest is being built (most edges hook) and concurrent hooks on the same few roots
-// (RMAT hubs) serialise on failed CAS retries; launches of at most kYoungChunk edges cut the
-// edges in flight and let later edges see earlier unions (RMAT-26 window 1: 6.4 -> 2.0 ms,
-// tools/exp_chunks.py). Once mature, a batch is one launch (steady windows are filter-bound).
-constexpr uint64_t kYoungChunk = 1ull << 18;
-static uint64_t young_chunk() {
-    static const uint64_t v = env_u64("GSGPU_YOUNG_CHUNK", kYoungChunk);
-    return v ? v : kYoungChunk;
-}
-// Folding a partial summary (AOS pairs: fold_pairs / the multi-GPU merge): the pairs (v, R) of one
-// component all name its root R. If R's component is not yet joined to the receiver's component of
-// the v's, every pair in flight reads the same stale roots and CASes the same word (R's or the
-// receiver's giant root): millions of same-address atomics, 5-14 ms for 6M pairs (RMAT-26 window
-// 1, tools/sim_ranks.py), where a receiver that already holds the join folds them in 0.2 ms.
-// 8 ranks' window-1 merges: 32 ms in one launch each, 2.1 ms with a 2^10 head (2^14: 2.6, 2^17: 6.5). So a
-// short head launch of GSGPU_MERGE_HEAD pairs (default 2^10) joins the big components first, then
-// the rest follow in launches of GSGPU_MERGE_CHUNK pairs (0 = one launch).
-constexpr uint64_t kMergeBulk = 1ull << 20;   // smaller batches: one launch (a delta of a mature
-                                              // summary rarely joins big components)
-static uint64_t merge_head() {
-    static const uint64_t v = env_u64("GSGPU_MERGE_HEAD", 1u << 10);
-    return v;
-}
-static uint64_t merge_chunk() {
-    static const uint64_t v = env_u64("GSGPU_MERGE_CHUNK", 0);
-    return v;
-}
-// first young launch after reset: GSGPU_YOUNG_HEAD edges, doubling per launch up to the chunk
-// (0 = chunks from the start): the hubs' first touches and joins happen with few edges in flight
-static uint64_t young_head() {
-    static const uint64_t v = env_u64("GSGPU_YOUNG_HEAD", 0);
-    return v;
-}
-static uint64_t ring_from() {
-    static const uint64_t v = env_u64("GSGPU_RING_FROM", 1);
-    return v;
-}
-
-// GSGPU_YOUNG_SPLIT=S, GSGPU_YOUNG_SPLITS=k: inside the young forest, close internally (compress
-// + giant pick: no emission, labels stay canonical) after S, 2S, .. 2^(k-1) S edges since reset,
-// so the rest of the young window folds with the giant filter on. Default: one split at
-// capacity / 16 edges where gbits outgrows L2 (ids >= 2^25; 0 = off). RMAT-26 window 1:
-// 1487 -> 1297 us for one extra full close (+118 us); splits at 2^21 or 2^23, or 3-5 doubling
-// splits, gained less (tools/young_split_sweep.sh)
-static uint64_t young_split(const gs_cc_t* h) {
-    static const uint64_t v = env_u64("GSGPU_YOUNG_SPLIT", ~0ull);
-    if (v != ~0ull) return v;
-    return h->cap >= (1u << 25) ? h->cap / 16 : 0;
-}
-static uint64_t young_splits() { static const uint64_t v = env_u64("GSGPU_YOUNG_SPLITS", 1); return v; }
+// Young-forest split points (dense ids, SoA folds): one internal close at capacity/16 edges since
+// reset where gbits outgrows L2 (ids >= 2^kRingMinBits), or at GSGPU_YOUNG_SPLIT
 static uint64_t next_young_split(const gs_cc_t* h, uint64_t done) {
-    uint64_t s = young_split(h);
-    for (uint64_t i = 0; s && i < young_splits(); ++i, s *= 2)
-        if (done < s) return s;
-    return 0;
+    uint64_t s = dbg().young_split;
+    if (s == ~0ull) s = (uint64_t)h->cap >= (1ull << std::min<uint32_t>(dbg().ring_min_bits, 63)) ? h->cap / kYoungSplitDiv : 0;
+    return (s && done < s) ? s : 0;
 }
 
 int compress_impl(gs_cc_t* h);
 
+// UpdateCC over a batch of dense ids: the ring fold once the forest is mature, else young-forest
+// launches (one per batch, cut at the young limit and at the split point, which closes internally),
+// or for partial summaries (AOS) a head launch first.
 template <typename IdT, bool AOS>
 void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, size_t esz) {
     const uint64_t young_limit = h->cap / 4;
     // mature forest (past the young limit), aligned device uint32 SoA: the steady ring fold
     if (std::is_same<IdT, uint32_t>::value && !AOS && h->hot && use_ring(h) &&
-        h->edges_since_reset >= ring_from() * young_limit && n >= 4 &&
+        h->edges_since_reset >= young_limit && n >= 4 &&
         ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0) {
         const uint64_t done = n & ~(uint64_t)3;
         launch_fold_ring(h, reinterpret_cast<const uint32_t*>(a), reinterpret_cast<const uint32_t*>(b), done);
@@ -437,28 +366,19 @@ void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, siz
     uint64_t off = 0;
     while (off < n) {
         uint64_t m = n - off;
-        if (h->edges_since_reset < young_limit) {
-            const uint64_t left = young_limit - h->edges_since_reset;
-            uint64_t c = young_persist() ? left : young_chunk();
-            if (young_head()) {          // geometric ramp: head, 2 head, 4 head, ... up to the chunk
-                uint64_t r = young_head();
-                while (r < c && 2 * r <= h->edges_since_reset + young_head()) r *= 2;
-                c = std::min(c, r);
-            }
-            m = std::min(m, std::max<uint64_t>(std::min(c, left), 1));
+        const bool young = h->edges_since_reset < young_limit;
+        uint64_t sp = 0;
+        if (young) {
+            m = std::min(m, young_limit - h->edges_since_reset);
             if (!AOS && !h->sparse) {
-                const uint64_t sp = next_young_split(h, h->edges_since_reset);
+                sp = next_young_split(h, h->edges_since_reset);
                 if (sp) m = std::min(m, sp - h->edges_since_reset);
             }
-        } else if (AOS && off == 0 && merge_head() && n > kMergeBulk) {
-            m = std::min(m, merge_head());
-        } else if (AOS && merge_chunk()) {
-            m = std::min(m, merge_chunk());
+        } else if (AOS && off == 0 && n > kMergeBulk) {
+            m = std::min(m, kMergeHead);
         }
         const size_t stride = AOS ? 2 * esz : esz;
-        launch_fold<IdT, AOS>(h, a + off * stride, b ? b + off * esz : nullptr, m,
-                              h->edges_since_reset < young_limit);
-        const uint64_t sp = (!AOS && !h->sparse && h->edges_since_reset < young_limit) ? next_young_split(h, h->edges_since_reset) : 0;
+        launch_fold<IdT, AOS>(h, a + off * stride, b ? b + off * esz : nullptr, m, young);
         h->edges_since_reset += m;
         off += m;
         if (sp && h->edges_since_reset == sp && off < n) {
@@ -474,6 +394,8 @@ SparseArgs sparse_args(gs_cc_t* h) {
 }
 
 // UpdateCC over arbitrary int64 ids (GS_CC_SPARSE_IDS), young-forest split as for dense ids
+// (young sparse folds in launches of kSparseYoungChunk edges: later edges see earlier unions)
+constexpr uint64_t kSparseYoungChunk = 1ull << 18;
 void launch_fold_sparse(gs_cc_t* h, const int64_t* a, const int64_t* b, uint64_t n, bool aos) {
     const SparseArgs sa = sparse_args(h);
     const uint64_t young_limit = h->cfg.vertex_capacity / 4;
@@ -481,7 +403,7 @@ void launch_fold_sparse(gs_cc_t* h, const int64_t* a, const int64_t* b, uint64_t
     while (off < n) {
         uint64_t m = n - off;
         if (h->edges_since_reset < young_limit)
-            m = std::min(m, std::max<uint64_t>(std::min(kYoungChunk, young_limit - h->edges_since_reset), 1));
+            m = std::min(m, std::max<uint64_t>(std::min(kSparseYoungChunk, young_limit - h->edges_since_reset), 1));
         FoldArgs f{m, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
         const unsigned grid = grid_for((m + 1) / 2, 256, 16384);
         KTimer t(h, h->fold_timer);
@@ -573,15 +495,7 @@ int compress_impl(gs_cc_t* h) {
             klaunch(k_pick_giant, dim3(1), dim3(1024), h->stream, t.start(), nullptr, (const uint32_t*)h->parent, h->cap,
                     in, (int)force);
         ++h->closes;
-        // 2048 workgroups: the incremental close is a 2M-word bitmap scan; 16384 cost 140 us more
-        // per 64-window step (tools/sweep_env.sh)
-        static const unsigned cgrid = (unsigned)std::max<uint64_t>(env_u64("GSGPU_COMPRESS_GRID", 2048), 1);
-        // closes of the young forest (<= capacity/4 edges since reset) are mostly full passes
-        // (a 4-B read per vertex + grandparent gathers): GSGPU_COMPRESS_GRID_YOUNG (A/B; 8192-65536
-        // gave the same close sum per 64-window step as 2048, tools/close_grid_sweep.sh)
-        static const unsigned ygrid = (unsigned)std::max<uint64_t>(env_u64("GSGPU_COMPRESS_GRID_YOUNG", 2048), 1);
-        const bool young = h->edges_since_reset <= (uint64_t)h->cap / 4;
-        klaunch(k_compress, dim3(grid_for(h->cap, 1024, young ? ygrid : cgrid)), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
+        klaunch(k_compress, dim3(grid_for(h->cap, 1024, kCompressGrid)), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
                 h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot);
     }
     GS_HIP(hipGetLastError());
@@ -770,14 +684,10 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
                 h->hot_cand = nullptr;
             }
             h->hot_bits = bits;
-            // warm set: only where gbits outgrows an XCD's 4 MiB L2 (ids >= 2^25; GSGPU_WARM_MIN_BITS
-            // for tests), its table L2-resident and at most 1/8 of gbits (GSGPU_WARM_BUCKETS = log2
-            // buckets of 4 B, at most 2^19 = 2 MiB; 8-bit slots need at least 2^(B-8))
-            static const bool warm_on = env_u64("GSGPU_WARM", 1) != 0;
-            static const uint32_t wmin = (uint32_t)env_u64("GSGPU_WARM_MIN_BITS", 25);
-            static const uint32_t wmax = (uint32_t)std::min<uint64_t>(env_u64("GSGPU_WARM_BUCKETS", 18), 19);
-            h->warm_bits = std::min<uint32_t>(wmax, bits - 6);
-            if (h->hot && warm_on && bits >= wmin && bits <= h->warm_bits + 8) {
+            // warm set: only where gbits outgrows an XCD's 4 MiB L2 (with the ring fold), its table
+            // L2-resident and at most 1/8 of gbits (8-bit slots need at least 2^(B-8) buckets)
+            h->warm_bits = std::min<uint32_t>(kWarmBucketsMaxBits, bits - 6);
+            if (h->hot && bits >= dbg().ring_min_bits && bits <= h->warm_bits + 8) {
                 const size_t cbytes = (size_t)((((uint64_t)1 << bits) + 1) / 2) * 4;
                 if (hipMalloc(&h->warm, (size_t)4 << h->warm_bits) != hipSuccess ||
                     hipMalloc(&h->wcnt, cbytes) != hipSuccess || hipMemsetAsync(h->wcnt, 0, cbytes, h->stream) != hipSuccess) {
@@ -839,7 +749,7 @@ int gs_cc_reset(gs_cc_t* h) {
     // hot set owner none
     GS_HIP(hipMemsetAsync(h->derr + 1, 0xFF, 5 * sizeof(uint32_t), h->stream));
     {
-        static const uint32_t budget = (uint32_t)env_u64("GSGPU_HOT_BUDGET", kHotAdmitLaunches);   // derr[6]
+        static const uint32_t budget = kHotAdmitLaunches;   // derr[6]
         GS_HIP(hipMemcpyAsync(h->derr + 6, &budget, sizeof(uint32_t), hipMemcpyHostToDevice, h->stream));
     }
     GS_HIP(hipMemsetAsync(h->derr + 7, 0, sizeof(uint32_t), h->stream));      // warm set: not built
@@ -1098,9 +1008,8 @@ int gs_cc_labels_device(gs_cc_t* h, const void** p) {
 }
 
 static int export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long* counter) {
-    // one workgroup per contiguous range of mark words: GSGPU_EXPORT_BLOCKS (<= kExportBlocks)
-    static const unsigned eb = (unsigned)std::min<uint64_t>(std::max<uint64_t>(env_u64("GSGPU_EXPORT_BLOCKS", kExportBlocks), 1), kExportBlocks);
-    const dim3 grid(grid_for((h->cap + 31) / 32, 256, eb));
+    // one workgroup per contiguous range of mark words
+    const dim3 grid(grid_for((h->cap + 31) / 32, 256, kExportBlocks));
     {
         KTimer t(h, GS_K_EXPORT);
         klaunch(k_export_count, grid, dim3(256), h->stream, t.start(), nullptr,

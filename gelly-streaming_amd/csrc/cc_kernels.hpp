@@ -180,6 +180,10 @@ struct FoldArgs {
 // Layout: 2^14 buckets x 4 slots of 16-bit remainders. With ids < 2^B (B = hot_bits, 20..29),
 // h = v * kHotMul mod 2^B (odd multiplier: a bijection), bucket = h >> (B - 14), slot value =
 // (h mod 2^(B-14)) + 1; (bucket, slot value) <-> v is one-to-one, so membership is exact. 0 = empty.
+// Exactness (and k_compress clearing the table when the giant becomes another component) is
+// needed for CORRECTNESS, not only speed: a hit stands in for v's gbits bit, a hit on both
+// endpoints drops the edge, and a hit on one endpoint makes the survivor's union start from the
+// giant root instead of parent[v] (union_group_g). The same holds for warm_probe.
 // Entries are only ever added (a 0 half-word CASed to a remainder) and every entry is a vertex
 // whose gbits bit was set, i.e. a member of the giant component; components only merge until
 // reset, so an entry stays a member while the giant is the same component (k_pick_giant clears
@@ -265,7 +269,6 @@ struct HotArgs {
     uint32_t bits;      // B: every id < 2^B
     uint32_t* cand;     // 2^kHotCandBits candidate slots
     uint64_t sample_edges = kHotSampleEdges;   // admission offers endpoints of a launch's first edges
-    uint32_t probe = 1;                        // 0: no LDS probes (A/B experiments)
     uint32_t* budget = nullptr;                // admitting launches left (device word, see below)
     uint32_t periodic = 0;                     // the host's periodic refresh: admit in this launch
     uint32_t five = 0;                         // slot format: 5 x 12 bits (B <= 26) instead of 4 x 16
@@ -276,7 +279,6 @@ struct HotArgs {
     const uint32_t* warm_valid = nullptr;      // device word: warm set built for the current giant
     uint32_t* wcnt = nullptr;                  // endpoint counters for the next warm build
     uint64_t count_edges = 0;                  // count this launch's first edges (if !*warm_valid)
-    uint32_t gflag = 1;                        // survivors' giant flags stand in for parent reads
 };
 
 // ---- warm set (L2-resident second tier) ----
@@ -365,8 +367,8 @@ __device__ __forceinline__ void filter_group(const FoldArgs& f, const uint32_t (
     uint32_t wu[EPT], wv[EPT];
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
-        hu[k] = HOT && hot.probe && hot_probe(tab, u[k], hot.bits, hot.five != 0);
-        hv[k] = HOT && hot.probe && hot_probe(tab, v[k], hot.bits, hot.five != 0);
+        hu[k] = HOT && hot_probe(tab, u[k], hot.bits, hot.five != 0);
+        hv[k] = HOT && hot_probe(tab, v[k], hot.bits, hot.five != 0);
         mu[k] = hu[k];
         mv[k] = hv[k];
     }
@@ -438,7 +440,7 @@ __device__ __forceinline__ void union_group(const FoldArgs& f, const uint32_t (&
 // in the young forest the giant root gR is hooked again and again, and every walk from a stand-in
 // gR then halves a shared word (x = a hub, or gR's own word when the walk starts at gR):
 // one same-address atomic per edge, window 1 1.3 -> 2.7 ms; taking gR itself for a root instead
-// fails every hook CAS on gR's word once it is hooked (14 ms). tools/gflag_check.sh
+// fails every hook CAS on gR's word once it is hooked (14 ms). A/B in profiles/r01_v12
 template <bool MARK, bool STATS, int EPT>
 __device__ __forceinline__ void union_group_g(const FoldArgs& f, const uint32_t (&u)[EPT], const uint32_t (&v)[EPT],
                                               const bool (&ok)[EPT], const uint32_t (&gflag)[EPT], uint32_t gR,
@@ -605,9 +607,9 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const uint32_t* __res
         for (uint32_t i = threadIdx.x; i < kHotBuckets; i += blockDim.x) tab[i] = hot.table[i];
     }
     // the root gbits were built for (= the giant's label at the last close); survivors' giant
-    // flags use it in place of a parent[] read (union_group_g). Off (kInvalid) without a filter,
-    // for ids >= 2^31 (the ring's flag bit), or with GSGPU_RING_GFLAG=0 (hot.gflag)
-    const uint32_t gR = (filt && hot.gflag && f.rc.cap <= 0x80000000u) ? f.giant[1] : kInvalid;
+    // flags use it in place of a parent[] read (union_group_g). Off (kInvalid) without a filter
+    // or for ids >= 2^31 (the ring's flag bit)
+    const uint32_t gR = (filt && f.rc.cap <= 0x80000000u) ? f.giant[1] : kInvalid;
     // admitting launch? (read before workgroup 0's decrement may land: a workgroup that reads the
     // decremented budget only skips this launch's admission, which is a heuristic anyway)
     const uint32_t budget = hot.budget ? *hot.budget : 1u;

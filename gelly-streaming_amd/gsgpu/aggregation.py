@@ -223,7 +223,10 @@ class SummaryTreeReduce(SummaryBulkAggregation):
     def _run_reference(self, stream, wins, cap) -> Iterator[DisjointSet]:
         P = self.parallelism
         pool = [self._new(cap) for _ in range(P + 1)]
-        summary: Optional[DisjointSet] = None
+        summary: Optional[DisjointSet] = None     # Merger.summary = initialVal (empty)
+        if self._restored is not None:            # restoreState: the Merger resumes from it
+            summary = pool[P]
+            summary.restore(*self._restored)
         try:
             for w in wins:
                 lo, ln = w.start, w.stop - w.start
@@ -257,8 +260,10 @@ class SummaryTreeReduce(SummaryBulkAggregation):
                 else:
                     summary = self.combine_fun.reduce(acc, summary)
                 summary.close_window()
+                self._summary = summary            # what snapshotState serialises (ListCheckpointed)
                 yield summary
         finally:
+            self._summary = None
             for d in pool:
                 d.close()
 

@@ -111,6 +111,53 @@ class Candidates:
             out.setdefault(b, {})[a] = c
         return out
 
+    # ---- checkpoint / resume (the Merger's ListCheckpointed state, SummaryAggregation.java:127-135) ----
+    def snapshot(self) -> Tuple[bool, np.ndarray, np.ndarray, np.ndarray]:
+        """(success, vertices, keys, signs): everything a Candidates serialises (Candidates.java:27)."""
+        ok = self.getSuccess()
+        if not ok:
+            e = np.empty(0, dtype=np.int64)
+            return False, e, e, np.empty(0, dtype=bool)
+        v, k, s = self.pairs()
+        return True, v, k, s
+
+    def restore(self, success, vertices, keys, signs) -> None:
+        """This summary becomes the snapshotted one: reset, then one parity edge per vertex.
+        A vertex signed false (other side than its key, which is signed true) gets the edge
+        (v, key); a vertex signed true other than the key gets an edge to a false-signed vertex
+        of its component (a connected bipartite component with two true-signed vertices has
+        one); a lone key gets its self-loop (edgeToCandidate(v, v) adds it). A failed snapshot
+        is restored as failed (Candidates.fail(): empty map) by an odd cycle on ids 0..2."""
+        self.reset()
+        if not success:
+            if self.capacity < 3:
+                raise ValueError("restoring a failed Candidates needs vertex_capacity >= 3")
+            self.fold(np.array([0, 1, 2]), np.array([1, 2, 0]))
+            return
+        v = np.asarray(vertices, dtype=np.int64)
+        k = np.asarray(keys, dtype=np.int64)
+        s = np.asarray(signs, dtype=bool)
+        if not (v.shape == k.shape == s.shape):
+            raise ValueError("restore: vertices, keys and signs differ in length")
+        if v.size == 0:
+            return
+        neg = {}                                   # component key -> one false-signed vertex
+        for a, b, c in zip(v.tolist(), k.tolist(), s.tolist()):
+            if not c:
+                neg.setdefault(b, a)
+        src, dst = [], []
+        for a, b, c in zip(v.tolist(), k.tolist(), s.tolist()):
+            if not c:
+                src.append(a); dst.append(b)
+            elif a != b:
+                if b not in neg:
+                    raise ValueError("restore: component %d has two true-signed vertices and no false one" % b)
+                src.append(a); dst.append(neg[b])
+            else:
+                src.append(a); dst.append(a)
+        self.fold(np.array(src, dtype=np.int64), np.array(dst, dtype=np.int64))
+        self.close_window()
+
     def toString(self) -> str:
         """Tuple2<Boolean, TreeMap<Long, TreeMap<Long, SignedVertex>>>.toString."""
         ok = self.getSuccess()
@@ -144,30 +191,53 @@ class BipartitenessCheck:
         self.parallelism = max(int(parallelism), 1)
         self.window_edges = window_edges
         self.mode = mode
+        self._summary: Optional[Candidates] = None     # the Merger's cumulative summary
+        self._restored = None                          # restoreState's snapshot, for the next run
+
+    # ---- Merger checkpointing (ListCheckpointed<S>, SummaryAggregation.java:127-135) ----
+    def snapshotState(self, checkpointId: int = 0, timestamp: int = 0) -> list:
+        """Collections.singletonList(summary); empty before the first emission."""
+        if self._summary is None:
+            return []
+        return [self._summary.snapshot()]
+
+    def restoreState(self, state: list) -> None:
+        """summary = list.get(0): the next run() starts its Merger from this snapshot."""
+        self._restored = state[0] if state else None
 
     def _capacity(self, stream) -> int:
         if self.vertex_capacity:
             return int(self.vertex_capacity)
-        if len(stream) == 0:
-            return 1
-        return int(max(stream.src.max(), stream.dst.max())) + 1
+        hi = 0 if len(stream) == 0 else int(max(stream.src.max(), stream.dst.max())) + 1
+        if self._restored is not None and len(self._restored[1]):
+            hi = max(hi, int(np.max(self._restored[1])) + 1)
+        if self._restored is not None and not self._restored[0]:
+            hi = max(hi, 3)                            # a failed snapshot is restored on ids 0..2
+        return max(hi, 1)
 
     def run(self, stream) -> Iterator[Candidates]:
         cap = self._capacity(stream)
         wins = stream.windows(self.time_millis, self.window_edges)
         if self.mode == "fused":
             summary = Candidates(cap, self.id_bits, self.device)
+            if self._restored is not None:
+                summary.restore(*self._restored)
+            self._summary = summary
             try:
                 for w in wins:
                     summary.fold(stream.src[w], stream.dst[w])
                     summary.close_window()
                     yield summary
             finally:
+                self._summary = None
                 summary.close()
             return
         P = self.parallelism
         pool: List[Candidates] = [Candidates(cap, self.id_bits, self.device) for _ in range(P + 1)]
         summary: Optional[Candidates] = None
+        if self._restored is not None:                 # restoreState: the Merger resumes from it
+            summary = pool[P]
+            summary.restore(*self._restored)
         try:
             for w in wins:
                 lo, ln = w.start, w.stop - w.start
@@ -183,7 +253,9 @@ class BipartitenessCheck:
                     acc = part if acc is None else acc.merge(part)       # combineFunction.reduce(c1, c2) = c1.merge(c2)
                 summary = acc if summary is None else acc.merge(summary)  # Merger: reduce(windowResult, summary)
                 summary.close_window()
+                self._summary = summary
                 yield summary
         finally:
+            self._summary = None
             for c in pool:
                 c.close()

@@ -110,3 +110,26 @@ def test_self_loops_range_and_reset():
     assert c.toString() == "(false,{})"
     c.reset()
     assert c.toString() == "(true,{})"
+
+
+@pytest.mark.parametrize("mode", ["fused", "reference"])
+@pytest.mark.parametrize("odd_at", [-1, 1500, 4200])
+def test_checkpoint_resume(mode, odd_at):
+    """snapshotState after k windows, restoreState into a NEW operator, run the rest: every later
+    emission equals the uninterrupted run's (the Merger is ListCheckpointed, SummaryAggregation.java:127-135).
+    odd_at 1500: the snapshot itself is failed; 4200: the failure comes after the restore."""
+    s, d = _bipartite_stream(2000, 6000, seed=21, odd_at=odd_at)
+    W, k = 1000, 3
+    want = [c.toString() for c in SimpleEdgeStream(s, d).aggregate(
+        BipartitenessCheck(1000, window_edges=W, mode=mode, parallelism=3, vertex_capacity=2000))]
+    op = BipartitenessCheck(1000, window_edges=W, mode=mode, parallelism=3, vertex_capacity=2000)
+    state = None
+    for w, c in enumerate(SimpleEdgeStream(s[:k * W], d[:k * W]).aggregate(op)):
+        assert c.toString() == want[w]
+        if w == k - 1:
+            state = op.snapshotState(1, 0)
+    assert state is not None and len(state) == 1
+    op2 = BipartitenessCheck(1000, window_edges=W, mode=mode, parallelism=3, vertex_capacity=2000)
+    op2.restoreState(state)
+    got = [c.toString() for c in SimpleEdgeStream(s[k * W:], d[k * W:]).aggregate(op2)]
+    assert got == want[k:]

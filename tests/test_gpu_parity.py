@@ -113,21 +113,29 @@ def test_streams_golden(case, mode, bits):
 
 # ---------------- Merger checkpoint / resume (ListCheckpointed, SummaryAggregation.java:127-135) ----------------
 @pytest.mark.parametrize("bits", [32, 64])
-@pytest.mark.parametrize("mode", ["fused", "reference"])
+@pytest.mark.parametrize("mode", ["fused", "reference", "tree"])
 @pytest.mark.parametrize("case", _streams()[:3], ids=lambda c: c["name"])
 def test_merger_checkpoint_resume(case, mode, bits):
     """Run k windows, snapshotState, restore into a NEW operator and run the rest of the stream:
-    every later emission equals the uninterrupted pipeline's (the golden labels)."""
+    every later emission equals the uninterrupted pipeline's (the golden labels). mode "tree":
+    ConnectedComponentsTree, whose output also goes through the ListCheckpointed Merger
+    (SummaryTreeReduce.java:87-90 -> SummaryAggregation.java:127-135)."""
+    from gsgpu import ConnectedComponentsTree
     W = case["window_edges"]
     nwin = case["labels"].shape[0]
     k = max(1, nwin // 2)
-    kw = dict(window_edges=W, parallelism=case["partitions"], mode=mode, id_bits=bits, vertex_capacity=case["cap"])
-    cc = ConnectedComponents(1000, **kw)
+    kw = dict(window_edges=W, id_bits=bits, vertex_capacity=case["cap"])
+    if mode == "tree":
+        make = lambda: ConnectedComponentsTree(1000, max(case["partitions"], 3), **kw)
+    else:
+        make = lambda: ConnectedComponents(1000, parallelism=case["partitions"], mode=mode, **kw)
+    cc = make()
+    state = None
     for w, ds in enumerate(SimpleEdgeStream(case["src"][:k * W], case["dst"][:k * W]).aggregate(cc)):
         if w == k - 1:
             state = cc.snapshotState(1, 0)
-    assert len(state) == 1
-    cc2 = ConnectedComponents(1000, **kw)
+    assert state is not None and len(state) == 1
+    cc2 = make()
     cc2.restoreState(state)
     w = k
     for ds in SimpleEdgeStream(case["src"][k * W:], case["dst"][k * W:]).aggregate(cc2):
@@ -505,26 +513,6 @@ def test_bench_two_ranks_one_gpu_verified(merge):
     out = subprocess.check_output(cmd, env=env, timeout=240).decode()
     line = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
-    assert line["verify"] == {"edges_consistent": True, "labels_minimal_idempotent": True, "equals_torch_cc": True}
-
-
-# ---------------- opt-in fold variants, end to end against the independent torch CC ----------------
-@pytest.mark.parametrize("env", [{"GSGPU_FOLD_MODE": "plain"}, {"GSGPU_FOLD_MODE": "ring"}, {"GSGPU_FOLD_MODE": "auto"},
-                                 {"GSGPU_WARM": "0"}, {"GSGPU_WARM_MIN_BITS": "25"},
-                                 {"GSGPU_WARM_BUCKETS": "14", "GSGPU_WARM_AT": "1", "GSGPU_WARM_EVERY": "2"},
-                                 {"GSGPU_WARM_SAMPLE": "16777216", "GSGPU_FOLD_STATS": "1"},
-                                 {"GSGPU_FOLD_MODE": "ring", "GSGPU_FOLD_STATS": "1"},
-                                 {"GSGPU_FOLD_MODE": "plain", "GSGPU_FOLD_STATS": "1"},
-                                 {"GSGPU_FOLD_MODE": "plain", "GSGPU_FOLD_EPT": "8"}, {"GSGPU_TIMING": "marker"}],
-                         ids=["plain", "ring", "auto", "warm_off", "warm_production_default", "warm_tiny_table",
-                              "warm_big_sample_stats", "ring_stats", "plain_stats", "plain_ept8", "marker_timing"])
-def test_fold_variants_verified(env):
-    import subprocess, sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    cmd = [sys.executable, os.path.join(root, "bench.py"), "--steps", "1", "--warmup", "0", "--scale", "22",
-           "--edge-factor", "16", "--window-log2", "20", "--no-cpu-baseline", "--verify"]
-    out = subprocess.check_output(cmd, env=dict(os.environ, **env), timeout=240).decode()
-    line = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
     assert line["verify"] == {"edges_consistent": True, "labels_minimal_idempotent": True, "equals_torch_cc": True}
 
 

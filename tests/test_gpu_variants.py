@@ -1,0 +1,68 @@
+"""GPU parity of the production fold selection and of each named fold variant, one subprocess per
+configuration (the library reads its debug variables once per process; csrc/cc_api.hip).
+
+* test_headline_config_production: RMAT-26 EF16, 2^24-edge windows, production defaults — windows
+  1..6 bit-exact vs the C oracle, final labels vs an independent torch CC (tests/headline_check.py).
+* test_variant_parity: every golden stream, RMAT-21, ER-21 and the giant-switch stream, per window
+  vs the C oracle, under production defaults and under each forced variant (tests/variant_check.py).
+* test_fold_variants_verified: bench.py --verify (RMAT-22, 2^20-edge windows) under each variant.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _env(extra):
+    env = {k: v for k, v in os.environ.items() if not k.startswith("GSGPU_")}
+    env.update(extra)
+    return env
+
+
+def _last_json(out: bytes):
+    return json.loads([l for l in out.decode().splitlines() if l.startswith("{")][-1])
+
+
+def test_headline_config_production():
+    out = subprocess.check_output([sys.executable, os.path.join(HERE, "headline_check.py")], env=_env({}), timeout=900)
+    r = _last_json(out)
+    print(r)
+    assert r["oracle_checksums_equal"], r
+    assert r["final_equals_torch_cc"] and r["labels_minimal_idempotent"], r
+    assert r["ok"], r
+
+
+VARIANTS = {
+    "production": {},
+    "ring_warm_split_from_2^20": {"GSGPU_RING_MIN_BITS": "20"},
+    "ring_warm_no_split": {"GSGPU_RING_MIN_BITS": "20", "GSGPU_YOUNG_SPLIT": "0"},
+    "ring_warm_stats": {"GSGPU_RING_MIN_BITS": "20", "GSGPU_FOLD_STATS": "1"},
+    "ring_forced_no_warm": {"GSGPU_FOLD_MODE": "ring"},
+    "plain_forced": {"GSGPU_FOLD_MODE": "plain", "GSGPU_RING_MIN_BITS": "20"},
+    "young_split_2^18": {"GSGPU_YOUNG_SPLIT": str(1 << 18)},
+}
+
+
+@pytest.mark.parametrize("name", list(VARIANTS))
+def test_variant_parity(name):
+    out = subprocess.check_output([sys.executable, os.path.join(HERE, "variant_check.py")], env=_env(VARIANTS[name]),
+                                  timeout=600)
+    r = _last_json(out)
+    bad = [c for c in r["cases"] if not c["ok"]]
+    assert r["ok"] and not bad, bad
+
+
+@pytest.mark.parametrize("name", ["production", "ring_warm_split_from_2^20", "plain_forced", "ring_warm_stats"])
+def test_fold_variants_verified(name):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0", "--scale", "22",
+           "--edge-factor", "16", "--window-log2", "20", "--no-cpu-baseline", "--verify"]
+    out = subprocess.check_output(cmd, env=_env(VARIANTS[name]), timeout=300)
+    line = _last_json(out)
+    assert line["verify"] == {"edges_consistent": True, "labels_minimal_idempotent": True, "equals_torch_cc": True}

@@ -1,0 +1,110 @@
+"""Per-window parity of one fold configuration against the C oracle (run as a SUBPROCESS).
+
+The library reads its debug variables (GSGPU_FOLD_MODE, GSGPU_RING_MIN_BITS, GSGPU_YOUNG_SPLIT,
+GSGPU_FOLD_STATS; csrc/cc_api.hip) once per process, so every fold variant is checked in a process
+of its own: tests/test_gpu_variants.py starts this script with one named environment and reads the
+JSON line it prints. With no variable set this is the production configuration.
+
+Streams (every one compared window by window, bit-exact, against oracle/ run with P partitions
+= the reference's SummaryBulkAggregation dataflow, SummaryBulkAggregation.java:68-90):
+  golden        the committed golden streams (tests/golden), dense labels per window
+  rmat21        RMAT scale 21, 2^24 edges, 2^20-edge windows (checksum per window + final labels)
+  er21          Erdos-Renyi n = 2^21, m = 2^22, 2^19-edge windows
+  giant_switch  two vertex blocks: a giant grows in the small block first, then a bigger one in
+                the other block takes over at a re-pick (the hot set and warm set must be
+                dropped), then both are joined — the ring path's stale-entry hazards
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (os.path.join(ROOT, "gelly-streaming_amd"), os.path.join(ROOT, "oracle")):
+    sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+
+
+def giant_switch_stream(seed: int = 11):
+    """Block A = [0, 2^19), block B = [2^20, 2^21) (ids in a 2^21 space). Windows of 2^19 edges:
+    1-8 inside A (A's giant forms and is picked), 9-24 inside B (B's giant grows to twice A's and
+    wins a re-pick), 25-28 both blocks, 29-32 both blocks plus a few A-B edges (the two giants
+    join). Self-loops and duplicates included."""
+    rng = np.random.default_rng(seed)
+    W = 1 << 19
+    A0, A1, B0, B1 = 0, 1 << 19, 1 << 20, 1 << 21
+    src, dst = [], []
+
+    def block(lo, hi, n):
+        return rng.integers(lo, hi, n), rng.integers(lo, hi, n)
+
+    for _ in range(8):
+        s, d = block(A0, A1, W); src.append(s); dst.append(d)
+    for _ in range(16):
+        s, d = block(B0, B1, W); src.append(s); dst.append(d)
+    for w in range(8):
+        sa, da = block(A0, A1, W // 2)
+        sb, db = block(B0, B1, W // 2)
+        s, d = np.concatenate([sa, sb]), np.concatenate([da, db])
+        if w >= 4:                                     # a few A-B edges
+            k = rng.integers(0, W, 16)
+            d[k] = rng.integers(B0, B1, 16)
+        s[:64] = d[:64]                                # self-loops
+        perm = rng.permutation(W)
+        src.append(s[perm]); dst.append(d[perm])
+    return np.concatenate(src).astype(np.int64), np.concatenate(dst).astype(np.int64), W, B1
+
+
+def run_case(torch, oracle, name, s, d, W, cap, partitions=4):
+    import gsgpu
+    from pyoracle import EMIT_CHECKSUM
+    want = oracle.run(s, d, W, partitions=partitions, threads=8, emit=EMIT_CHECKSUM, label_cap=cap,
+                      want_final=True)
+    ds = gsgpu.DisjointSet(cap, id_bits=32, stream=torch.cuda.current_stream())
+    ts = torch.from_numpy(s.astype(np.int32)).cuda()
+    td = torch.from_numpy(d.astype(np.int32)).cuda()
+    bad = None
+    for w, lo in enumerate(range(0, s.size, W)):
+        ds.fold(ts[lo:lo + W], td[lo:lo + W])
+        ds.close_window()
+        if ds.checksum()[0] != int(want["checksums"][w]) and bad is None:
+            bad = w
+    final_ok = bool(np.array_equal(ds.dense().astype(np.int64), want["final"]))
+    ds.close()
+    return {"case": name, "windows": int(len(want["checksums"])), "first_bad_window": bad, "final_equal": final_ok,
+            "ok": bad is None and final_ok}
+
+
+def main():
+    import torch
+    import gsgpu
+    from gsgpu import ConnectedComponents, SimpleEdgeStream
+    from pyoracle import coracle
+    assert torch.cuda.is_available()
+    oracle = coracle()
+    res = []
+    # golden streams (tests/golden, minted by the Python twin of DisjointSet.java, scipy-checked)
+    idx = json.load(open(os.path.join(HERE, "golden", "streams_index.json")))
+    z = np.load(os.path.join(HERE, "golden", "streams.npz"))
+    for c in idx:
+        n = c["name"]
+        cc = ConnectedComponents(1000, window_edges=c["window_edges"], id_bits=32, vertex_capacity=c["cap"])
+        ok = True
+        for w, ds in enumerate(SimpleEdgeStream(z[n + "__src"], z[n + "__dst"]).aggregate(cc)):
+            ok &= bool(np.array_equal(ds.dense().astype(np.int64), z[n + "__labels"][w]))
+        res.append({"case": "golden/" + n, "ok": ok})
+    s, d = oracle.gen_rmat(0, 1 << 24, 21, 5)
+    res.append(run_case(torch, oracle, "rmat21", s, d, 1 << 20, 1 << 21))
+    s, d = oracle.gen_er(0, 1 << 22, 1 << 21, 6)
+    res.append(run_case(torch, oracle, "er21", s, d, 1 << 19, 1 << 21))
+    s, d, W, cap = giant_switch_stream()
+    res.append(run_case(torch, oracle, "giant_switch", s, d, W, cap))
+    env = {k: v for k, v in os.environ.items() if k.startswith("GSGPU_")}
+    print(json.dumps({"env": env, "ok": all(r["ok"] for r in res), "cases": res}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
