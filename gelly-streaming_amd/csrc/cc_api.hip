@@ -613,6 +613,30 @@ int find_sparse(gs_cc_t* h, const int64_t* ids, int64_t* roots, uint8_t* found, 
 
 }  // namespace
 
+namespace gsgpu {
+// internal accessors for comm.hip
+struct CcInfo {
+    uint32_t cap;
+    int device;
+    hipStream_t stream;
+    bool marks;
+    bool sparse;
+};
+int cc_info(gs_cc_t* h, CcInfo* out) {
+    GS_TRY(check(h));
+    *out = CcInfo{h->cap, h->device, h->stream, h->mark_buf != nullptr, h->sparse};
+    return GS_OK;
+}
+static int export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long* counter);
+int cc_export_async(gs_cc_t* h, void* pairs, uint64_t cap, unsigned long long* dcount) {
+    GS_TRY(check(h));
+    if (!h->mark_buf || h->sparse) return fail(GS_ERR_UNSUPPORTED, "export: no marks on this handle");
+    if (cap < h->cap) return fail(GS_ERR_CAPACITY, "export: capacity %llu < vertex capacity %u", (unsigned long long)cap, h->cap);
+    DeviceGuard g(h->device);
+    return export_launch(h, pairs, cap, dcount);
+}
+}  // namespace gsgpu
+
 extern "C" {
 
 int gs_version(void) { return GSGPU_VERSION; }
@@ -1007,7 +1031,7 @@ int gs_cc_labels_device(gs_cc_t* h, const void** p) {
     return GS_OK;
 }
 
-static int export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long* counter) {
+int gsgpu::export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long* counter) {
     // one workgroup per contiguous range of mark words
     const dim3 grid(grid_for((h->cap + 31) / 32, 256, kExportBlocks));
     {

@@ -1,0 +1,486 @@
+// comm.hip — the multi-GPU CombineCC under the C ABI: gs_comm_* and gs_cc_merge_window.
+//
+// Replaces the reference's two exchanges of partial summaries (paths relative to the reference's
+// src/main/java/org/apache/flink/graph/streaming/):
+//   * the windowAll gather of every partition's window result to the parallelism-1 reduce and
+//     Merger (SummaryBulkAggregation.java:81-83, SummaryAggregation.java:106-119), and
+//   * ConnectedComponentsTree's pairwise tree, partials keyed by partition / 2 per round
+//     (SummaryTreeReduce.java:95-123).
+// One process per GPU; one RCCL communicator per rank (ncclCommInitRank from a unique id that
+// rank 0 makes and the caller distributes, the way torch.distributed or a Flink job's
+// configuration would). A partial summary crosses the wire as a DELTA: the (vertex, root) pairs
+// of every root this rank hooked since its last export (gs_cc_export_marks), 8 B per pair;
+// folding a delta (= DisjointSet.merge over its pairs, DisjointSet.java:127-131) carries every
+// component join of that rank's window into another summary.
+//
+// Transports: RCCL over xGMI (production), or an in-process group of handles on one device driven
+// by one thread per rank (gs_comm_create_local: the same exchange code, collectives done with
+// device-to-device copies ordered by HIP events and host barriers) for tests on a one-GPU box,
+// where RCCL refuses two ranks on one device.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "common.hpp"
+
+namespace gsgpu {
+// internal accessors of a summary handle (cc_api.hip)
+struct CcInfo {
+    uint32_t cap;
+    int device;
+    hipStream_t stream;
+    bool marks;
+    bool sparse;
+};
+int cc_info(gs_cc_t* h, CcInfo* out);
+int cc_export_async(gs_cc_t* h, void* pairs, uint64_t cap, unsigned long long* dcount);
+
+namespace {
+
+// pairs [n, m) of buf = copies of pair 0 (a repeated union is a no-op): fixed-size slots for the
+// all-gather
+__global__ void k_pad_pairs(uint2* __restrict__ buf, uint64_t n, uint64_t m) {
+    const uint2 p = buf[0];
+    for (uint64_t i = n + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x)
+        buf[i] = p;
+}
+
+// ---- in-process group (tests): threads on one device ----
+struct LocalGroup {
+    explicit LocalGroup(int w) : world(w), send(w, nullptr), ev(w, nullptr), done(w, nullptr), box((size_t)w * w) {}
+    int world;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    std::vector<const void*> send;
+    std::vector<hipEvent_t> ev, done;             // per rank: data ready / peers' reads done
+    struct Box {                                   // point-to-point mailbox src -> dst
+        const void* p = nullptr;
+        size_t bytes = 0;
+        hipEvent_t ready = nullptr, taken = nullptr;
+        int state = 0;                             // 0 empty, 1 posted, 2 copied
+    };
+    std::vector<Box> box;
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t g = gen;
+        if (++arrived == world) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != g; });
+        }
+    }
+};
+
+}  // namespace
+}  // namespace gsgpu
+
+using namespace gsgpu;
+
+struct gs_comm {
+    int rank = 0, world = 1, device = 0;
+    ncclComm_t nccl = nullptr;                     // RCCL transport
+    std::shared_ptr<LocalGroup> local;             // or the in-process group
+    hipEvent_t ev_ready = nullptr, ev_done = nullptr;
+    // exchange buffers (device), sized at the first merge for the handle's capacity
+    uint64_t cap_pairs = 0;
+    uint32_t* sendbuf = nullptr;                   // 2 * cap_pairs words
+    uint32_t* recvbuf = nullptr;                   // grows: world * m pairs
+    size_t recv_bytes = 0;
+    unsigned long long* dcnt = nullptr;            // [world + 1]: all-gathered counts, [world] own/received
+    unsigned long long* hcnt = nullptr;            // pinned mirror
+    bool root_marking_off = false;
+    uint64_t bytes_sent = 0, bytes_recv = 0, exchanges = 0;
+};
+
+namespace {
+
+int nccl_fail(ncclResult_t r, const char* what) {
+    return fail(GS_ERR_COMM, "%s failed: %s", what, ncclGetErrorString(r));
+}
+#define GS_NCCL(expr)                                                                        \
+    do {                                                                                     \
+        ncclResult_t r_ = (expr);                                                            \
+        if (r_ != ncclSuccess) return nccl_fail(r_, #expr);                                  \
+    } while (0)
+
+// ---- the three collective primitives the exchanges need ----
+int allgather(gs_comm_t* c, const void* send, void* recv, size_t bytes, hipStream_t s) {
+    if (c->nccl) {
+        GS_NCCL(ncclAllGather(send, recv, bytes, ncclUint8, c->nccl, s));
+        return GS_OK;
+    }
+    LocalGroup& g = *c->local;
+    GS_HIP(hipEventRecord(c->ev_ready, s));
+    g.send[c->rank] = send;
+    g.ev[c->rank] = c->ev_ready;
+    g.barrier();                                   // every rank's buffer and event published
+    for (int q = 0; q < c->world; ++q) {
+        if (q != c->rank) GS_HIP(hipStreamWaitEvent(s, g.ev[q], 0));
+        GS_HIP(hipMemcpyAsync(static_cast<char*>(recv) + (size_t)q * bytes, g.send[q], bytes, hipMemcpyDeviceToDevice, s));
+    }
+    GS_HIP(hipEventRecord(c->ev_done, s));
+    g.done[c->rank] = c->ev_done;
+    g.barrier();                                   // every rank's reads enqueued
+    for (int q = 0; q < c->world; ++q)             // a send buffer is rewritten only after the
+        if (q != c->rank) GS_HIP(hipStreamWaitEvent(s, g.done[q], 0));   // peers' reads of it
+    return GS_OK;
+}
+
+int send(gs_comm_t* c, const void* p, size_t bytes, int peer, hipStream_t s) {
+    if (c->nccl) {
+        GS_NCCL(ncclSend(p, bytes, ncclUint8, peer, c->nccl, s));
+        return GS_OK;
+    }
+    LocalGroup& g = *c->local;
+    LocalGroup::Box& b = g.box[(size_t)c->rank * c->world + peer];
+    GS_HIP(hipEventRecord(c->ev_ready, s));
+    std::unique_lock<std::mutex> lk(g.mu);
+    b.p = p;
+    b.bytes = bytes;
+    b.ready = c->ev_ready;
+    b.state = 1;
+    g.cv.notify_all();
+    g.cv.wait(lk, [&] { return b.state == 2; });   // the receiver has enqueued its copy
+    b.state = 0;
+    const hipEvent_t taken = b.taken;
+    lk.unlock();
+    if (!taken) return fail(GS_ERR_COMM, "local send of %zu bytes to rank %d: the receiver refused it", bytes, peer);
+    GS_HIP(hipStreamWaitEvent(s, taken, 0));       // p is reused only after the copy ran
+    return GS_OK;
+}
+
+int recv(gs_comm_t* c, void* p, size_t bytes, int peer, hipStream_t s) {
+    if (c->nccl) {
+        GS_NCCL(ncclRecv(p, bytes, ncclUint8, peer, c->nccl, s));
+        return GS_OK;
+    }
+    LocalGroup& g = *c->local;
+    LocalGroup::Box& b = g.box[(size_t)peer * c->world + c->rank];
+    std::unique_lock<std::mutex> lk(g.mu);
+    g.cv.wait(lk, [&] { return b.state == 1; });
+    if (b.bytes != bytes) {
+        b.taken = nullptr;
+        b.state = 2;
+        g.cv.notify_all();
+        return fail(GS_ERR_COMM, "local recv of %zu bytes from rank %d, %zu sent", bytes, peer, b.bytes);
+    }
+    GS_HIP(hipStreamWaitEvent(s, b.ready, 0));
+    GS_HIP(hipMemcpyAsync(p, b.p, bytes, hipMemcpyDeviceToDevice, s));
+    GS_HIP(hipEventRecord(c->ev_done, s));
+    b.taken = c->ev_done;
+    b.state = 2;
+    g.cv.notify_all();
+    return GS_OK;
+}
+
+struct Group {                                     // ncclGroupStart/End around p2p batches
+    gs_comm_t* c;
+    explicit Group(gs_comm_t* c_) : c(c_) { if (c->nccl) (void)ncclGroupStart(); }
+    int end() {
+        if (c->nccl) GS_NCCL(ncclGroupEnd());
+        c = nullptr;
+        return GS_OK;
+    }
+    ~Group() { if (c && c->nccl) (void)ncclGroupEnd(); }
+};
+
+int ensure(void** p, size_t* have, size_t need) {
+    if (*have >= need) return GS_OK;
+    if (*p) { GS_HIP(hipFree(*p)); *p = nullptr; *have = 0; }
+    if (hipMalloc(p, need) != hipSuccess) { (void)hipGetLastError(); return fail(GS_ERR_NOMEM, "hipMalloc(%zu) failed", need); }
+    *have = need;
+    return GS_OK;
+}
+
+int prepare(gs_comm_t* c, gs_cc_t* h, CcInfo* info) {
+    GS_TRY(cc_info(h, info));
+    if (info->sparse) return fail(GS_ERR_UNSUPPORTED, "gs_cc_merge_window: sparse-id summary (the exchange is dense-id)");
+    if (!info->marks) return fail(GS_ERR_UNSUPPORTED, "gs_cc_merge_window: handle created without GS_CC_TRACK_MARKS");
+    if (info->device != c->device) return fail(GS_ERR_INVALID, "gs_cc_merge_window: handle on device %d, communicator on %d",
+                                               info->device, c->device);
+    if (c->cap_pairs < info->cap) {
+        if (c->sendbuf) (void)hipFree(c->sendbuf);
+        c->sendbuf = nullptr;
+        if (hipMalloc(&c->sendbuf, (size_t)info->cap * 8) != hipSuccess) {
+            (void)hipGetLastError();
+            c->cap_pairs = 0;
+            return fail(GS_ERR_NOMEM, "exchange buffer of %u pairs", info->cap);
+        }
+        c->cap_pairs = info->cap;
+    }
+    return GS_OK;
+}
+
+// Folds deltas laid out in slots of m pairs (slot q: counts[q] real pairs, then copies of its
+// first pair; skip[q] = do not fold). While the deltas are big (young windows: components not yet
+// joined) each slot is its own fold call, whose short head launch makes the big joins first
+// (cc_api.hip kMergeHead); otherwise runs of slots go in one call.
+constexpr uint64_t kBulkDeltaPairs = 1ull << 21;
+int fold_slots(gs_cc_t* h, const uint32_t* buf, uint64_t m, const std::vector<uint64_t>& cnt, const std::vector<char>& skip) {
+    const int P = (int)cnt.size();
+    uint64_t mx = 0;
+    for (int q = 0; q < P; ++q) if (!skip[q]) mx = std::max(mx, cnt[q]);
+    if (mx == 0) return GS_OK;
+    if (mx > kBulkDeltaPairs) {
+        for (int q = 0; q < P; ++q)
+            if (!skip[q] && cnt[q]) GS_TRY(gs_cc_fold_pairs32(h, buf + 2 * (uint64_t)q * m, cnt[q]));
+        return GS_OK;
+    }
+    int q = 0;
+    while (q < P) {
+        if (skip[q] || cnt[q] == 0) { ++q; continue; }
+        int e = q;
+        while (e + 1 < P && !skip[e + 1] && cnt[e + 1]) ++e;
+        const uint64_t npairs = (uint64_t)(e - q) * m + cnt[e];     // the last slot: its real pairs only
+        GS_TRY(gs_cc_fold_pairs32(h, buf + 2 * (uint64_t)q * m, npairs));
+        q = e + 1;
+    }
+    return GS_OK;
+}
+
+// Replicated global summary: every rank folds the others' deltas, so every rank's giant filter is
+// the global one and its next delta holds only connectivity new to the whole job.
+int merge_allgather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
+    const int P = c->world;
+    hipStream_t s = in.stream;
+    GS_TRY(cc_export_async(h, c->sendbuf, c->cap_pairs, c->dcnt + P));
+    GS_TRY(allgather(c, c->dcnt + P, c->dcnt, sizeof(unsigned long long), s));
+    GS_HIP(hipMemcpyAsync(c->hcnt, c->dcnt, P * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    GS_HIP(hipStreamSynchronize(s));               // the slot size is the largest delta
+    std::vector<uint64_t> cnt(P);
+    uint64_t m = 0;
+    for (int q = 0; q < P; ++q) { cnt[q] = c->hcnt[q]; m = std::max(m, cnt[q]); }
+    if (m) {
+        const uint64_t n = cnt[c->rank];
+        if (n && n < m)
+            hipLaunchKernelGGL(k_pad_pairs, dim3((unsigned)std::min<uint64_t>((m - n + 255) / 256, 4096)), dim3(256), 0, s,
+                               reinterpret_cast<uint2*>(c->sendbuf), n, m);
+        GS_HIP(hipGetLastError());
+        GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)P * m * 8));
+        GS_TRY(allgather(c, c->sendbuf, c->recvbuf, m * 8, s));
+        std::vector<char> skip(P, 0);
+        skip[c->rank] = 1;
+        GS_TRY(gs_cc_set_marking(h, 0));           // the others' deltas are theirs to export
+        const int rc = fold_slots(h, c->recvbuf, m, cnt, skip);
+        GS_TRY(gs_cc_set_marking(h, 1));
+        GS_TRY(rc);
+        c->bytes_sent += m * 8 * (P - 1);
+        c->bytes_recv += m * 8 * (P - 1);
+    }
+    return gs_cc_close_window(h);
+}
+
+// windowAll: every other rank sends its delta straight to rank 0 (the Merger), which folds them
+// all and emits; the other ranks only close their own summaries (their giant filters).
+int merge_gather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
+    const int P = c->world;
+    hipStream_t s = in.stream;
+    if (c->rank != 0) {
+        GS_TRY(cc_export_async(h, c->sendbuf, c->cap_pairs, c->dcnt + P));
+        GS_HIP(hipMemcpyAsync(c->hcnt + P, c->dcnt + P, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+        GS_HIP(hipStreamSynchronize(s));
+        const uint64_t n = c->hcnt[P];
+        GS_TRY(send(c, c->dcnt + P, sizeof(unsigned long long), 0, s));
+        if (n) GS_TRY(send(c, c->sendbuf, n * 8, 0, s));
+        c->bytes_sent += n * 8;
+        return gs_cc_close_window(h);
+    }
+    if (!c->root_marking_off) {                    // rank 0 never exports
+        GS_TRY(gs_cc_set_marking(h, 0));
+        c->root_marking_off = true;
+    }
+    {
+        Group g(c);
+        for (int q = 1; q < P; ++q) GS_TRY(recv(c, c->dcnt + q, sizeof(unsigned long long), q, s));
+        GS_TRY(g.end());
+    }
+    GS_HIP(hipMemcpyAsync(c->hcnt, c->dcnt, P * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    GS_HIP(hipStreamSynchronize(s));
+    std::vector<uint64_t> cnt(P, 0);
+    uint64_t total = 0, mx = 0;
+    for (int q = 1; q < P; ++q) { cnt[q] = c->hcnt[q]; total += cnt[q]; mx = std::max(mx, cnt[q]); }
+    if (total) {
+        GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)total * 8));
+        {
+            Group g(c);
+            uint64_t off = 0;
+            for (int q = 1; q < P; ++q) {
+                if (cnt[q]) GS_TRY(recv(c, c->recvbuf + 2 * off, cnt[q] * 8, q, s));
+                off += cnt[q];
+            }
+            GS_TRY(g.end());
+        }
+        if (mx > kBulkDeltaPairs) {                // big deltas one call each (head launch first)
+            uint64_t off = 0;
+            for (int q = 1; q < P; ++q) {
+                if (cnt[q]) GS_TRY(gs_cc_fold_pairs32(h, c->recvbuf + 2 * off, cnt[q]));
+                off += cnt[q];
+            }
+        } else {
+            GS_TRY(gs_cc_fold_pairs32(h, c->recvbuf, total));
+        }
+        c->bytes_recv += total * 8;
+    }
+    return gs_cc_close_window(h);
+}
+
+// ConnectedComponentsTree's pairwise rounds (SummaryTreeReduce.enhance): in round r (step 2^r)
+// rank i + step sends its delta to rank i (i % 2^(r+1) == 0), which folds it with marking on (it
+// forwards what it gained in a later round). After ceil(log2 P) rounds rank 0 holds every edge.
+int merge_tree(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
+    const int P = c->world;
+    hipStream_t s = in.stream;
+    if (c->rank == 0 && !c->root_marking_off) {
+        GS_TRY(gs_cc_set_marking(h, 0));
+        c->root_marking_off = true;
+    }
+    for (int step = 1; step < P; step *= 2) {
+        if (c->rank % (2 * step) == step) {        // sender: done for this window after this
+            GS_TRY(cc_export_async(h, c->sendbuf, c->cap_pairs, c->dcnt + P));
+            GS_HIP(hipMemcpyAsync(c->hcnt + P, c->dcnt + P, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+            GS_HIP(hipStreamSynchronize(s));
+            const uint64_t n = c->hcnt[P];
+            const int peer = c->rank - step;
+            GS_TRY(send(c, c->dcnt + P, sizeof(unsigned long long), peer, s));
+            if (n) GS_TRY(send(c, c->sendbuf, n * 8, peer, s));
+            c->bytes_sent += n * 8;
+            break;
+        }
+        if (c->rank % (2 * step) == 0 && c->rank + step < P) {
+            const int peer = c->rank + step;
+            GS_TRY(recv(c, c->dcnt, sizeof(unsigned long long), peer, s));
+            GS_HIP(hipMemcpyAsync(c->hcnt, c->dcnt, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+            GS_HIP(hipStreamSynchronize(s));
+            const uint64_t n = c->hcnt[0];
+            if (n) {
+                GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)n * 8));
+                GS_TRY(recv(c, c->recvbuf, n * 8, peer, s));
+                GS_TRY(gs_cc_fold_pairs32(h, c->recvbuf, n));
+            }
+            c->bytes_recv += n * 8;
+        }
+    }
+    return gs_cc_close_window(h);
+}
+
+int alloc_common(gs_comm_t* c) {
+    if (hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess ||
+        hipMalloc(&c->dcnt, (c->world + 1) * sizeof(unsigned long long)) != hipSuccess ||
+        hipHostMalloc(&c->hcnt, (c->world + 1) * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(GS_ERR_NOMEM, "communicator scratch allocation failed");
+    }
+    GS_HIP(hipMemset(c->dcnt, 0, (c->world + 1) * sizeof(unsigned long long)));
+    return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_comm_unique_id(void* id, uint64_t id_bytes) {
+    if (!id || id_bytes < sizeof(ncclUniqueId)) return fail(GS_ERR_INVALID, "gs_comm_unique_id: need %zu bytes", sizeof(ncclUniqueId));
+    ncclUniqueId u;
+    GS_NCCL(ncclGetUniqueId(&u));
+    memcpy(id, &u, sizeof(u));
+    return GS_OK;
+}
+
+int gs_comm_create(gs_comm_t** out, const void* unique_id, int rank, int world, int device) {
+    if (!out || !unique_id) return fail(GS_ERR_INVALID, "gs_comm_create: null argument");
+    *out = nullptr;
+    if (world < 1 || rank < 0 || rank >= world) return fail(GS_ERR_INVALID, "gs_comm_create: rank %d of %d", rank, world);
+    DeviceGuard g(device);
+    if (!g.ok) return fail(GS_ERR_HIP, "gs_comm_create: hipSetDevice(%d) failed", device);
+    std::unique_ptr<gs_comm_t> c(new gs_comm_t());
+    c->rank = rank;
+    c->world = world;
+    c->device = device;
+    GS_TRY(alloc_common(c.get()));
+    ncclUniqueId u;
+    memcpy(&u, unique_id, sizeof(u));
+    const ncclResult_t r = ncclCommInitRank(&c->nccl, world, u, rank);
+    if (r != ncclSuccess) {
+        c->nccl = nullptr;
+        const int rc = nccl_fail(r, "ncclCommInitRank");
+        gs_comm_destroy(c.release());
+        return rc;
+    }
+    *out = c.release();
+    return GS_OK;
+}
+
+int gs_comm_create_local(gs_comm_t** comms, int world, int device) {
+    if (!comms || world < 1) return fail(GS_ERR_INVALID, "gs_comm_create_local: bad arguments");
+    DeviceGuard g(device);
+    if (!g.ok) return fail(GS_ERR_HIP, "gs_comm_create_local: hipSetDevice(%d) failed", device);
+    auto grp = std::make_shared<LocalGroup>(world);
+    for (int r = 0; r < world; ++r) comms[r] = nullptr;
+    for (int r = 0; r < world; ++r) {
+        gs_comm_t* c = new gs_comm_t();
+        c->rank = r;
+        c->world = world;
+        c->device = device;
+        c->local = grp;
+        comms[r] = c;
+        const int rc = alloc_common(c);
+        if (rc != GS_OK) {
+            for (int q = 0; q <= r; ++q) { gs_comm_destroy(comms[q]); comms[q] = nullptr; }
+            return rc;
+        }
+    }
+    return GS_OK;
+}
+
+int gs_comm_destroy(gs_comm_t* c) {
+    if (!c) return GS_OK;
+    DeviceGuard g(c->device);
+    (void)hipDeviceSynchronize();
+    if (c->nccl) (void)ncclCommDestroy(c->nccl);
+    if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
+    if (c->ev_done) (void)hipEventDestroy(c->ev_done);
+    if (c->sendbuf) (void)hipFree(c->sendbuf);
+    if (c->recvbuf) (void)hipFree(c->recvbuf);
+    if (c->dcnt) (void)hipFree(c->dcnt);
+    if (c->hcnt) (void)hipHostFree(c->hcnt);
+    delete c;
+    return GS_OK;
+}
+
+int gs_comm_info(gs_comm_t* c, int* rank, int* world, uint64_t* bytes_sent, uint64_t* bytes_recv, uint64_t* exchanges) {
+    if (!c) return fail(GS_ERR_INVALID, "null communicator");
+    if (rank) *rank = c->rank;
+    if (world) *world = c->world;
+    if (bytes_sent) *bytes_sent = c->bytes_sent;
+    if (bytes_recv) *bytes_recv = c->bytes_recv;
+    if (exchanges) *exchanges = c->exchanges;
+    return GS_OK;
+}
+
+int gs_cc_merge_window(gs_cc_t* h, gs_comm_t* c, int mode) {
+    if (!h || !c) return fail(GS_ERR_INVALID, "gs_cc_merge_window: null argument");
+    CcInfo in;
+    GS_TRY(prepare(c, h, &in));
+    DeviceGuard g(in.device);
+    int rc;
+    switch (mode) {
+    case GS_MERGE_ALLGATHER: rc = merge_allgather(c, h, in); break;
+    case GS_MERGE_GATHER: rc = merge_gather(c, h, in); break;
+    case GS_MERGE_TREE: rc = merge_tree(c, h, in); break;
+    default: return fail(GS_ERR_INVALID, "gs_cc_merge_window: mode %d", mode);
+    }
+    if (rc == GS_OK) ++c->exchanges;
+    return rc;
+}
+
+}  // extern "C"

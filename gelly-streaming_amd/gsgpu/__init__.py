@@ -7,6 +7,7 @@ from .summary import DisjointSet, UpdateCC, CombineCC, combine_cc  # noqa: F401
 from .aggregation import (SimpleEdgeStream, SummaryBulkAggregation, ConnectedComponents,  # noqa: F401
                           SummaryTreeReduce, ConnectedComponentsTree)
 from .bipartite import Candidates, BipartitenessCheck  # noqa: F401
+from .comm import Comm  # noqa: F401
 
 __all__ = ["DisjointSet", "UpdateCC", "CombineCC", "combine_cc", "SimpleEdgeStream",
            "SummaryBulkAggregation", "ConnectedComponents", "SummaryTreeReduce", "ConnectedComponentsTree",

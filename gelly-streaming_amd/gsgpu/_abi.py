@@ -21,16 +21,18 @@ GS_ERR_NOMEM = -4
 GS_ERR_STATE = -5
 GS_ERR_UNSUPPORTED = -6
 GS_ERR_CAPACITY = -7
+GS_ERR_COMM = -8
 
 GS_CC_TRACK_MARKS = 1
 GS_CC_SPARSE_IDS = 2
 
 GS_K_FOLD, GS_K_COMPRESS, GS_K_MERGE, GS_K_EXPORT = 0, 1, 2, 3
+GS_MERGE_ALLGATHER, GS_MERGE_GATHER, GS_MERGE_TREE = 0, 1, 2
 GS_TIMING_MASK = 0x100
 
 _ERRNAMES = {GS_ERR_INVALID: "INVALID", GS_ERR_HIP: "HIP", GS_ERR_RANGE: "RANGE",
              GS_ERR_NOMEM: "NOMEM", GS_ERR_STATE: "STATE", GS_ERR_UNSUPPORTED: "UNSUPPORTED",
-             GS_ERR_CAPACITY: "CAPACITY"}
+             GS_ERR_CAPACITY: "CAPACITY", GS_ERR_COMM: "COMM"}
 
 # every symbol include/gsgpu.h declares (tests check the library exports all of them)
 EXPORTED_SYMBOLS = (
@@ -42,6 +44,8 @@ EXPORTED_SYMBOLS = (
     "gs_bip_create", "gs_bip_destroy", "gs_bip_reset", "gs_bip_set_stream", "gs_bip_sync", "gs_bip_fold",
     "gs_bip_fold_pairs", "gs_bip_merge", "gs_bip_close_window", "gs_bip_status", "gs_bip_checksum",
     "gs_bip_emit_pairs",
+    "gs_comm_unique_id", "gs_comm_create", "gs_comm_create_local", "gs_comm_destroy", "gs_comm_info",
+    "gs_cc_merge_window",
     "gs_last_error", "gs_version",
 )
 
@@ -118,6 +122,12 @@ def lib() -> ctypes.CDLL:
         "gs_bip_status": [vp, P(i32), P(u64), P(u64)],
         "gs_bip_checksum": [vp, P(u64), P(i32), P(u64), P(u64)],
         "gs_bip_emit_pairs": [vp, vp, vp, vp, u64, P(u64)],
+        "gs_comm_unique_id": [vp, u64],
+        "gs_comm_create": [P(vp), vp, i32, i32, i32],
+        "gs_comm_create_local": [P(vp), i32, i32],
+        "gs_comm_destroy": [vp],
+        "gs_comm_info": [vp, P(i32), P(i32), P(u64), P(u64), P(u64)],
+        "gs_cc_merge_window": [vp, vp, i32],
     }
     for name, args in sig.items():
         f = getattr(L, name)

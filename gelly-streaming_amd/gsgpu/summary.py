@@ -191,6 +191,12 @@ class DisjointSet:
         """Merger step: compress so every label is the canonical (min-id) root."""
         call("gs_cc_close_window", self.handle)
 
+    def merge_window(self, comm, mode: str = "allgather") -> None:
+        """Multi-GPU CombineCC of this window (gs_cc_merge_window): exchange this rank's partial
+        summary over ``comm`` (gsgpu.comm.Comm) and close the window. Needs track_marks=True."""
+        from .comm import MODES
+        call("gs_cc_merge_window", self.handle, comm.handle, MODES[mode])
+
     def stats(self) -> Tuple[int, int]:
         nv, nc = U64(), U64()
         call("gs_cc_stats", self.handle, ctypes.byref(nv), ctypes.byref(nc))

@@ -51,7 +51,8 @@ enum {
     GS_ERR_NOMEM = -4,        /* device allocation failed                               */
     GS_ERR_STATE = -5,        /* call not valid in the handle's current state           */
     GS_ERR_UNSUPPORTED = -6,  /* feature not built / not enabled on this handle         */
-    GS_ERR_CAPACITY = -7      /* output buffer too small                                */
+    GS_ERR_CAPACITY = -7,     /* output buffer too small                                */
+    GS_ERR_COMM = -8          /* collective / communicator failure (RCCL)               */
 };
 
 /* gs_cc_config.flags */
@@ -140,6 +141,32 @@ int gs_cc_export_marks_async(gs_cc_t* h, void* pairs, uint64_t cap, void* dev_co
 /* Pause (on = 0) / resume (on = 1) marking on a GS_CC_TRACK_MARKS handle: folds while paused leave
  * no marks (a replica folding the other ranks' partial summaries must not re-export them). */
 int gs_cc_set_marking(gs_cc_t* h, int on);
+
+/* ---- multi-GPU CombineCC (windowAll / tree reduce of partial summaries), csrc/comm.hip ----
+ * One process (or thread) per GPU, one gs_comm_t per rank. Replaces the windowAll gather of the
+ * partitions' window results (SummaryBulkAggregation.java:81-83) and ConnectedComponentsTree's
+ * pairwise rounds (SummaryTreeReduce.java:95-123) with RCCL collectives over xGMI.
+ *   gs_comm_unique_id   rank 0 makes the 128-byte RCCL unique id; the caller hands it to every
+ *                       rank (torch.distributed broadcast, the job configuration, ...)
+ *   gs_comm_create      every rank, concurrently: ncclCommInitRank(world, id, rank) on `device`
+ *   gs_comm_create_local  `world` communicators of ONE process and device, one thread per rank
+ *                       (tests of the exchange on a one-GPU box: RCCL refuses two ranks on one device)
+ *   gs_cc_merge_window  after folding this rank's slice of a window: exchange this window's
+ *                       partial summary (the handle needs GS_CC_TRACK_MARKS) and close the window.
+ *     GS_MERGE_ALLGATHER  every rank keeps the GLOBAL summary (all-gather of deltas; every rank's
+ *                         emission is the Merger's)
+ *     GS_MERGE_GATHER     windowAll: deltas to rank 0, which folds them and emits
+ *     GS_MERGE_TREE       log2(P) pairwise rounds to rank 0 (SummaryTreeReduce.enhance)
+ *   Every rank must call it once per window with the same mode. It synchronises the handle's
+ *   stream once per window (delta sizes). In GATHER / TREE only rank 0's emission is the job's. */
+typedef struct gs_comm gs_comm_t;
+enum { GS_MERGE_ALLGATHER = 0, GS_MERGE_GATHER = 1, GS_MERGE_TREE = 2 };
+int gs_comm_unique_id(void* id, uint64_t id_bytes);
+int gs_comm_create(gs_comm_t** out, const void* unique_id, int rank, int world, int device);
+int gs_comm_create_local(gs_comm_t** comms, int world, int device);
+int gs_comm_destroy(gs_comm_t* comm);
+int gs_comm_info(gs_comm_t* comm, int* rank, int* world, uint64_t* bytes_sent, uint64_t* bytes_recv, uint64_t* exchanges);
+int gs_cc_merge_window(gs_cc_t* h, gs_comm_t* comm, int mode);
 
 /* ---- instrumentation ----
  * kernel ids: 0 fold, 1 compress (close_window), 2 merge, 3 export. */
