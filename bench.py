@@ -1,14 +1,23 @@
 """bench.py — streaming Connected Components edges/s on MI355X (+ % of the HBM roofline).
 
-Workload (BASELINE.json metric "streaming CC edges/sec (RMAT-26) at 1/2/4/8 MI355X"):
-  RMAT scale 26 (Graph500 a,b,c,d = .57,.19,.19,.05, ids scrambled), edge factor 16 per GPU:
-  every rank folds 2^30 edges of the counter-based stream (int32 ids, generated in HBM before the
-  timed region) in 64 windows of 2^24 edges; after each window the partial summaries are merged
-  (rank 0 = Merger: log2(P) pairwise tree over RCCL, gsgpu/tree.py) and rank 0 closes the window
-  (full compression = the canonical per-window emission, resident in HBM).
-  Weak scaling: at P GPUs the stream has P*2^30 edges over the same 2^26-vertex space; window w of
-  the global stream is P*2^24 edges, rank r owns slice r of it.
+Workload (BASELINE.json metric "streaming CC edges/sec (RMAT-26) at 1/2/4/8 MI355X", configs[2]):
+  RMAT scale 26 (Graph500 a,b,c,d = .57,.19,.19,.05, ids scrambled), edge factor 16: ONE stream of
+  2^30 edges (seed 1) in 64 global windows of 2^24 edges; after each window the partial summaries
+  are merged (CombineCC) and the window is closed (full compression = the canonical per-window
+  emission, resident in HBM). Inputs are generated in HBM by the counter-based generator before the
+  timed region.
+  --scaling strong (default): the stream is fixed; rank r of P folds slice r of every global window
+      (2^24 / P edges: the PartitionMapper split of each window, SummaryBulkAggregation.java:76-80,
+      93-106), so each GPU holds E/P edges.
+  --scaling weak: every rank folds 2^30 edges; global window = P x 2^24 edges of a P x 2^30 stream.
+  N > 1: the exchange runs under the C ABI (gs_cc_merge_window over RCCL, csrc/comm.hip) with
+  --dist-backend nccl; --dist-backend gloo runs the Python exchange (gsgpu/tree.py) over host
+  staging, for several ranks on one GPU.
 One step = one whole pass over the stream from an empty summary (reset included).
+
+Other lines (not the headline): --workload c2 | c4 | c5 | c3_single (the whole stream as one
+window), --id-bits 64 (the reference's Long ids), --host-input (edges in pinned host memory: the
+PCIe-inclusive rate of gs_cc_fold's staged path).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under torch.distributed.run.
 Rank 0 prints one JSON line.
@@ -29,11 +38,16 @@ import torch.distributed as dist  # noqa: E402
 
 import gsgpu  # noqa: E402
 from gsgpu import gen  # noqa: E402
-from gsgpu._abi import GS_K_COMPRESS, GS_K_EXPORT, GS_K_FOLD, GS_K_MERGE, GS_TIMING_MASK  # noqa: E402
+from gsgpu._abi import GS_K_COMPRESS, GS_K_EXPORT, GS_K_FOLD, GS_K_MERGE, GS_K_RING, GS_TIMING_MASK  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "streaming CC edges/sec (RMAT-26) at 1/2/4/8 MI355X + % of HBM roofline"
-BYTES_PER_EDGE_ALG = 16        # 8 B edge read + 2 x 4 B parent reads
+# SURVEY.md §8(d) / BASELINE.md: per edge 8 B edge read + 2 x 4 B parent reads (int32 ids; x2 for
+# int64), per window 4 B (8 B) canonical label write per seen vertex
+WORKLOADS = {  # name: (generator, scale or n, edge factor, window log2, seed)
+    "c3": ("rmat", 26, 16, 24, 1), "c3_single": ("rmat", 26, 16, 30, 1),
+    "c2": ("rmat", 20, 16, 20, 1), "c4": ("er", 24, 1, 20, 2), "c5": ("rmat", 24, 16, 16, 3),
+}
 
 
 def parse():
@@ -41,30 +55,55 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scale", type=int, default=26)
-    ap.add_argument("--edge-factor", type=int, default=16)
-    ap.add_argument("--window-log2", type=int, default=24)
-    ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5"],
-                    help="c3 (default, the headline): RMAT-26 EF16 per GPU, 2^24-edge windows; "
-                         "c2: RMAT-20 EF16, 2^20-edge windows; c4: Erdos-Renyi n=m=2^24, 2^20-edge windows; "
-                         "c5: RMAT-24 EF16, 2^16-edge windows, per-window emission latency p50/p99")
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS),
+                    help="c3 (default, the headline): RMAT-26 EF16, 2^24-edge windows; c3_single: the same "
+                         "stream as one window; c2: RMAT-20 EF16, 2^20-edge windows; c4: Erdos-Renyi n=m=2^24, "
+                         "2^20-edge windows; c5: RMAT-24 EF16, 2^16-edge windows + per-window emission latency")
+    ap.add_argument("--scale", type=int, default=None, help="override the workload's RMAT scale")
+    ap.add_argument("--edge-factor", type=int, default=None)
+    ap.add_argument("--window-log2", type=int, default=None, help="global window = 2^this edges")
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+    ap.add_argument("--id-bits", type=int, default=32, choices=[32, 64])
+    ap.add_argument("--host-input", action="store_true",
+                    help="edges in pinned host memory, folded through gs_cc_fold's staged H2D path")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-edges", type=int, default=1 << 25,
-                    help="cpu_baseline sample: the first this-many edges (whole windows) of the same stream")
     ap.add_argument("--verify", action="store_true", help="check final labels with an independent torch CC "
                     "(multi-rank: rank 0 regenerates the whole global stream; small scales only)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="nccl = RCCL over xGMI (production); gloo = host-staged, for testing the "
-                         "multi-rank path with several ranks on one GPU")
+                    help="nccl = the C-ABI exchange over RCCL/xGMI (production); gloo = the Python exchange "
+                         "over host staging (several ranks on one GPU, tests)")
     ap.add_argument("--merge", default="allgather", choices=["allgather", "gather", "tree"],
-                    help="multi-rank CombineCC: allgather = replicated global summary, all-pairs delta exchange "
-                         "(fastest, tools/sim_ranks.py); gather = flat windowAll gather to rank 0 (ConnectedComponents, "
-                         "SummaryBulkAggregation.java:81); tree = log2(P) pairwise rounds (ConnectedComponentsTree, "
-                         "SummaryTreeReduce.java:95-123)")
+                    help="multi-rank CombineCC: allgather = replicated global summary (every rank folds every "
+                         "delta); gather = windowAll gather to rank 0 (SummaryBulkAggregation.java:81); tree = "
+                         "log2(P) pairwise rounds (SummaryTreeReduce.java:95-123)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "fold_traffic.json"),
-                    help="PMC-derived HBM bytes per fold launch (written by profiles/pmc_traffic.py)")
-    return ap.parse_args()
+                    help="PMC-derived HBM bytes per k_fold_ring launch (profiles/pmc_traffic.py)")
+    a = ap.parse_args()
+    kind, scale, ef, wl, seed = WORKLOADS[a.workload]
+    a.kind = kind
+    a.scale = scale if a.scale is None else a.scale
+    a.edge_factor = ef if a.edge_factor is None else a.edge_factor
+    a.window_log2 = wl if a.window_log2 is None else a.window_log2
+    a.seed = seed if a.seed is None else a.seed
+    return a
+
+
+def layout(a, world: int, rank: int):
+    """(edges this rank folds, its slice per window, global window, windows, global stream edges)."""
+    E = a.edge_factor << a.scale
+    if a.scaling == "strong":
+        W_glob = min(1 << a.window_log2, E)
+        if W_glob % world:
+            raise SystemExit("global window %d does not split over %d ranks" % (W_glob, world))
+        W_rank = W_glob // world
+        nwin = (E + W_glob - 1) // W_glob
+        if E % W_glob:
+            raise SystemExit("stream of %d edges is not a whole number of %d-edge windows" % (E, W_glob))
+        return nwin * W_rank, W_rank, W_glob, nwin, E
+    W_rank = min(1 << a.window_log2, E)
+    nwin = (E + W_rank - 1) // W_rank
+    return E, W_rank, W_rank * world, nwin, E * world
 
 
 def main():
@@ -84,59 +123,65 @@ def main():
     if a.gpus != world and rank == 0:
         print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (a.gpus, world), file=sys.stderr)
 
-    if a.workload != "c3":                     # BASELINE.json configs other than the headline
-        a.scale, a.edge_factor, a.window_log2, a.seed = {
-            "c2": (20, 16, 20, 1), "c4": (24, 1, 20, 2), "c5": (24, 16, 16, 3)}[a.workload]
-    V = 1 << a.scale
-    E_rank = a.edge_factor << a.scale
-    W_rank = min(1 << a.window_log2, E_rank)
-    nwin = (E_rank + W_rank - 1) // W_rank
-    W_glob = W_rank * world
+    V = (1 << a.scale) if a.kind == "rmat" else (1 << a.scale)
+    E_rank, W_rank, W_glob, nwin, E_glob = layout(a, world, rank)
+    idt = torch.int32 if a.id_bits == 32 else torch.int64
 
-    # ---- inputs resident in HBM before timing ----
-    src = torch.empty(E_rank, dtype=torch.int32, device=dev)
-    dst = torch.empty(E_rank, dtype=torch.int32, device=dev)
+    # ---- inputs resident in HBM (or pinned host memory) before timing ----
+    src = torch.empty(E_rank, dtype=idt, device=dev)
+    dst = torch.empty(E_rank, dtype=idt, device=dev)
     for w in range(nwin):
-        lo = w * W_rank
-        n = min(W_rank, E_rank - lo)
-        if a.workload == "c4":
-            gen.erdos_renyi(src[lo:lo + n], dst[lo:lo + n], w * W_glob + rank * W_rank, V, a.seed)
+        lo, first = w * W_rank, w * W_glob + rank * W_rank
+        if a.kind == "er":
+            gen.erdos_renyi(src[lo:lo + W_rank], dst[lo:lo + W_rank], first, V, a.seed)
         else:
-            gen.rmat(src[lo:lo + n], dst[lo:lo + n], w * W_glob + rank * W_rank, a.scale, a.seed)
+            gen.rmat(src[lo:lo + W_rank], dst[lo:lo + W_rank], first, a.scale, a.seed)
     torch.cuda.synchronize()
+    if a.host_input:
+        hsrc, hdst = src.cpu().pin_memory(), dst.cpu().pin_memory()
+        fsrc, fdst = hsrc, hdst
+    else:
+        fsrc, fdst = src, dst
 
     stream = torch.cuda.current_stream()
-    marks = world > 1 and (a.merge == "allgather" or rank != 0)
-    ds = gsgpu.DisjointSet(V, id_bits=32, device=local, track_marks=marks, stream=stream)
-    tree = None
-    if world > 1:
+    marks = world > 1 and (a.merge == "allgather" or a.dist_backend == "nccl" or rank != 0)
+    ds = gsgpu.DisjointSet(V, id_bits=a.id_bits, device=local, track_marks=marks, stream=stream)
+    comm = tree = None
+    if world > 1 and a.dist_backend == "nccl":
+        comm = gsgpu.Comm.from_process_group(local)                  # C ABI: gs_comm_create (RCCL)
+    elif world > 1:
         from gsgpu.tree import AllgatherMerge, GatherMerge, TreeMerge
         cls = {"allgather": AllgatherMerge, "gather": GatherMerge, "tree": TreeMerge}[a.merge]
         tree = cls(ds, capacity_pairs=V, device=dev)
-    gather = world > 1 and a.merge == "gather"
+    gather = tree is not None and a.merge == "gather"
+
+    def window(w, after=None):
+        lo = w * W_rank
+        if gather:
+            tree.before_fold()
+        ds.fold(fsrc[lo:lo + W_rank], fdst[lo:lo + W_rank])
+        if comm is not None:
+            ds.merge_window(comm, a.merge)
+        elif tree is not None:
+            tree.merge_window()
+        else:
+            ds.close_window()
 
     def step():
         ds.reset()
         for w in range(nwin):
-            lo = w * W_rank
-            if gather:
-                tree.before_fold()
-            ds.fold(src[lo:lo + W_rank], dst[lo:lo + W_rank])
-            if tree is not None:
-                tree.merge_window()
-            else:
-                ds.close_window()
+            window(w)
 
     log = lambda m: print("[bench rank %d] %s" % (rank, m), file=sys.stderr, flush=True)
-    log("inputs ready: %d edges/rank, %d windows of %d" % (E_rank, nwin, W_rank))
+    log("inputs ready: %d edges/rank, %d windows of %d (global %d), %s scaling" % (E_rank, nwin, W_rank, W_glob, a.scaling))
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
     log("warmup done")
-    # timing events only on the kernels the JSON line reports from the timed region (every timed
-    # launch costs ~3 us of dispatch: all kernels timed = +0.7 ms per 64-window step, the fold
-    # alone +0.3 ms); the close is timed afterwards, outside the timed region
-    ds.timing(GS_TIMING_MASK | (1 << GS_K_FOLD) | ((1 << GS_K_MERGE) | (1 << GS_K_EXPORT) if world > 1 else 0))
+    # timing events only on the kernels the JSON line reports from the timed region (each timed
+    # launch costs ~3 us of dispatch); the close is timed afterwards, outside the timed region
+    ds.timing(GS_TIMING_MASK | (1 << GS_K_FOLD) | (1 << GS_K_RING) |
+              ((1 << GS_K_MERGE) | (1 << GS_K_EXPORT) if world > 1 else 0))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -146,20 +191,24 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    fold_ms, fold_n = ds.kernel_time(GS_K_FOLD)
+    elapsed = time.perf_counter() - t0
+    young_ms, young_n = ds.kernel_time(GS_K_FOLD)
+    ring_ms, ring_n = ds.kernel_time(GS_K_RING)
     merge_ms, _ = ds.kernel_time(GS_K_MERGE)
     export_ms, _ = ds.kernel_time(GS_K_EXPORT)
     ds.timing(False)
-    # the close's kernels, timed over one more (untimed-region) step
+    # one more (untimed) step: the close's kernel time, and |V_seen| after every window for the
+    # label-write term of the wall-clock roofline
     ds.timing(GS_TIMING_MASK | (1 << GS_K_COMPRESS))
-    step()
-    torch.cuda.synchronize()
-    comp_ms, comp_n = ds.kernel_time(GS_K_COMPRESS)        # one step
+    ds.reset()
+    seen_sum = 0
+    for w in range(nwin):
+        window(w)
+        seen_sum += ds.stats()[0]
+    comp_ms, comp_n = ds.kernel_time(GS_K_COMPRESS)
     ds.timing(False)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if a.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -168,20 +217,13 @@ def main():
         lat = []
         ds.reset()
         for w in range(nwin):
-            lo = w * W_rank
             if world > 1:
                 dist.barrier()
             torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            if gather:
-                tree.before_fold()
-            ds.fold(src[lo:lo + W_rank], dst[lo:lo + W_rank])
-            if tree is not None:
-                tree.merge_window()
-            else:
-                ds.close_window()
+            t1 = time.perf_counter()
+            window(w)
             torch.cuda.synchronize()
-            lat.append((time.perf_counter() - t0) * 1e6)
+            lat.append((time.perf_counter() - t1) * 1e6)
         lat.sort()
         latency = {"p50_us": lat[len(lat) // 2], "p99_us": lat[min(len(lat) - 1, int(len(lat) * 0.99))],
                    "max_us": lat[-1], "windows": len(lat)}
@@ -191,24 +233,32 @@ def main():
         if world == 1:
             verify = verify_labels(ds, src, dst, V)
         else:                                   # the union of every rank's slices
-            gs = torch.empty(E_rank * world, dtype=torch.int32, device=dev)
-            gd = torch.empty(E_rank * world, dtype=torch.int32, device=dev)
-            gen.rmat(gs, gd, 0, a.scale, a.seed)
+            gs = torch.empty(nwin * W_glob, dtype=idt, device=dev)
+            gd = torch.empty(nwin * W_glob, dtype=idt, device=dev)
+            if a.kind == "er":
+                gen.erdos_renyi(gs, gd, 0, V, a.seed)
+            else:
+                gen.rmat(gs, gd, 0, a.scale, a.seed)
             verify = verify_labels(ds, gs, gd, V)
 
     if rank == 0:
+        eb = 8 if a.id_bits == 32 else 16            # edge bytes; parent words are 4 B either way
+        per_edge = eb + 8 if a.id_bits == 32 else 2 * 16   # int64 doubles every term
+        label_b = 4 if a.id_bits == 32 else 8
         total_edges = a.steps * E_rank * world
-        folds = a.steps * nwin                       # window folds in the timed region (this rank)
-        fold_win_ms = fold_ms / max(folds, 1)        # fold time per window (window 1 = several launches)
-        achieved = BYTES_PER_EDGE_ALG * W_rank / (fold_win_ms * 1e-3) / 1e9
-        traffic = None
-        if os.path.exists(a.traffic_json):
-            try:
-                tj = json.load(open(a.traffic_json))
-                if tj.get("window_edges") == W_rank and tj.get("scale") == a.scale:
-                    traffic = tj.get("hbm_bytes_per_window")
-            except Exception:
-                traffic = None
+        folds = a.steps * nwin
+        ring_avg = ring_ms / ring_n if ring_n else None
+        fold_win_ms = (young_ms + ring_ms) / max(folds, 1)
+        ring_edges = W_rank - (W_rank % 4)
+        if ring_avg:
+            kernel, avg_ms = "k_fold_ring", ring_avg
+            alg_launch = per_edge * ring_edges
+        else:                                        # no steady ring launches (small ids: plain k_fold)
+            kernel, avg_ms = "k_fold (every window)", fold_win_ms
+            alg_launch = per_edge * W_rank
+        achieved = alg_launch / (avg_ms * 1e-3) / 1e9
+        alg_step = per_edge * E_rank * world + label_b * seen_sum          # BASELINE.md B_alg per step
+        wall_gbs = alg_step * a.steps / elapsed / 1e9
         nv, nc = ds.stats()
         line = {
             "metric": METRIC,
@@ -219,17 +269,23 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": elapsed / a.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": a.scaling,
             "vs_baseline": None,
-            "dtype": "int32",
+            "dtype": "int32" if a.id_bits == 32 else "int64",
             "data": "synthetic: counter-based %s stream generated in HBM (seed %d), no dataset"
-                    % ("Erdos-Renyi" if a.workload == "c4" else "RMAT", a.seed),
+                    % ("Erdos-Renyi" if a.kind == "er" else "RMAT", a.seed),
             "config": {
-                "workload": "%s_%s%d_ef%d_window%s" % (a.workload, "er" if a.workload == "c4" else "rmat",
-                                                        a.scale, a.edge_factor, _pow2(W_rank)),
-                "scale": a.scale, "vertices": V, "edge_factor_per_gpu": a.edge_factor,
-                "edges_per_gpu": E_rank, "window_edges_per_gpu": W_rank, "windows": nwin,
-                "parallelism": "1 subtask per GPU x %d, %s" % (world, ("RCCL %s merge" % a.merge) if world > 1 else "no merge"),
+                "workload": "%s_%s%d_ef%d_window%s%s%s" % (a.workload.split("_")[0], "er" if a.kind == "er" else "rmat",
+                                                         a.scale, a.edge_factor, _pow2(W_glob),
+                                                         "_int64" if a.id_bits == 64 else "",
+                                                         "_hostinput" if a.host_input else ""),
+                "scale": a.scale, "vertices": V, "edge_factor": a.edge_factor,
+                "edges_total": E_glob, "edges_per_gpu": E_rank, "window_edges": W_glob,
+                "window_edges_per_gpu": W_rank, "windows": nwin, "id_bits": a.id_bits,
+                "input": "pinned host memory (PCIe-inclusive)" if a.host_input else "HBM",
+                "parallelism": "1 subtask per GPU x %d, %s" % (
+                    world, ("%s merge, %s" % (a.merge, "C ABI over RCCL" if comm is not None else "torch.distributed gloo"))
+                    if world > 1 else "no merge"),
                 "emission": "per window, canonical min-id labels resident in HBM",
             },
             "roofline": {
@@ -238,15 +294,25 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "kernel": "UpdateCC per window: k_fold_ring (steady windows) / k_fold (young-forest launches)",
-                "alg_bytes_per_window": BYTES_PER_EDGE_ALG * W_rank,
-                "fold_ms_per_window": fold_win_ms,
-                "fold_launches": fold_n,
-                "windows_timed": folds,
+                "traffic": traffic_per_launch(a, W_rank) if kernel == "k_fold_ring" else None,
+                "kernel": kernel,
+                "alg_bytes_per_launch": alg_launch,
+                "avg_launch_ms": avg_ms,
+                "launches": ring_n if ring_avg else folds,
+                "definition": "dominant kernel: %d B per edge (edge read + 2 parent words, SURVEY.md 8(d)) x edges "
+                              "per launch / its average launch duration (HIP events on the launch stream, timed "
+                              "region)" % per_edge,
+                "fold_all": {"achieved": per_edge * W_rank / (fold_win_ms * 1e-3) / 1e9,
+                             "frac": per_edge * W_rank / (fold_win_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                             "ms_per_window": fold_win_ms, "young_launches": young_n // max(a.steps, 1),
+                             "definition": "every UpdateCC launch of a window (young k_fold + steady k_fold_ring)"},
+                "wall": {"achieved": wall_gbs, "frac": wall_gbs / (world * HBM_PEAK_GBS),
+                         "alg_bytes_per_step": alg_step,
+                         "definition": "BASELINE.md: sum over windows of (%d E_w + %d |V_seen,w|) / wall time / "
+                                       "(P x 8 TB/s)" % (per_edge, label_b)},
             },
             "kernels": {
-                "fold_share": fold_ms / (elapsed * 1e3),
+                "fold_share": (young_ms + ring_ms) / (elapsed * 1e3),
                 "compress_ms_per_window": comp_ms / max(comp_n, 1),
                 "compress_share": comp_ms / (elapsed / a.steps * 1e3),
             },
@@ -254,12 +320,16 @@ def main():
             "final_components": nc,
         }
         if world > 1:                                # rank 0's side of the exchange
+            if comm is not None:
+                _, _, sent, recv, nex = comm.info()
+            else:
+                sent, recv, nex = tree.bytes_sent, tree.bytes_recv, (a.warmup + a.steps + 1) * nwin
             line["exchange"] = {
-                "merge": a.merge,
+                "merge": a.merge, "transport": "RCCL (C ABI)" if comm is not None else "gloo (Python)",
                 "merge_fold_ms_per_window": merge_ms / max(folds, 1),
                 "export_ms_per_window": export_ms / max(folds, 1),
-                "bytes_sent_per_window": tree.bytes_sent / (a.warmup + a.steps + 1) / nwin,
-                "bytes_recv_per_window": tree.bytes_recv / (a.warmup + a.steps + 1) / nwin,
+                "bytes_sent_per_window": sent / max(nex, 1),
+                "bytes_recv_per_window": recv / max(nex, 1),
                 "wall_ms_per_window": elapsed / a.steps / nwin * 1e3,
             }
         if verify is not None:
@@ -268,11 +338,13 @@ def main():
             line["window_latency"] = latency
         if not a.no_cpu_baseline and world == 1:
             log("timed region done (%.1f ms/step); cpu baseline..." % (elapsed / a.steps * 1e3))
-            line["cpu_baseline"] = cpu_baseline(a, src, dst, W_rank)
+            line["cpu_baseline"] = cpu_baseline(a, ds, window, src, dst, W_rank, nwin)
         print(json.dumps(line), flush=True)
     if gather:
         tree.drain()
     ds.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 
@@ -282,6 +354,20 @@ def _pow2(x: int) -> str:
         if x >= (1 << sh) and x % (1 << sh) == 0:
             return "%d%s" % (x >> sh, suf)
     return str(x)
+
+
+def traffic_per_launch(a, W_rank):
+    """HBM bytes per k_fold_ring launch from the committed PMC passes (profiles/pmc_traffic.py), if
+    they were taken on this configuration."""
+    if not os.path.exists(a.traffic_json):
+        return None
+    try:
+        tj = json.load(open(a.traffic_json))
+        if tj.get("window_edges") == W_rank and tj.get("scale") == a.scale and tj.get("id_bits", 32) == a.id_bits:
+            return tj.get("ring", {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
 
 
 def torch_min_labels(src, dst, V):
@@ -309,7 +395,7 @@ def torch_min_labels(src, dst, V):
 
 
 def verify_labels(ds, src, dst, V):
-    lab = torch.empty(V, dtype=torch.int32, device=src.device)
+    lab = torch.empty(V, dtype=torch.int32 if ds.id_bits == 32 else torch.int64, device=src.device)
     ds.dense(out=lab)
     lab = lab.long()
     s, d = src.long(), dst.long()
@@ -321,23 +407,49 @@ def verify_labels(ds, src, dst, V):
     return {"edges_consistent": ok_edges, "labels_minimal_idempotent": ok_min, "equals_torch_cc": ok_exact}
 
 
-def cpu_baseline(a, src, dst, W):
+def cpu_baseline(a, ds, window, src, dst, W, nwin):
     """Reference-semantics CPU restatement (oracle/, C): hash-map DisjointSet per partition on P
-    host threads, single-thread CombineCC + Merger, FlattenSet emission per window; timed on a
-    bounded sample (the first windows of the same stream)."""
+    host threads (P = the host's core count), single-thread CombineCC + Merger,
+    FlattenSet emission per window (SummaryBulkAggregation.java:76-83, SummaryAggregation.java:106-119,
+    ConnectedComponentsExample.java:143-156). Sampled windows from the start, the middle and the end
+    of the stream: the Merger's cumulative summary makes a window's cost depend on everything
+    before it, so a span that starts at window s is run from the Merger restored (untimed, as
+    restoreState would) from the canonical emission of window s-1, taken from the GPU run."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from pyoracle import EMIT_FLATTEN, coracle
     import numpy as np
-    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    cores = max(1, min(cores, 16, os.cpu_count() or 1))
-    n = min(max(a.cpu_sample_edges // W, 1) * W, src.numel())
-    hs = src[:n].cpu().numpy().astype(np.int64)
-    hd = dst[:n].cpu().numpy().astype(np.int64)
-    r = coracle().run(hs, hd, W, partitions=cores, threads=cores, emit=EMIT_FLATTEN)
-    return {"value": n / r["seconds"], "unit": "edges/s", "cores": cores, "kind": "port",
-            "sample": "first %d windows (%d edges) of the same RMAT-%d stream, window %d edges, "
-                      "P=%d partitions on %d threads, FlattenSet emission per window; %.1f s"
-                      % (r["windows"], n, a.scale, W, cores, cores, r["seconds"])}
+    cores = os.cpu_count() or 1
+    try:
+        share = len(os.sched_getaffinity(0))
+    except Exception:
+        share = cores
+    o = coracle()
+    spans = sorted({(0, min(2, nwin)), (nwin // 2, 1), (nwin - 1, 1)})
+    edges = 0
+    secs = 0.0
+    names = []
+    for s0, ln in spans:
+        if s0 + ln > nwin or s0 < 0:
+            continue
+        init = None
+        if s0:
+            ds.reset()
+            for w in range(s0):
+                window(w)
+            init = ds.pairs()                      # the canonical emission of window s0-1 (host)
+        lo, hi = s0 * W, (s0 + ln) * W
+        r = o.run(src[lo:hi].cpu().numpy().astype(np.int64), dst[lo:hi].cpu().numpy().astype(np.int64), W,
+                  partitions=cores, threads=cores, emit=EMIT_FLATTEN, init=init)
+        edges += hi - lo
+        secs += r["seconds"]
+        names.append("%d-%d" % (s0 + 1, s0 + ln) if ln > 1 else "%d" % (s0 + 1))
+    return {"value": edges / secs, "unit": "edges/s", "cores": cores, "kind": "port",
+            "sample": "windows %s of %d (%d edges) of the same %s stream, window %d edges; a span starting at "
+                      "window s runs from the Merger restored from window s-1's emission (untimed); P=%d "
+                      "partitions on %d threads (nproc=%d, CPUs in this process's affinity=%d), FlattenSet "
+                      "emission per window; %.1f s timed" % (", ".join(names), nwin, edges,
+                                                              "RMAT-%d" % a.scale if a.kind == "rmat" else "ER",
+                                                              W, cores, cores, os.cpu_count() or 1, share, secs)}
 
 
 if __name__ == "__main__":

@@ -68,8 +68,10 @@ struct gs_cc {
     uint32_t* derr = nullptr;            // derr[0] deferred device error flags; derr[1..5] giant state
     unsigned long long* dscratch = nullptr;  // reduction outputs (8 words)
     unsigned long long* hscratch = nullptr;  // pinned mirror
-    void* stage = nullptr;               // host->device staging (2 * staging_edges ids)
+    void* stage = nullptr;               // host->device staging: 2 slots x (src, dst) x staging_edges ids
     size_t stage_bytes = 0;
+    hipStream_t copy = nullptr;          // H2D copies of host-buffer folds (double-buffered staging)
+    hipEvent_t staged[2] = {nullptr, nullptr}, freed[2] = {nullptr, nullptr};
     void* tmp = nullptr;                 // emission temporaries
     size_t tmp_bytes = 0;
     bool compressed = true;
@@ -288,7 +290,8 @@ static bool use_ring(const gs_cc_t* h) {
     return m == kFoldRing || (m == kFoldAuto && h->hot_bits >= dbg().ring_min_bits);
 }
 
-void launch_fold_ring(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t n) {
+template <typename IdT>
+void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     ensure_stats(h);
     HotArgs hot{h->hot, h->hot_bits, h->hot_cand};
     // admission: while the device budget lasts (cc_kernels.hpp), plus every kHotAdmitEvery-th launch
@@ -309,16 +312,16 @@ void launch_fold_ring(gs_cc_t* h, const uint32_t* a, const uint32_t* b, uint64_t
     hot.wcnt = build ? h->wcnt : nullptr;
     hot.count_edges = build ? kWarmSample : 0;
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
-    KTimer t(h, h->fold_timer);
+    KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_RING : h->fold_timer);
     const bool st = h->dstats != nullptr;
     const dim3 grid(grid_for(n / 4, kHotThreads, (unsigned)std::max(h->cus, 1)));
     hipEvent_t stop = build ? nullptr : t.stop();
     if (h->mark) {
-        if (st) klaunch(k_fold_ring<true, true>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
-        else klaunch(k_fold_ring<true, false>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
+        if (st) klaunch(k_fold_ring<IdT, true, true>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
+        else klaunch(k_fold_ring<IdT, true, false>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
     } else {
-        if (st) klaunch(k_fold_ring<false, true>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
-        else klaunch(k_fold_ring<false, false>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
+        if (st) klaunch(k_fold_ring<IdT, false, true>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
+        else klaunch(k_fold_ring<IdT, false, false>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
     }
     if (build) {
         // hottest band first: a full bucket then drops the colder ids
@@ -351,12 +354,11 @@ int compress_impl(gs_cc_t* h);
 template <typename IdT, bool AOS>
 void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, size_t esz) {
     const uint64_t young_limit = h->cap / 4;
-    // mature forest (past the young limit), aligned device uint32 SoA: the steady ring fold
-    if (std::is_same<IdT, uint32_t>::value && !AOS && h->hot && use_ring(h) &&
-        h->edges_since_reset >= young_limit && n >= 4 &&
+    // mature forest (past the young limit), aligned device SoA (32- or 64-bit ids): the steady ring fold
+    if (!AOS && h->hot && use_ring(h) && h->edges_since_reset >= young_limit && n >= 4 &&
         ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0) {
         const uint64_t done = n & ~(uint64_t)3;
-        launch_fold_ring(h, reinterpret_cast<const uint32_t*>(a), reinterpret_cast<const uint32_t*>(b), done);
+        launch_fold_ring<IdT>(h, reinterpret_cast<const IdT*>(a), reinterpret_cast<const IdT*>(b), done);
         h->edges_since_reset += done;
         if (done == n) return;
         a += done * esz;
@@ -437,6 +439,9 @@ void launch_fold_any(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool 
     }
 }
 
+// host-buffer folds: edges per staging chunk (one window of the headline workload)
+constexpr uint64_t kStagingEdges = 1ull << 24;
+
 int fold_impl(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, uint32_t id_bits) {
     GS_TRY(check(h));
     if (n == 0) return GS_OK;
@@ -452,21 +457,38 @@ int fold_impl(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, ui
         GS_HIP(hipGetLastError());
         return GS_OK;
     }
-    // host buffers: stage chunk by chunk (stream order protects the staging buffer)
-    const uint64_t chunk = h->cfg.staging_edges ? h->cfg.staging_edges : (1ull << 22);
-    GS_TRY(ensure_buf(&h->stage, &h->stage_bytes, (size_t)chunk * esz * 2));
-    for (uint64_t off = 0; off < n; off += chunk) {
-        const uint64_t m = (n - off < chunk) ? (n - off) : chunk;
-        char* s0 = static_cast<char*>(h->stage);
-        char* s1 = s0 + (size_t)chunk * esz;
-        if (aos) {
-            GS_HIP(hipMemcpyAsync(s0, static_cast<const char*>(a) + off * esz * 2, m * esz * 2, hipMemcpyHostToDevice, h->stream));
-        } else {
-            GS_HIP(hipMemcpyAsync(s0, static_cast<const char*>(a) + off * esz, m * esz, hipMemcpyHostToDevice, h->stream));
-            GS_HIP(hipMemcpyAsync(s1, static_cast<const char*>(b) + off * esz, m * esz, hipMemcpyHostToDevice, h->stream));
+    // host buffers (pinned: DMA at the PCIe rate; pageable: through the runtime's bounce buffers):
+    // double-buffered staging. Chunk i is copied into slot i & 1 on the copy stream while chunk
+    // i - 1 folds on the handle's stream; a slot is refilled only after the fold that read it.
+    const uint64_t chunk = h->cfg.staging_edges ? h->cfg.staging_edges : kStagingEdges;
+    GS_TRY(ensure_buf(&h->stage, &h->stage_bytes, (size_t)chunk * esz * 4));
+    if (!h->copy) {
+        GS_HIP(hipStreamCreateWithFlags(&h->copy, hipStreamNonBlocking));
+        for (int k = 0; k < 2; ++k) {
+            GS_HIP(hipEventCreateWithFlags(&h->staged[k], hipEventDisableTiming));
+            GS_HIP(hipEventCreateWithFlags(&h->freed[k], hipEventDisableTiming));
         }
+    }
+    GS_HIP(hipEventRecord(h->freed[0], h->stream));      // folds queued before this call may still read
+    GS_HIP(hipEventRecord(h->freed[1], h->stream));      // the slots
+    uint64_t i = 0;
+    for (uint64_t off = 0; off < n; off += chunk, ++i) {
+        const uint64_t m = (n - off < chunk) ? (n - off) : chunk;
+        const int k = (int)(i & 1);
+        char* s0 = static_cast<char*>(h->stage) + (size_t)k * chunk * esz * 2;
+        char* s1 = s0 + (size_t)chunk * esz;
+        GS_HIP(hipStreamWaitEvent(h->copy, h->freed[k], 0));
+        if (aos) {
+            GS_HIP(hipMemcpyAsync(s0, static_cast<const char*>(a) + off * esz * 2, m * esz * 2, hipMemcpyHostToDevice, h->copy));
+        } else {
+            GS_HIP(hipMemcpyAsync(s0, static_cast<const char*>(a) + off * esz, m * esz, hipMemcpyHostToDevice, h->copy));
+            GS_HIP(hipMemcpyAsync(s1, static_cast<const char*>(b) + off * esz, m * esz, hipMemcpyHostToDevice, h->copy));
+        }
+        GS_HIP(hipEventRecord(h->staged[k], h->copy));
+        GS_HIP(hipStreamWaitEvent(h->stream, h->staged[k], 0));
         launch_fold_any(h, s0, s1, m, aos, id_bits);
         GS_HIP(hipGetLastError());
+        GS_HIP(hipEventRecord(h->freed[k], h->stream));
     }
     return GS_OK;
 }
@@ -756,6 +778,12 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->dscratch) (void)hipFree(h->dscratch);
     if (h->hscratch) (void)hipHostFree(h->hscratch);
     if (h->stage) (void)hipFree(h->stage);
+    if (h->copy) (void)hipStreamSynchronize(h->copy);
+    for (int k = 0; k < 2; ++k) {
+        if (h->staged[k]) (void)hipEventDestroy(h->staged[k]);
+        if (h->freed[k]) (void)hipEventDestroy(h->freed[k]);
+    }
+    if (h->copy) (void)hipStreamDestroy(h->copy);
     if (h->tmp) (void)hipFree(h->tmp);
     if (h->own) (void)hipStreamDestroy(h->own);
     delete h;
@@ -1101,6 +1129,7 @@ int gs_cc_timing(gs_cc_t* h, int enable) {
     GS_TRY(resolve_timing(h));
     h->timing = enable != 0;
     h->timing_mask = (enable & GS_TIMING_MASK) ? ((uint32_t)enable & 0xFFu) : ~0u;
+    if (h->timing_mask & (1u << GS_K_FOLD)) h->timing_mask |= 1u << GS_K_RING;   // "fold" = both launch kinds
     for (int k = 0; k < GS_K_COUNT; ++k) { h->total_ms[k] = 0; h->launches[k] = 0; }
     return GS_OK;
 }

@@ -596,8 +596,31 @@ __device__ __forceinline__ void ring_flush(const FoldArgs& f, uint2* ring, uint3
     __builtin_amdgcn_wave_barrier();
 }
 
-template <bool MARK, bool STATS>
-__global__ __launch_bounds__(kHotThreads) void k_fold_ring(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+// 4 consecutive ids of an aligned SoA stream as uint32 (int64 ids: two 16-B loads; a negative or
+// >= cap id fails the range check either way)
+template <typename IdT>
+__device__ __forceinline__ void load4(const IdT* __restrict__ p, uint64_t g, uint32_t (&x)[4], bool (&ok)[4], uint32_t cap) {
+    if (sizeof(IdT) == 4) {
+        const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p) + g);
+        x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ok[k] = ok[k] && x[k] < cap;
+    } else {
+        const u64x2 q0 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(p) + 2 * g);
+        const u64x2 q1 = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(p) + 2 * g + 1);
+        const uint64_t y[4] = {q0.x, q0.y, q1.x, q1.y};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            ok[k] = ok[k] && y[k] < (uint64_t)cap;
+            x[k] = (uint32_t)y[k];
+        }
+    }
+}
+
+template <typename IdT, bool MARK, bool STATS>
+__global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict__ a, const IdT* __restrict__ b,
                                                            FoldArgs f, HotArgs hot) {
     __shared__ uint2 tab[kHotBuckets];
     __shared__ uint2 rings[kHotThreads / 64][kRingCap];
@@ -631,14 +654,13 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const uint32_t* __res
         bool ok[4] = {false, false, false, false};
         uint32_t gf[4] = {0u, 0u, 0u, 0u};
         if (g < groups) {
-            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a) + g);
-            const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b) + g);
-            u[0] = x.x; u[1] = x.y; u[2] = x.z; u[3] = x.w;
-            v[0] = y.x; v[1] = y.y; v[2] = y.z; v[3] = y.w;
+            bool oka[4] = {true, true, true, true}, okb[4] = {true, true, true, true};
+            load4<IdT>(a, g, u, oka, f.rc.cap);
+            load4<IdT>(b, g, v, okb, f.rc.cap);
             bool bad = false;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                ok[k] = u[k] < f.rc.cap && v[k] < f.rc.cap;
+                ok[k] = oka[k] && okb[k];
                 bad |= !ok[k];
                 if (!ok[k]) { u[k] = 0; v[k] = 0; }
             }

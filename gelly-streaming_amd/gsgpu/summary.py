@@ -286,6 +286,12 @@ class DisjointSet:
         call("gs_cc_kernel_time", self.handle, int(kernel), ctypes.byref(ms), ctypes.byref(n))
         return float(ms.value), int(n.value)
 
+    def fold_time(self) -> Tuple[float, int]:
+        """(ms, launches) of every UpdateCC launch: k_fold (young / plain) + k_fold_ring (steady)."""
+        a, na = self.kernel_time(_abi.GS_K_FOLD)
+        b, nb = self.kernel_time(_abi.GS_K_RING)
+        return a + b, na + nb
+
 
 def combine_cc(s1: DisjointSet, s2: DisjointSet) -> DisjointSet:
     """CombineCC.reduce (ConnectedComponents.java:116-125) on two device summaries."""

@@ -28,7 +28,9 @@
  * Conventions: every function returns 0 (GS_OK) or a negative GS_ERR_* code; the message of the
  * last failure on the calling thread is gs_last_error(). No C++ exception crosses the ABI.
  * Buffers passed in may be host (pageable or pinned) or device pointers; the caller keeps
- * ownership of them, the library owns all device state of a handle. One handle per subtask
+ * ownership of them, the library owns all device state of a handle. Input buffers of a fold must
+ * stay unchanged until the handle's stream has run it (gs_cc_sync): host edges are copied
+ * asynchronously (double-buffered staging, gs_cc_config.staging_edges per chunk). One handle per subtask
  * thread; calls on one handle must be serialised by the caller; different handles may be used
  * concurrently. All work of a handle is ordered on its HIP stream (gs_cc_set_stream).
  */
@@ -76,7 +78,7 @@ typedef struct gs_cc_config {
                                    (GS_CC_SPARSE_IDS: the number of distinct ids, <= 2^30)   */
     int32_t  device;            /* HIP device ordinal                                      */
     uint32_t flags;             /* GS_CC_*                                                 */
-    uint64_t staging_edges;     /* staging size for host-pointer folds (0 = 2^22)          */
+    uint64_t staging_edges;     /* staging chunk of host-pointer folds, 2 slots (0 = 2^24) */
 } gs_cc_config;
 
 /* ---- lifetime ---- */
@@ -169,8 +171,9 @@ int gs_comm_info(gs_comm_t* comm, int* rank, int* world, uint64_t* bytes_sent, u
 int gs_cc_merge_window(gs_cc_t* h, gs_comm_t* comm, int mode);
 
 /* ---- instrumentation ----
- * kernel ids: 0 fold, 1 compress (close_window), 2 merge, 3 export. */
-enum { GS_K_FOLD = 0, GS_K_COMPRESS = 1, GS_K_MERGE = 2, GS_K_EXPORT = 3, GS_K_COUNT = 4 };
+ * kernel ids: 0 fold (young-forest / plain k_fold launches), 1 compress (close_window), 2 merge,
+ * 3 export, 4 ring (the steady k_fold_ring launches; fold time = 0 + 4). */
+enum { GS_K_FOLD = 0, GS_K_COMPRESS = 1, GS_K_MERGE = 2, GS_K_EXPORT = 3, GS_K_RING = 4, GS_K_COUNT = 5 };
 /* enable = 0: off; 1: every kernel; GS_TIMING_MASK | (1 << GS_K_x) | ...: only those kernels
  * carry timing events (a timed launch costs ~3 us more dispatch time). Totals reset. */
 enum { GS_TIMING_MASK = 0x100 };

@@ -87,6 +87,13 @@ typedef struct {
 int gso_cc_run(const int64_t* src, const int64_t* dst, uint64_t n, const gso_run_cfg* cfg,
                uint64_t* out_checksums, int64_t* out_labels, int64_t* final_labels,
                gso_run_stats* stats);
+/* As gso_cc_run, with the Merger restored first (untimed) from a snapshot of n_init canonical
+ * (vertex, label) pairs (ListCheckpointed restoreState, SummaryAggregation.java:127-135): the run
+ * then continues the stream from the middle. */
+int gso_cc_run_from(const int64_t* init_v, const int64_t* init_l, uint64_t n_init,
+                    const int64_t* src, const int64_t* dst, uint64_t n, const gso_run_cfg* cfg,
+                    uint64_t* out_checksums, int64_t* out_labels, int64_t* final_labels,
+                    gso_run_stats* stats);
 
 /* ---------------- deterministic synthetic streams (same definition as the device generators) ---------------- */
 uint64_t gso_splitmix64(uint64_t x);

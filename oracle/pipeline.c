@@ -64,6 +64,13 @@ static uint64_t flatten_set(gso_ds* ds) {
 int gso_cc_run(const int64_t* src, const int64_t* dst, uint64_t n, const gso_run_cfg* cfg,
                uint64_t* out_checksums, int64_t* out_labels, int64_t* final_labels,
                gso_run_stats* stats) {
+    return gso_cc_run_from(NULL, NULL, 0, src, dst, n, cfg, out_checksums, out_labels, final_labels, stats);
+}
+
+int gso_cc_run_from(const int64_t* init_v, const int64_t* init_l, uint64_t n_init,
+                    const int64_t* src, const int64_t* dst, uint64_t n, const gso_run_cfg* cfg,
+                    uint64_t* out_checksums, int64_t* out_labels, int64_t* final_labels,
+                    gso_run_stats* stats) {
     const int P = cfg->partitions > 0 ? cfg->partitions : 1;
     int T = cfg->threads > 0 ? cfg->threads : 1;
     if (T > P) T = P;
@@ -72,9 +79,14 @@ int gso_cc_run(const int64_t* src, const int64_t* dst, uint64_t n, const gso_run
     fold_job* jobs = (fold_job*)calloc((size_t)T, sizeof(fold_job));
     pthread_t* th = (pthread_t*)calloc((size_t)T, sizeof(pthread_t));
     gso_ds* summary = NULL;            /* Merger.summary = initialVal (empty) */
+    if (n_init) {                      /* Merger.restoreState (SummaryAggregation.java:131-135): the
+                                          snapshotted summary, rebuilt from its (vertex, label) pairs */
+        summary = gso_ds_new();
+        for (uint64_t i = 0; i < n_init; ++i) gso_ds_union(summary, init_v[i], init_l[i]);
+    }
     uint64_t w = 0;
     volatile uint64_t sink = 0;
-    double t0 = now_s();
+    double t0 = now_s();                /* the restore is not timed */
 
     for (uint64_t lo = 0; lo < n; lo += W, ++w) {
         uint64_t len = (n - lo < W) ? (n - lo) : W;

@@ -229,6 +229,9 @@ class COracle:
         L.gso_ds_canonical_dense.argtypes = [vp, vp, u64]; L.gso_ds_canonical_dense.restype = u64
         L.gso_cc_run.argtypes = [vp, vp, u64, ctypes.POINTER(_RunCfg), vp, vp, vp, ctypes.POINTER(_RunStats)]
         L.gso_cc_run.restype = i32
+        L.gso_cc_run_from.argtypes = [vp, vp, u64, vp, vp, u64, ctypes.POINTER(_RunCfg), vp, vp, vp,
+                                      ctypes.POINTER(_RunStats)]
+        L.gso_cc_run_from.restype = i32
         L.gso_gen_rmat.argtypes = [vp, vp, u64, u64, i32, u64, u32, u32, u32, i32]
         L.gso_gen_er.argtypes = [vp, vp, u64, u64, u64, u64]
         L.gso_splitmix64.argtypes = [u64]; L.gso_splitmix64.restype = u64
@@ -253,7 +256,9 @@ class COracle:
     # ---- pipeline ----
     def run(self, src: np.ndarray, dst: np.ndarray, window_edges: int, partitions: int = 1,
             threads: int = 1, emit: int = EMIT_CHECKSUM, label_cap: int = 0,
-            want_final: bool = False):
+            want_final: bool = False, init=None):
+        """The pipeline over (src, dst); init = (vertices, labels): the Merger restored from that
+        snapshot first (untimed), so a run can start in the middle of a stream."""
         src = np.ascontiguousarray(src, dtype=np.int64)
         dst = np.ascontiguousarray(dst, dtype=np.int64)
         n = int(src.size)
@@ -264,8 +269,14 @@ class COracle:
         sums = np.zeros(max(nwin, 1), dtype=np.uint64)
         labels = np.empty((max(nwin, 1), label_cap), dtype=np.int64) if emit == EMIT_DENSE else None
         final = np.empty(label_cap, dtype=np.int64) if (want_final and label_cap) else None
-        rc = self.L.gso_cc_run(_p(src), _p(dst), n, ctypes.byref(cfg), _p(sums), _p(labels),
-                               _p(final), ctypes.byref(st))
+        if init is not None and len(init[0]):
+            iv = np.ascontiguousarray(init[0], dtype=np.int64)
+            il = np.ascontiguousarray(init[1], dtype=np.int64)
+            rc = self.L.gso_cc_run_from(_p(iv), _p(il), int(iv.size), _p(src), _p(dst), n, ctypes.byref(cfg),
+                                        _p(sums), _p(labels), _p(final), ctypes.byref(st))
+        else:
+            rc = self.L.gso_cc_run(_p(src), _p(dst), n, ctypes.byref(cfg), _p(sums), _p(labels),
+                                   _p(final), ctypes.byref(st))
         if rc != 0:
             raise RuntimeError("gso_cc_run failed: %d" % rc)
         return {"windows": int(st.windows), "checksums": sums[:nwin], "labels": labels,

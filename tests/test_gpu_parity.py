@@ -501,18 +501,36 @@ def test_cc_example_file_input(tmp_path):
 
 
 # ---------------- bench.py multi-rank path (2 ranks on one GPU, gloo-staged exchange) ----------------
+@pytest.mark.parametrize("scaling", ["strong", "weak"])
 @pytest.mark.parametrize("merge", ["allgather", "gather", "tree"])
-def test_bench_two_ranks_one_gpu_verified(merge):
+def test_bench_two_ranks_one_gpu_verified(merge, scaling):
     import subprocess, sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(root, "bench.py"),
            "--gpus", "2", "--steps", "1", "--warmup", "1", "--scale", "16", "--edge-factor", "16",
-           "--window-log2", "16", "--dist-backend", "gloo", "--verify", "--merge", merge]
+           "--window-log2", "16", "--dist-backend", "gloo", "--verify", "--merge", merge, "--scaling", scaling]
     out = subprocess.check_output(cmd, env=env, timeout=240).decode()
     line = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
-    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["n_gpus"] == 2 and line["scaling"] == scaling
+    assert line["config"]["edges_total"] == (1 << 20) * (2 if scaling == "weak" else 1)
+    assert line["verify"] == {"edges_consistent": True, "labels_minimal_idempotent": True, "equals_torch_cc": True}
+
+
+@pytest.mark.parametrize("extra", [["--id-bits", "64"], ["--host-input"], ["--host-input", "--id-bits", "64"],
+                                   ["--workload", "c3_single"]], ids=["int64", "host", "host_int64", "single_window"])
+def test_bench_lines_verified(extra):
+    """The extra bench lines (int64 ids, pinned-host input through the double-buffered staging,
+    one window), end to end against the independent torch CC, at RMAT-22 / 2^20-edge windows."""
+    import subprocess, sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--steps", "1", "--warmup", "0", "--scale", "22",
+           "--edge-factor", "16", "--no-cpu-baseline", "--verify"] + extra
+    if "--workload" not in extra:
+        cmd += ["--window-log2", "20"]
+    out = subprocess.check_output(cmd, timeout=300).decode()
+    line = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
     assert line["verify"] == {"edges_consistent": True, "labels_minimal_idempotent": True, "equals_torch_cc": True}
 
 

@@ -136,6 +136,21 @@ def test_streams_golden_c_oracle(oracle, case):
         assert dense_checksum(case["labels"][w])[0] == int(case["checksums"][w])
 
 
+@pytest.mark.parametrize("case", _streams(), ids=lambda c: c["name"])
+def test_run_from_restored_merger(oracle, case):
+    """gso_cc_run_from: the Merger restored from window k's canonical emission (restoreState,
+    SummaryAggregation.java:127-135) continues the stream with the uninterrupted emissions."""
+    W, nwin = case["window_edges"], case["labels"].shape[0]
+    k = nwin // 2
+    if k == 0:
+        pytest.skip("one window")
+    lab = case["labels"][k - 1]
+    v = np.nonzero(lab >= 0)[0].astype(np.int64)
+    r = oracle.run(case["src"][k * W:], case["dst"][k * W:], W, partitions=case["partitions"], threads=2,
+                   emit=EMIT_DENSE, label_cap=case["cap"], init=(v, lab[v]))
+    np.testing.assert_array_equal(r["labels"], case["labels"][k:])
+
+
 @pytest.mark.parametrize("case", _streams()[:4], ids=lambda c: c["name"])
 def test_streams_golden_python_twin(case):
     emis = py_cc_stream(case["src"].tolist(), case["dst"].tolist(), case["window_edges"], case["partitions"])
