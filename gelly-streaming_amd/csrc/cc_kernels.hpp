@@ -48,6 +48,12 @@ __device__ __forceinline__ uint32_t find_root(uint32_t* __restrict__ parent, uin
 __device__ __forceinline__ void set_mark(uint32_t* __restrict__ mark, uint32_t v) {
     __hip_atomic_fetch_or(&mark[v >> 5], 1u << (v & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// first touch: v's bit in the seen bitmap (experiment builds may drop it to measure its cost)
+__device__ __forceinline__ void set_seen(uint32_t* __restrict__ sbits, uint32_t v) {
+#ifndef GS_EXP_NOSBITS
+    set_mark(sbits, v);
+#endif
+}
 
 // Read-only root walk (no writes) for find() on const state.
 __device__ __forceinline__ uint32_t find_root_ro(const uint32_t* __restrict__ parent, uint32_t x) {
@@ -63,7 +69,7 @@ __device__ __forceinline__ uint32_t make_set(uint32_t* __restrict__ parent, uint
     if (pv != kInvalid) return pv;
     const uint32_t old = atomicCAS(&parent[v], kInvalid, v);
     if (old != kInvalid) return old;
-    set_mark(sbits, v);
+    set_seen(sbits, v);
     return v;
 }
 
@@ -83,7 +89,7 @@ __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32
         if (pu == kInvalid) {
             const uint32_t old = atomicCAS(&parent[u], kInvalid, u);
             if (old == kInvalid) {
-                set_mark(sbits, u);
+                set_seen(sbits, u);
                 if (MARK) set_mark(mark, u);
             }
         }
@@ -110,7 +116,7 @@ __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32
             const uint32_t old = atomicCAS(&parent[lo], kInvalid, lo);
             lf = false;
             if (old == kInvalid) {
-                set_mark(sbits, lo);
+                set_seen(sbits, lo);
             } else if (old != lo) {                 // initialised and hooked meanwhile
                 const uint32_t r = find_root(parent, old, parent[old], halve);
                 if (uhi) rv = r; else ru = r;
@@ -120,7 +126,7 @@ __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32
         const uint32_t expect = hf ? kInvalid : hi;
         const uint32_t old = atomicCAS(&parent[hi], expect, lo);
         if (old == expect) {                        // hooked: hi is no longer a root
-            if (hf) set_mark(sbits, hi);
+            if (hf) set_seen(sbits, hi);
             if (MARK) set_mark(mark, hi);
             if (STATS) ++st->hooks;
             return;
