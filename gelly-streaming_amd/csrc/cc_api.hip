@@ -75,6 +75,7 @@ struct gs_cc {
     void* tmp = nullptr;                 // emission temporaries
     size_t tmp_bytes = 0;
     bool compressed = true;
+    bool sbits_stale = false;            // a young launch skipped the seen bits: the next close rebuilds them
     uint64_t edges_since_reset = 0;      // drives the young-forest launch split (fold_impl)
     uint64_t ring_launches = 0;          // ring fold launches since reset (hot-set admission cadence)
     uint64_t closes = 0;                 // compressions since reset (giant re-sampled every kPickEvery)
@@ -132,6 +133,11 @@ hipEvent_t get_event(gs_cc_t* h) {
 // close c reads slot c & 1 and writes slot (c + 1) & 1; derr[5] = hot set owner, derr[6] = hot
 // set admission budget, derr[7] = warm set valid
 inline uint32_t* giant_state(gs_cc_t* h) { return h->derr + 1 + 2 * (h->closes & 1); }
+// derr[kWorkWord..+1]: the young k_fold's dynamic chunk counter, an atomicAdd per chunk from every
+// workgroup: on a 128-B line of its own, away from the giant state every union reads (sharing
+// its line made a hoisted read of the giant root 2.6x slower in window 1, profiles/r02_h)
+constexpr uint32_t kWorkWord = 32;
+constexpr size_t kDerrBytes = 256;
 
 // The events ride on the kernel dispatches themselves (hipExtLaunchKernelGGL start/stop events):
 // separate hipEventRecord marker packets are barrier packets, ~10 us of idle GPU each on gfx950
@@ -212,8 +218,16 @@ constexpr uint32_t kRingMinBits = 25;
 // warm set: counted in ring launch kWarmAt after reset (kWarmSample edges) and re-checked every
 // kWarmEvery-th launch (rebuilt only when invalid for the current giant); 4 band passes, hottest
 // first (2 bands: +0.17 ms per step; 2^24-edge samples: more hits, no faster once the count is paid)
+#if defined(GS_EXP_WS22)
+constexpr uint64_t kWarmAt = 3, kWarmEvery = 16, kWarmSample = 1ull << 22;
+#elif defined(GS_EXP_WS21)
+constexpr uint64_t kWarmAt = 3, kWarmEvery = 16, kWarmSample = 1ull << 21;
+#else
 constexpr uint64_t kWarmAt = 3, kWarmEvery = 16, kWarmSample = 1ull << 23;
-constexpr uint32_t kWarmBucketsMaxBits = 18;        // 2^18 x 4 B = 1 MiB table at RMAT-26
+#endif
+constexpr uint32_t kWarmBucketsMaxBits = 18;        // 2^18 x 4 B = 1 MiB table at RMAT-26 (2 MiB with
+                                                    // 2^24-edge samples: 5 us less per steady window,
+                                                    // 0.44 ms more count per step; profiles/r02_d)
 constexpr uint32_t kWarmBands[] = {0xFFFFFFFFu, 32u, 8u, 3u, 2u};
 constexpr uint32_t kHotThresh = 3;                  // sightings before hot-set admission (233 -> 229 us)
 // Young split: inside the young forest, close internally (compress + giant pick: no emission,
@@ -265,8 +279,15 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
                                   : grid_for((n + ept - 1) / ept, kFoldThreads, 16384);
     ensure_stats(h);
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
+    // a big young launch (>= capacity/16 edges, i.e. window 1 of the headline) leaves the seen
+    // bitmap to the close that follows it — a full pass in any case while the forest is this
+    // young — and saves one device-scope atomic per new vertex (window 1: ~6.4M)
+    if (young && !AOS && n >= h->cap / kYoungSplitDiv) {
+        f.sbits = nullptr;
+        h->sbits_stale = true;
+    }
     if (persist) {
-        f.work = reinterpret_cast<unsigned long long*>(h->derr + 8);
+        f.work = reinterpret_cast<unsigned long long*>(h->derr + kWorkWord);
         (void)hipMemsetAsync(f.work, 0, sizeof(unsigned long long), h->stream);
     }
     const bool vec = std::is_same<IdT, uint32_t>::value && !AOS &&
@@ -316,12 +337,13 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     const bool st = h->dstats != nullptr;
     const dim3 grid(grid_for(n / 4, kHotThreads, (unsigned)std::max(h->cus, 1)));
     hipEvent_t stop = build ? nullptr : t.stop();
+    hipEvent_t start = t.start();
     if (h->mark) {
-        if (st) klaunch(k_fold_ring<IdT, true, true>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
-        else klaunch(k_fold_ring<IdT, true, false>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
+        if (st) klaunch(k_fold_ring<IdT, true, true>, grid, dim3(kHotThreads), h->stream, start, stop, a, b, f, hot);
+        else klaunch(k_fold_ring<IdT, true, false>, grid, dim3(kHotThreads), h->stream, start, stop, a, b, f, hot);
     } else {
-        if (st) klaunch(k_fold_ring<IdT, false, true>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
-        else klaunch(k_fold_ring<IdT, false, false>, grid, dim3(kHotThreads), h->stream, t.start(), stop, a, b, f, hot);
+        if (st) klaunch(k_fold_ring<IdT, false, true>, grid, dim3(kHotThreads), h->stream, start, stop, a, b, f, hot);
+        else klaunch(k_fold_ring<IdT, false, false>, grid, dim3(kHotThreads), h->stream, start, stop, a, b, f, hot);
     }
     if (build) {
         // hottest band first: a full bucket then drops the colder ids
@@ -348,46 +370,62 @@ static uint64_t next_young_split(const gs_cc_t* h, uint64_t done) {
 
 int compress_impl(gs_cc_t* h);
 
-// UpdateCC over a batch of dense ids: the ring fold once the forest is mature, else young-forest
-// launches (one per batch, cut at the young limit and at the split point, which closes internally),
-// or for partial summaries (AOS) a head launch first.
+// A fold call longer than this many edges (past the young forest) closes internally between
+// chunks (compress + giant follow: no emission; labels stay canonical), so the giant filter keeps
+// up inside one huge window as it does across windows (one 2^30-edge window: 40.8 ms in one
+// launch with the filter frozen at 2^22 edges)
+constexpr uint64_t kInternalCloseEdges = 1ull << 24;
+
+static void internal_close(gs_cc_t* h) {
+    h->compressed = false;
+    (void)compress_impl(h);
+    h->compressed = false;
+}
+
+// UpdateCC over a batch of dense ids, cut into launches: young-forest launches (up to the young
+// limit, cut at the young split point, which closes internally), then mature launches of at most
+// kInternalCloseEdges edges with internal closes between them — the ring fold for aligned device
+// SoA batches where use_ring() holds, else k_fold. Partial summaries (AOS pairs) fold a short head
+// launch first, then the rest in one launch.
 template <typename IdT, bool AOS>
 void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, size_t esz) {
     const uint64_t young_limit = h->cap / 4;
-    // mature forest (past the young limit), aligned device SoA (32- or 64-bit ids): the steady ring fold
-    if (!AOS && h->hot && use_ring(h) && h->edges_since_reset >= young_limit && n >= 4 &&
-        ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0) {
-        const uint64_t done = n & ~(uint64_t)3;
-        launch_fold_ring<IdT>(h, reinterpret_cast<const IdT*>(a), reinterpret_cast<const IdT*>(b), done);
-        h->edges_since_reset += done;
-        if (done == n) return;
-        a += done * esz;
-        b += done * esz;
-        n -= done;
-    }
+    const size_t stride = AOS ? 2 * esz : esz;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
     uint64_t off = 0;
     while (off < n) {
         uint64_t m = n - off;
         const bool young = h->edges_since_reset < young_limit;
-        uint64_t sp = 0;
         if (young) {
             m = std::min(m, young_limit - h->edges_since_reset);
+            uint64_t sp = 0;
             if (!AOS && !h->sparse) {
                 sp = next_young_split(h, h->edges_since_reset);
                 if (sp) m = std::min(m, sp - h->edges_since_reset);
             }
-        } else if (AOS && off == 0 && n > kMergeBulk) {
-            m = std::min(m, kMergeHead);
+            launch_fold<IdT, AOS>(h, a + off * stride, b ? b + off * esz : nullptr, m, true);
+            h->edges_since_reset += m;
+            off += m;
+            if (sp && h->edges_since_reset == sp && off < n) internal_close(h);
+            continue;
         }
-        const size_t stride = AOS ? 2 * esz : esz;
-        launch_fold<IdT, AOS>(h, a + off * stride, b ? b + off * esz : nullptr, m, young);
+        if (AOS) {
+            if (off == 0 && n > kMergeBulk) m = std::min(m, kMergeHead);
+            launch_fold<IdT, AOS>(h, a + off * stride, nullptr, m, false);
+            h->edges_since_reset += m;
+            off += m;
+            continue;
+        }
+        m = std::min(m, kInternalCloseEdges);
+        if (h->hot && use_ring(h) && aligned && m >= 4) {
+            m &= ~(uint64_t)3;                          // the ring fold takes groups of 4 edges
+            launch_fold_ring<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
+        } else {
+            launch_fold<IdT, AOS>(h, a + off * stride, b + off * esz, m, false);
+        }
         h->edges_since_reset += m;
         off += m;
-        if (sp && h->edges_since_reset == sp && off < n) {
-            h->compressed = false;
-            (void)compress_impl(h);
-            h->compressed = false;
-        }
+        if (off < n && n - off >= 4) internal_close(h);   // (a tail of < 4 edges folds unclosed)
     }
 }
 
@@ -518,7 +556,9 @@ int compress_impl(gs_cc_t* h) {
                     in, (int)force);
         ++h->closes;
         klaunch(k_compress, dim3(grid_for(h->cap, 1024, kCompressGrid)), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
-                h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot);
+                h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot,
+                (int)h->sbits_stale);
+        h->sbits_stale = false;
     }
     GS_HIP(hipGetLastError());
     h->compressed = true;
@@ -704,7 +744,7 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
         h->mark = h->mark_buf;
     }
     if (hipMalloc(&h->gbits, mark_bytes(h->cap)) != hipSuccess || hipMalloc(&h->sbits, mark_bytes(h->cap)) != hipSuccess ||
-        hipMalloc(&h->derr, 64) != hipSuccess || hipMalloc(&h->dscratch, 8 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&h->derr, kDerrBytes) != hipSuccess || hipMalloc(&h->dscratch, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&h->hscratch, 8 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         return bail(fail(GS_ERR_NOMEM, "scratch allocation failed"));
@@ -814,6 +854,7 @@ int gs_cc_reset(gs_cc_t* h) {
         GS_HIP(hipMemsetAsync(h->nkeys, 0, sizeof(unsigned long long), h->stream));
     }
     h->compressed = true;
+    h->sbits_stale = false;
     h->minkey_valid = false;
     h->edges_since_reset = 0;
     h->closes = 0;

@@ -48,11 +48,15 @@ __device__ __forceinline__ uint32_t find_root(uint32_t* __restrict__ parent, uin
 __device__ __forceinline__ void set_mark(uint32_t* __restrict__ mark, uint32_t v) {
     __hip_atomic_fetch_or(&mark[v >> 5], 1u << (v & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// first touch: v's bit in the seen bitmap (experiment builds may drop it to measure its cost)
+// Measured and dropped (profiles/r02_g, r02_i): a new vertex hooked straight under the giant's
+// root setting its gbits bit instead (no close visit: closes -240 us per step) made the steady fold
+// 12 us slower per window — atomics into the bitmap the filter is reading push its lines out of
+// the L2s; skipping both bits left those vertices out of the filter (+4 us per steady window).
+// first touch: v's bit in the seen bitmap. sbits == nullptr: not kept by this launch (big young
+// folds: the next close is a full pass that rebuilds the bitmap from parent[], cc_api.hip
+// launch_fold) — one device-scope atomic less per new vertex
 __device__ __forceinline__ void set_seen(uint32_t* __restrict__ sbits, uint32_t v) {
-#ifndef GS_EXP_NOSBITS
-    set_mark(sbits, v);
-#endif
+    if (sbits) set_mark(sbits, v);
 }
 
 // Read-only root walk (no writes) for find() on const state.
@@ -875,15 +879,15 @@ __global__ __launch_bounds__(1024) void k_pick_giant(const uint32_t* __restrict_
 // the hot set when g is another component than the hot set's owner, and writes g to the output
 // slot as the next close's giant and the root gbits were built for.
 __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent, uint32_t n,
-                                                  uint32_t* __restrict__ gbits, const uint32_t* __restrict__ sbits,
+                                                  uint32_t* __restrict__ gbits, uint32_t* __restrict__ sbits,
                                                   const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                  uint32_t* __restrict__ owner, uint2* __restrict__ hot) {
+                                                  uint32_t* __restrict__ owner, uint2* __restrict__ hot, int rebuild_seen) {
     __shared__ uint32_t s_g, s_inc, s_clear;
     if (threadIdx.x == 0) {
         const uint32_t g0 = in[0];
         const uint32_t g = (g0 == kInvalid) ? kInvalid : find_root_ro(parent, g0);
         s_g = g;
-        s_inc = (g != kInvalid && g == in[1]) ? 1u : 0u;
+        s_inc = (g != kInvalid && g == in[1] && !rebuild_seen) ? 1u : 0u;
         s_clear = 0;
         if (blockIdx.x == 0) {
             if (g != kInvalid) {
@@ -959,7 +963,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                 const uint32_t v = base + k;
                 gp[k] = (p[k] != kInvalid && p[k] != v) ? parent[p[k]] : p[k];
             }
-            uint32_t nib = 0;
+            uint32_t nib = 0, seen = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const uint32_t v = base + k;
@@ -969,12 +973,20 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                     parent[v] = lab;
                 }
                 nib |= (lab == g && lab != kInvalid) ? (1u << k) : 0u;
+                seen |= (p[k] != kInvalid) ? (1u << k) : 0u;
             }
             uint32_t word = nib << (4 * (lane & 7));
             word |= __shfl_xor(word, 1, 64);
             word |= __shfl_xor(word, 2, 64);
             word |= __shfl_xor(word, 4, 64);
             if ((lane & 7) == 0 && base < n) gbits[base >> 5] = word;
+            {                                        // the seen bitmap, exact again after every full pass
+                uint32_t sw = seen << (4 * (lane & 7));
+                sw |= __shfl_xor(sw, 1, 64);
+                sw |= __shfl_xor(sw, 2, 64);
+                sw |= __shfl_xor(sw, 4, 64);
+                if ((lane & 7) == 0 && base < n) sbits[base >> 5] = sw;
+            }
         }
     }
 }

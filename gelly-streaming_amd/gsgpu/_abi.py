@@ -76,6 +76,15 @@ def lib() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
         raise GsgpuUnavailable("libgsgpu.so not found at %s — build it with `make -C gelly-streaming_amd` "
                                "(or __graft_entry__.build()); there is no CPU fallback" % LIB_PATH)
+    # One HIP runtime per process: torch's bundled ROCm libraries ask for "libamdhip64.so" (no
+    # version), libgsgpu.so for "libamdhip64.so.7". Loaded after torch, libgsgpu binds to torch's
+    # runtime (its soname IS libamdhip64.so.7, likewise librccl.so.1); loaded first, it would pull
+    # /opt/rocm's and torch would then load a second runtime next to it (two HSA teardowns at
+    # exit: "double free or corruption"). So torch, when importable, is loaded first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     try:
         L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     except OSError as e:  # pragma: no cover - depends on the box

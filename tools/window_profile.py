@@ -30,3 +30,8 @@ for rep in range(2):
     ds.timing(False)
 for r in rows:
     print("window %3d  fold %8.1f us  close %6.1f us" % r, file=sys.stderr if False else sys.stdout, flush=True)
+young = [r for r in rows if r[0] <= 12]
+steady = [r for r in rows if r[0] > 12]
+print("summary: fold w1 %.1f us, w2-12 %.1f us, steady mean %.1f us (%d windows), close total %.1f us, step fold+close %.1f us"
+      % (rows[0][1], sum(r[1] for r in young[1:]), sum(r[1] for r in steady) / max(len(steady), 1), len(steady),
+         sum(r[2] for r in rows), sum(r[1] + r[2] for r in rows)), flush=True)
