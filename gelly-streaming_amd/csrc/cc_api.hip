@@ -60,9 +60,9 @@ struct gs_cc {
     int device = 0;
     hipStream_t own = nullptr, stream = nullptr;
     uint32_t* parent = nullptr;          // dense summary / label array
-    uint32_t* mark = nullptr;            // export mark bitmap, 1 bit per vertex (GS_CC_TRACK_MARKS)
-    uint32_t* mark_buf = nullptr;        // the mark allocation (mark = mark_buf while marking, else null)
-    uint32_t* export_bcnt = nullptr;     // per-workgroup mark counts of an export (kExportBlocks words)
+    uint32_t* mark = nullptr;            // hook log while marking (GS_CC_TRACK_MARKS), else null
+    uint32_t* mark_buf = nullptr;        // the hook log: 2 x capacity entries (cc_kernels.hpp log_append)
+    unsigned long long* mark_ctr = nullptr;   // [log length, export cursor], a 128-B line of its own
     uint32_t* gbits = nullptr;           // giant-component filter bitmap (1 bit per vertex)
     uint32_t* sbits = nullptr;           // seen bitmap (1 bit per vertex), set on first touch
     uint32_t* derr = nullptr;            // derr[0] deferred device error flags; derr[1..5] giant state
@@ -279,6 +279,7 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
                                   : grid_for((n + ept - 1) / ept, kFoldThreads, 16384);
     ensure_stats(h);
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
+    f.mark_len = h->mark_ctr;
     // a big young launch (>= capacity/16 edges, i.e. window 1 of the headline) leaves the seen
     // bitmap to the close that follows it — a full pass in any case while the forest is this
     // young — and saves one device-scope atomic per new vertex (window 1: ~6.4M)
@@ -333,6 +334,7 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     hot.wcnt = build ? h->wcnt : nullptr;
     hot.count_edges = build ? kWarmSample : 0;
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
+    f.mark_len = h->mark_ctr;
     KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_RING : h->fold_timer);
     const bool st = h->dstats != nullptr;
     const dim3 grid(grid_for(n / 4, kHotThreads, (unsigned)std::max(h->cus, 1)));
@@ -445,6 +447,7 @@ void launch_fold_sparse(gs_cc_t* h, const int64_t* a, const int64_t* b, uint64_t
         if (h->edges_since_reset < young_limit)
             m = std::min(m, std::max<uint64_t>(std::min(kSparseYoungChunk, young_limit - h->edges_since_reset), 1));
         FoldArgs f{m, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
+        f.mark_len = h->mark_ctr;
         const unsigned grid = grid_for((m + 1) / 2, 256, 16384);
         KTimer t(h, h->fold_timer);
         const int64_t* pa = a + (aos ? 2 * off : off);
@@ -693,7 +696,7 @@ static int export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long
 int cc_export_async(gs_cc_t* h, void* pairs, uint64_t cap, unsigned long long* dcount) {
     GS_TRY(check(h));
     if (!h->mark_buf || h->sparse) return fail(GS_ERR_UNSUPPORTED, "export: no marks on this handle");
-    if (cap < h->cap) return fail(GS_ERR_CAPACITY, "export: capacity %llu < vertex capacity %u", (unsigned long long)cap, h->cap);
+    if (cap < 2ull * h->cap) return fail(GS_ERR_CAPACITY, "export: capacity %llu < 2 x vertex capacity %u", (unsigned long long)cap, h->cap);
     DeviceGuard g(h->device);
     return export_launch(h, pairs, cap, dcount);
 }
@@ -712,6 +715,8 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
     if (cfg->id_bits != 32 && cfg->id_bits != 64) return fail(GS_ERR_INVALID, "gs_cc_create: id_bits must be 32 or 64");
     const bool sparse = (cfg->flags & GS_CC_SPARSE_IDS) != 0;
     if (sparse && cfg->id_bits != 64) return fail(GS_ERR_INVALID, "gs_cc_create: GS_CC_SPARSE_IDS needs id_bits 64");
+    if (sparse && (cfg->flags & GS_CC_TRACK_MARKS))
+        return fail(GS_ERR_UNSUPPORTED, "gs_cc_create: GS_CC_TRACK_MARKS needs dense ids (the exchange is dense-id)");
     if (sparse && (cfg->vertex_capacity == 0 || cfg->vertex_capacity > (1ull << 30)))
         return fail(GS_ERR_INVALID, "gs_cc_create: sparse vertex_capacity must be in [1, 2^30]");
     if (cfg->vertex_capacity == 0 || cfg->vertex_capacity > 0xFFFFFFFFull)
@@ -739,8 +744,8 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
     h->stream = h->own;
     if (hipMalloc(&h->parent, (size_t)h->cap * sizeof(uint32_t)) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "parent[%u] allocation failed", h->cap)); }
     if (cfg->flags & GS_CC_TRACK_MARKS) {
-        if (hipMalloc(&h->mark_buf, mark_bytes(h->cap)) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "mark allocation failed")); }
-        if (hipMalloc(&h->export_bcnt, kExportBlocks * sizeof(uint32_t)) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "export count allocation failed")); }
+        if (hipMalloc(&h->mark_buf, (size_t)h->cap * 2 * sizeof(uint32_t)) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "hook log allocation failed")); }
+        if (hipMalloc(&h->mark_ctr, 128) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "hook log counter allocation failed")); }
         h->mark = h->mark_buf;
     }
     if (hipMalloc(&h->gbits, mark_bytes(h->cap)) != hipSuccess || hipMalloc(&h->sbits, mark_bytes(h->cap)) != hipSuccess ||
@@ -803,7 +808,7 @@ int gs_cc_destroy(gs_cc_t* h) {
     for (auto e : h->pool) (void)hipEventDestroy(e);
     if (h->parent) (void)hipFree(h->parent);
     if (h->mark_buf) (void)hipFree(h->mark_buf);
-    if (h->export_bcnt) (void)hipFree(h->export_bcnt);
+    if (h->mark_ctr) (void)hipFree(h->mark_ctr);
     if (h->derr) (void)hipFree(h->derr);
     if (h->gbits) (void)hipFree(h->gbits);
     if (h->sbits) (void)hipFree(h->sbits);
@@ -834,7 +839,7 @@ int gs_cc_reset(gs_cc_t* h) {
     GS_TRY(check(h));
     DeviceGuard g(h->device);
     GS_HIP(hipMemsetAsync(h->parent, 0xFF, (size_t)h->cap * sizeof(uint32_t), h->stream));
-    if (h->mark_buf) GS_HIP(hipMemsetAsync(h->mark_buf, 0, mark_bytes(h->cap), h->stream));
+    if (h->mark_ctr) GS_HIP(hipMemsetAsync(h->mark_ctr, 0, 2 * sizeof(unsigned long long), h->stream));
     GS_HIP(hipMemsetAsync(h->gbits, 0, mark_bytes(h->cap), h->stream));
     GS_HIP(hipMemsetAsync(h->sbits, 0, mark_bytes(h->cap), h->stream));
     // giant state (cc_kernels.hpp, giant_state()): both slots no giant / gbits built for none,
@@ -920,13 +925,14 @@ int gs_cc_merge(gs_cc_t* into, gs_cc_t* from) {
         KTimer t(into, GS_K_MERGE);
         const dim3 grid(grid_for(from->cap, 256, 16384));
         FoldArgs f{0, into->parent, into->mark, into->sbits, into->gbits, giant_state(into), RangeCheck{into->cap, into->derr}, nullptr};
+        f.mark_len = into->mark_ctr;
         if (into->mark) klaunch(k_merge_sparse<true>, grid, dim3(256), into->stream, t.start(), t.stop(), (const uint32_t*)from->parent, sparse_args(from), f, sparse_args(into));
         else klaunch(k_merge_sparse<false>, grid, dim3(256), into->stream, t.start(), t.stop(), (const uint32_t*)from->parent, sparse_args(from), f, sparse_args(into));
     } else {
         KTimer t(into, GS_K_MERGE);
         const dim3 grid(grid_for(from->cap, 256, 16384));
-        if (into->mark) klaunch(k_merge_dense<true>, grid, dim3(256), into->stream, t.start(), t.stop(), (const uint32_t*)from->parent, from->cap, into->parent, into->mark, into->sbits);
-        else klaunch(k_merge_dense<false>, grid, dim3(256), into->stream, t.start(), t.stop(), (const uint32_t*)from->parent, from->cap, into->parent, into->mark, into->sbits);
+        if (into->mark) klaunch(k_merge_dense<true>, grid, dim3(256), into->stream, t.start(), t.stop(), (const uint32_t*)from->parent, from->cap, into->parent, into->mark, into->mark_ctr, into->sbits);
+        else klaunch(k_merge_dense<false>, grid, dim3(256), into->stream, t.start(), t.stop(), (const uint32_t*)from->parent, from->cap, into->parent, into->mark, into->mark_ctr, into->sbits);
     }
     GS_HIP(hipGetLastError());
     if (from->stream != into->stream) {   // `from` must not be reused before the merge read it
@@ -1101,14 +1107,14 @@ int gs_cc_labels_device(gs_cc_t* h, const void** p) {
 }
 
 int gsgpu::export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long* counter) {
-    // one workgroup per contiguous range of mark words
-    const dim3 grid(grid_for((h->cap + 31) / 32, 256, kExportBlocks));
+    // the pending hook-log entries -> (v, root(v)) pairs; the grid is fixed (the count is on the
+    // device): a steady window's few thousand hooks need a few workgroups, a young one's millions
+    // are strided over 1024
     {
         KTimer t(h, GS_K_EXPORT);
-        klaunch(k_export_count, grid, dim3(256), h->stream, t.start(), nullptr,
-                (const uint32_t*)h->mark_buf, h->cap, h->export_bcnt);
-        klaunch(k_export_marks, grid, dim3(256), h->stream, nullptr, t.stop(),
-                h->mark_buf, (const uint32_t*)h->parent, h->cap, (uint32_t*)out, cap, (const uint32_t*)h->export_bcnt, counter);
+        klaunch(k_export_log, dim3(1024), dim3(256), h->stream, t.start(), nullptr, (const uint32_t*)h->mark_buf,
+                (const unsigned long long*)h->mark_ctr, (const uint32_t*)h->parent, (uint32_t*)out, cap, counter);
+        klaunch(k_log_advance, dim3(1), dim3(1), h->stream, nullptr, t.stop(), h->mark_ctr, cap);
     }
     GS_HIP(hipGetLastError());
     return GS_OK;
@@ -1151,8 +1157,8 @@ int gs_cc_export_marks_async(gs_cc_t* h, void* pairs, uint64_t cap, void* dev_co
     GS_TRY(export_check(h, "gs_cc_export_marks_async"));
     if (!dev_count || !is_device_pointer(dev_count) || (cap && (!pairs || !is_device_pointer(pairs))))
         return fail(GS_ERR_INVALID, "gs_cc_export_marks_async: pairs and dev_count must be device pointers");
-    if (cap < h->cap) return fail(GS_ERR_CAPACITY, "gs_cc_export_marks_async: capacity %llu < vertex capacity %u",
-                                  (unsigned long long)cap, h->cap);
+    if (cap < 2ull * h->cap) return fail(GS_ERR_CAPACITY, "gs_cc_export_marks_async: capacity %llu < 2 x vertex capacity %u",
+                                         (unsigned long long)cap, h->cap);
     DeviceGuard g(h->device);
     return export_launch(h, pairs, cap, static_cast<unsigned long long*>(dev_count));
 }

@@ -77,27 +77,27 @@ __device__ __forceinline__ uint32_t make_set(uint32_t* __restrict__ parent, uint
     return v;
 }
 
-// union(u, v) given the parent words read by the caller. MARK: record hooked roots and
-// self-loop first touches in mark[] for the partial-summary export.
+// union(u, v) given the parent words read by the caller. Returns the vertex the partial-summary
+// export must carry (MARK: the root it hooked, or a self-loop's first touch; kInvalid if none):
+// the caller appends it to the handle's hook log (log_append).
 // per-thread diagnostic counters (GSGPU_FOLD_STATS=1 builds the STATS variant of k_fold)
 struct FoldStats {
     uint32_t early = 0, hooks = 0, casfail = 0, inits = 0;
 };
 
 template <bool MARK, bool STATS = false>
-__device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32_t* __restrict__ mark,
-                                           uint32_t* __restrict__ sbits,
-                                           uint32_t u, uint32_t v, uint32_t pu, uint32_t pv,
-                                           FoldStats* st = nullptr, bool halve = true) {
+__device__ __forceinline__ uint32_t union_edge(uint32_t* __restrict__ parent, uint32_t* __restrict__ sbits,
+                                               uint32_t u, uint32_t v, uint32_t pu, uint32_t pv,
+                                               FoldStats* st = nullptr, bool halve = true) {
     if (u == v) {                                   // union(u,u): makeSet only
         if (pu == kInvalid) {
             const uint32_t old = atomicCAS(&parent[u], kInvalid, u);
             if (old == kInvalid) {
                 set_seen(sbits, u);
-                if (MARK) set_mark(mark, u);
+                if (MARK) return u;
             }
         }
-        return;
+        return kInvalid;
     }
     // A side whose word was read as kInvalid is a fresh vertex: it is a root of its own, and if
     // it ends up the larger root it is hooked straight from kInvalid (one CAS instead of an
@@ -107,7 +107,7 @@ __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32
     if (STATS) st->inits += fu + fv;
     if (!fu && !fv && pu == pv) {                   // common parent: already one component
         if (STATS) ++st->early;
-        return;
+        return kInvalid;
     }
     uint32_t ru = fu ? u : find_root(parent, u, pu, halve);
     uint32_t rv = fv ? v : find_root(parent, v, pv, halve);
@@ -131,9 +131,8 @@ __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32
         const uint32_t old = atomicCAS(&parent[hi], expect, lo);
         if (old == expect) {                        // hooked: hi is no longer a root
             if (hf) set_seen(sbits, hi);
-            if (MARK) set_mark(mark, hi);
             if (STATS) ++st->hooks;
-            return;
+            return MARK ? hi : kInvalid;
         }
         if (STATS) ++st->casfail;
         hf = false;
@@ -144,8 +143,45 @@ __device__ __forceinline__ void union_edge(uint32_t* __restrict__ parent, uint32
         const uint32_t r = find_root(parent, old, parent[old], halve);
         if (uhi) ru = r; else rv = r;
     }
+    return kInvalid;
 }
 
+
+// Hook log (GS_CC_TRACK_MARKS): the vertices a partial-summary export carries, appended in
+// launch order. Wave-aggregated: one atomicAdd on the log length per wave call (the active lanes'
+// entries are written contiguously), so a window's few hooks cost no per-hook same-address atomic
+// and the export reads just the log instead of scanning a V-bit bitmap. Works with any set of
+// active lanes (ballots over the exec mask). Every vertex is hooked at most once and first-touched
+// by a self-loop at most once between resets, so 2 x capacity entries never overflow.
+template <int EPT>
+__device__ __forceinline__ void log_append(uint32_t* __restrict__ log, unsigned long long* __restrict__ len,
+                                           const uint32_t (&m)[EPT]) {
+    const uint64_t lt = (1ull << __lane_id()) - 1;
+    uint64_t masks[EPT];
+    uint32_t total = 0;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        masks[k] = __ballot(m[k] != kInvalid);
+        total += (uint32_t)__popcll(masks[k]);
+    }
+    if (total == 0) return;                          // uniform over the active lanes
+    const uint64_t active = __ballot(1);
+    const int leader = __ffsll((long long)active) - 1;
+    uint32_t lo = 0, hi = 0;
+    if ((int)__lane_id() == leader) {
+        const unsigned long long b = atomicAdd(len, (unsigned long long)total);
+        lo = (uint32_t)b;
+        hi = (uint32_t)(b >> 32);
+    }
+    lo = __shfl(lo, leader, 64);
+    hi = __shfl(hi, leader, 64);
+    uint64_t pos = ((uint64_t)hi << 32) | lo;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        if (m[k] != kInvalid) log[pos + __popcll(masks[k] & lt)] = m[k];
+        pos += __popcll(masks[k]);
+    }
+}
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -171,7 +207,7 @@ constexpr int kEdgesPerThread = 4;          // default; k_fold takes EPT as a te
 struct FoldArgs {
     uint64_t n;
     uint32_t* parent;
-    uint32_t* mark;
+    uint32_t* mark;                       // hook log (GS_CC_TRACK_MARKS, marking on), or null
     uint32_t* sbits;
     const uint32_t* gbits;
     const uint32_t* giant;
@@ -179,6 +215,7 @@ struct FoldArgs {
     unsigned long long* stats;   // STATS: [valid, filtered, early, hooks, casfail, inits]
     uint32_t halve = 1;          // path halving in root walks (find_root)
     unsigned long long* work = nullptr;   // k_fold: dynamic chunk counter (young forest), or null
+    unsigned long long* mark_len = nullptr;   // MARK: the hook log's length word (mark = the log)
 };
 
 // ---- LDS hot set (steady state) ----
@@ -436,9 +473,11 @@ __device__ __forceinline__ void union_group(const FoldArgs& f, const uint32_t (&
         pu[k] = ok[k] ? f.parent[u[k]] : 0u;
         pv[k] = ok[k] ? f.parent[v[k]] : 0u;
     }
+    uint32_t m[EPT];
 #pragma unroll
     for (int k = 0; k < EPT; ++k)
-        if (ok[k]) union_edge<MARK, STATS>(f.parent, f.mark, f.sbits, u[k], v[k], pu[k], pv[k], &st, f.halve != 0);
+        m[k] = ok[k] ? union_edge<MARK, STATS>(f.parent, f.sbits, u[k], v[k], pu[k], pv[k], &st, f.halve != 0) : kInvalid;
+    if (MARK) log_append<EPT>(f.mark, f.mark_len, m);
 }
 
 // As union_group, for survivors whose giant flags are known (bit 0: u in the giant, bit 1: v): a
@@ -461,9 +500,11 @@ __device__ __forceinline__ void union_group_g(const FoldArgs& f, const uint32_t 
         pu[k] = !ok[k] ? 0u : (gflag[k] & 1u) ? gR : f.parent[u[k]];
         pv[k] = !ok[k] ? 0u : (gflag[k] & 2u) ? gR : f.parent[v[k]];
     }
+    uint32_t m[EPT];
 #pragma unroll
     for (int k = 0; k < EPT; ++k)
-        if (ok[k]) union_edge<MARK, STATS>(f.parent, f.mark, f.sbits, u[k], v[k], pu[k], pv[k], &st, f.halve != 0);
+        m[k] = ok[k] ? union_edge<MARK, STATS>(f.parent, f.sbits, u[k], v[k], pu[k], pv[k], &st, f.halve != 0) : kInvalid;
+    if (MARK) log_append<EPT>(f.mark, f.mark_len, m);
 }
 
 // Filter, parent gathers and unions of one thread's EPT edges (ids already range-checked;
@@ -773,13 +814,14 @@ __global__ void k_warm_done(uint32_t* __restrict__ valid) { *valid = 1u; }
 // every v in other (DisjointSet.java:127-131 iterates other.getMatches()).
 template <bool MARK>
 __global__ __launch_bounds__(256) void k_merge_dense(const uint32_t* __restrict__ other, uint32_t n_other,
-                                                     uint32_t* __restrict__ parent, uint32_t* __restrict__ mark,
+                                                     uint32_t* __restrict__ parent, uint32_t* __restrict__ log,
+                                                     unsigned long long* __restrict__ log_len,
                                                      uint32_t* __restrict__ sbits) {
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n_other; v += stride) {
         const uint32_t p = other[v];
-        if (p == kInvalid) continue;
-        union_edge<MARK>(parent, mark, sbits, v, p, parent[v], parent[p]);
+        const uint32_t m[1] = {p == kInvalid ? kInvalid : union_edge<MARK>(parent, sbits, v, p, parent[v], parent[p])};
+        if (MARK) log_append<1>(log, log_len, m);
     }
 }
 
@@ -1135,145 +1177,33 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_scatter(const uint32_t* _
     }
 }
 
-// Partial-summary export (multi-GPU CombineCC): every marked vertex v (a root hooked since the
-// last export, or a self-loop first touch) becomes the pair (v, root(v)); its mark is cleared.
-// Roots, not the parent words at hook time: the receiver's unions then all point at the few
-// component minima its own forest already holds (short walks, no hook chains to contend on).
-// Each workgroup owns a contiguous range of mark words: it counts them, takes its output range with
-// ONE atomicAdd on the shared counter (one per wave serialised ~32K same-address atomics: 400 us
-// per RMAT-26 window, tools/sim_ranks.py), then scatters tile by tile (block-wide scan). Pairs
-// past `cap` are not written and keep their marks for the next export. Each mark word is one
-// thread's, so its plain clear cannot race with another workgroup's store.
-// Each lane reads 4 mark words at once (16 B): a workgroup's range is 2 passes of 256 quads at
-// RMAT-26 instead of 8 dependent passes of 256 words (the scan and the root walks of one pass
-// wait on its loads).
-constexpr int kExportBlocks = 1024;
-constexpr uint32_t kExportList = 4096;              // marks listed per tile (16 KiB of LDS)
-__device__ __forceinline__ uint4 load_mark_quad(const uint32_t* mark, uint32_t q, uint32_t nwords) {
-    const uint32_t w = q << 2;
-    if (w + 3 < nwords) return reinterpret_cast<const uint4*>(mark)[q];
-    uint4 r;
-    r.x = w < nwords ? mark[w] : 0u;
-    r.y = w + 1 < nwords ? mark[w + 1] : 0u;
-    r.z = w + 2 < nwords ? mark[w + 2] : 0u;
-    r.w = 0u;
-    return r;
-}
-// Pass 1: each workgroup counts the marks of its range into bcnt[blockIdx.x] (plain store: no
-// same-address atomics; one atomicAdd per workgroup on a shared counter serialised at ~12 ns
-// each, ~12 us of a 23 us export at 1024 workgroups).
-__device__ __forceinline__ void export_range(uint32_t n, uint32_t& nwords, uint32_t& lo, uint32_t& hi) {
-    nwords = (n + 31) >> 5;
-    const uint32_t nquads = (nwords + 3) >> 2;
-    const uint32_t per = (nquads + gridDim.x - 1) / gridDim.x;
-    lo = min(blockIdx.x * per, nquads);
-    hi = min(lo + per, nquads);
-}
-__global__ __launch_bounds__(256) void k_export_count(const uint32_t* __restrict__ mark, uint32_t n,
-                                                      uint32_t* __restrict__ bcnt) {
-    __shared__ uint32_t s_wave[4];
-    uint32_t nwords, lo, hi;
-    export_range(n, nwords, lo, hi);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t c = 0;
-    for (uint32_t q = lo + threadIdx.x; q < hi; q += blockDim.x) {
-        const uint4 m = load_mark_quad(mark, q, nwords);
-        c += __popc(m.x) + __popc(m.y) + __popc(m.z) + __popc(m.w);
+// Partial-summary export (multi-GPU CombineCC): every pending hook-log entry v (a root hooked
+// since the last export, or a self-loop first touch) becomes the pair (v, root(v)). Roots, not
+// the parent words at hook time: the receiver's unions then all point at the few component minima
+// its own forest already holds (short walks, no hook chains to contend on). ctr = [length, read
+// cursor]; the pending entries are [cursor, length); *count receives their number; at most cap
+// pairs are written, the rest stay pending (k_log_advance). One thread per entry: the export
+// costs O(hooks) instead of a scan of a V-bit mark bitmap (23 us per RMAT-26 window).
+__global__ __launch_bounds__(256) void k_export_log(const uint32_t* __restrict__ log, const unsigned long long* __restrict__ ctr,
+                                                    const uint32_t* __restrict__ parent, uint32_t* __restrict__ pairs,
+                                                    uint64_t cap, unsigned long long* __restrict__ count) {
+    const unsigned long long len = ctr[0], rd = ctr[1];
+    const unsigned long long n = len - rd;
+    const unsigned long long take = n < cap ? n : cap;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *count = n;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < take;
+         i += (unsigned long long)gridDim.x * blockDim.x) {
+        const uint32_t v = log[rd + i];
+        pairs[2 * i] = v;
+        pairs[2 * i + 1] = find_root_ro(parent, v);
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
-    if (lane == 0) s_wave[wave] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) bcnt[blockIdx.x] = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
 }
-
-// Pass 2 (same grid): a workgroup's output offset is the sum of the counts of the workgroups
-// before it (4 KiB of bcnt at 1024 workgroups, reduced by the workgroup); the last workgroup
-// stores the total into *counter (no memset, no atomics). Then the scatter, tile by tile.
-__global__ __launch_bounds__(256) void k_export_marks(uint32_t* __restrict__ mark, const uint32_t* __restrict__ parent,
-                                                      uint32_t n, uint32_t* __restrict__ pairs, uint64_t cap,
-                                                      const uint32_t* __restrict__ bcnt,
-                                                      unsigned long long* __restrict__ counter) {
-    __shared__ unsigned long long s_red[4];
-    __shared__ uint32_t s_wave[4];
-    __shared__ uint32_t s_list[kExportList];
-    uint32_t nwords, lo, hi;
-    export_range(n, nwords, lo, hi);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    unsigned long long before = 0;
-    for (uint32_t i = threadIdx.x; i < blockIdx.x; i += blockDim.x) before += bcnt[i];
-    before = wave_sum(before);
-    if (lane == 0) s_red[wave] = before;
-    __syncthreads();
-    unsigned long long base = s_red[0] + s_red[1] + s_red[2] + s_red[3];
-    const uint32_t mine = bcnt[blockIdx.x];
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *counter = base + mine;
-    if (mine == 0) return;                                       // nothing marked here (uniform)
-    for (uint32_t q0 = lo; q0 < hi; q0 += blockDim.x) {          // uniform over the block
-        const uint32_t q = q0 + threadIdx.x;
-        const uint4 m4 = (q < hi) ? load_mark_quad(mark, q, nwords) : make_uint4(0u, 0u, 0u, 0u);
-        const uint32_t cnt = __popc(m4.x) + __popc(m4.y) + __popc(m4.z) + __popc(m4.w);
-        uint32_t incl = cnt;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += y;
-        }
-        __syncthreads();                                         // s_wave free
-        if (lane == 63) s_wave[wave] = incl;
-        __syncthreads();
-        uint32_t woff = 0, tile = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            woff += (i < wave) ? s_wave[i] : 0u;
-            tile += s_wave[i];
-        }
-        unsigned long long pos = base + woff + incl - cnt;
-        const unsigned long long tbase = base;                   // the tile's first output index
-        base += tile;
-        // a tile of at most kExportList marks is listed in LDS and its root walks are spread over
-        // all 256 threads (one word's marks would otherwise walk one after another on one lane)
-        const bool listed = tile <= kExportList;                 // uniform
-        if (cnt) {
-            const uint32_t mw[4] = {m4.x, m4.y, m4.z, m4.w};
-            uint32_t li = woff + incl - cnt;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                uint32_t m = mw[k];
-                if (!m) continue;
-                const uint32_t w = (q << 2) + k;
-                uint32_t keep = 0;
-                while (m) {
-                    const int b = __ffs(m) - 1;
-                    m &= m - 1;
-                    const uint32_t v = (w << 5) + b;
-                    if (pos < cap) {
-                        if (listed) {
-                            s_list[li] = v;
-                        } else {
-                            pairs[2 * pos] = v;
-                            pairs[2 * pos + 1] = find_root_ro(parent, v);
-                        }
-                    } else {
-                        keep |= 1u << b;            // overflowing marks stay for the next export
-                    }
-                    ++pos;
-                    ++li;
-                }
-                mark[w] = keep;
-            }
-        }
-        if (listed && tile) {
-            __syncthreads();                                     // s_list complete
-            const uint32_t nval = tbase >= cap ? 0u : (uint32_t)min((unsigned long long)tile, cap - tbase);
-            for (uint32_t i = threadIdx.x; i < nval; i += blockDim.x) {
-                const uint32_t v = s_list[i];
-                pairs[2 * (tbase + i)] = v;
-                pairs[2 * (tbase + i) + 1] = find_root_ro(parent, v);
-            }
-            // s_list is rewritten only after the next tile's first __syncthreads
-        }
-    }
+// after k_export_log (stream order): consume what it wrote; an emptied log restarts at 0
+__global__ void k_log_advance(unsigned long long* __restrict__ ctr, uint64_t cap) {
+    const unsigned long long len = ctr[0], rd = ctr[1];
+    const unsigned long long take = (len - rd) < cap ? (len - rd) : cap;
+    if (rd + take == len) { ctr[0] = 0; ctr[1] = 0; }
+    else ctr[1] = rd + take;
 }
 
 }  // namespace gsgpu

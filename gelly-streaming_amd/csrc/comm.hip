@@ -92,7 +92,7 @@ struct gs_comm {
     hipEvent_t ev_ready = nullptr, ev_done = nullptr;
     // exchange buffers (device), sized at the first merge for the handle's capacity
     uint64_t cap_pairs = 0;
-    uint32_t* sendbuf = nullptr;                   // 2 * cap_pairs words
+    uint32_t* sendbuf = nullptr;                   // cap_pairs pairs (2 x the handle's capacity)
     uint32_t* recvbuf = nullptr;                   // grows: world * m pairs
     size_t recv_bytes = 0;
     unsigned long long* dcnt = nullptr;            // [world + 1]: all-gathered counts, [world] own/received
@@ -207,15 +207,16 @@ int prepare(gs_comm_t* c, gs_cc_t* h, CcInfo* info) {
     if (!info->marks) return fail(GS_ERR_UNSUPPORTED, "gs_cc_merge_window: handle created without GS_CC_TRACK_MARKS");
     if (info->device != c->device) return fail(GS_ERR_INVALID, "gs_cc_merge_window: handle on device %d, communicator on %d",
                                                info->device, c->device);
-    if (c->cap_pairs < info->cap) {
+    const uint64_t need = 2ull * info->cap;        // an export never exceeds 2 x capacity pairs
+    if (c->cap_pairs < need) {
         if (c->sendbuf) (void)hipFree(c->sendbuf);
         c->sendbuf = nullptr;
-        if (hipMalloc(&c->sendbuf, (size_t)info->cap * 8) != hipSuccess) {
+        if (hipMalloc(&c->sendbuf, (size_t)need * 8) != hipSuccess) {
             (void)hipGetLastError();
             c->cap_pairs = 0;
-            return fail(GS_ERR_NOMEM, "exchange buffer of %u pairs", info->cap);
+            return fail(GS_ERR_NOMEM, "exchange buffer of %llu pairs", (unsigned long long)need);
         }
-        c->cap_pairs = info->cap;
+        c->cap_pairs = need;
     }
     return GS_OK;
 }

@@ -314,7 +314,8 @@ class AllgatherMerge:
         self.dcnt = None
         if self.device.type == "cuda" and hasattr(summary, "export_marks_async"):
             self.dcnt = self.cnt if self.cnt.is_cuda else torch.zeros(1, dtype=torch.int64, device=self.device)
-        self.sendbuf = torch.empty(2 * self.cap, dtype=torch.int32, device=self.device)
+        # an export holds at most 2 x capacity pairs (include/gsgpu.h gs_cc_export_marks_async)
+        self.sendbuf = torch.empty(4 * self.cap, dtype=torch.int32, device=self.device)
         self.recvbuf = torch.empty(2 * self.world, dtype=torch.int32, device=self.device)   # grows
         self.hsend = torch.empty(0, dtype=torch.int32)
         self.hrecv = torch.empty(0, dtype=torch.int32)

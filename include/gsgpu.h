@@ -129,16 +129,17 @@ int gs_cc_find_flags(gs_cc_t* h, const void* ids, void* roots, uint8_t* found, u
 int gs_cc_labels_device(gs_cc_t* h, const void** dev_ptr);
 
 /* ---- partial-summary exchange (windowAll / tree merge) ----
- * Requires GS_CC_TRACK_MARKS. Writes the (vertex, root) pairs (uint32, interleaved) of every
- * vertex whose root status changed in this handle since the last export (roots it hooked,
- * singletons made by self-loops), and clears those marks. Folding these pairs into another
+ * Requires GS_CC_TRACK_MARKS (dense ids). Writes the (vertex, root) pairs (uint32, interleaved) of
+ * every vertex whose root status changed in this handle since the last export (roots it hooked,
+ * singletons made by self-loops: the handle's hook log, at most 2 x vertex_capacity entries), and
+ * consumes them; pairs past cap stay for the next export. Folding these pairs into another
  * summary (gs_cc_fold_pairs, 32-bit ids regardless of id_bits via gs_cc_fold_pairs32) transfers
  * all connectivity this handle gained. */
 int gs_cc_export_marks(gs_cc_t* h, void* pairs, uint64_t cap, uint64_t* n_out);
 int gs_cc_fold_pairs32(gs_cc_t* h, const void* pairs, uint64_t n);
 /* as gs_cc_export_marks, but only enqueued on the handle's stream: the pair count lands in the
  * device uint64 *dev_count (no host synchronisation; a collective can take it from there).
- * pairs and dev_count are device pointers; cap must be >= vertex_capacity (never overflows). */
+ * pairs and dev_count are device pointers; cap must be >= 2 x vertex_capacity (never overflows). */
 int gs_cc_export_marks_async(gs_cc_t* h, void* pairs, uint64_t cap, void* dev_count);
 /* Pause (on = 0) / resume (on = 1) marking on a GS_CC_TRACK_MARKS handle: folds while paused leave
  * no marks (a replica folding the other ranks' partial summaries must not re-export them). */

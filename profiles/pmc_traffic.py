@@ -56,8 +56,28 @@ def main():
         b = json.load(open(os.path.join(root, "..", "bench.json")))
         out["window_edges"] = b["config"]["window_edges_per_gpu"]
         out["scale"] = b["config"]["scale"]
+        out["id_bits"] = b["config"].get("id_bits", 32)
     except Exception:
         pass
+    # the dominant kernel alone, per launch (what bench.py's roofline.traffic reports): k_fold_ring
+    ring = [k for k in agg if "k_fold_ring" in k]
+    if ring:
+        k = ring[0]
+        nl = max(ncalls.get(k) or 1, 1)
+        f_ring = agg[k].get("FETCH_SIZE", 0.0) * 1024 / nl
+        w_ring = agg[k].get("WRITE_SIZE", 0.0) * 1024 / nl
+        e_ring = 8 * out.get("window_edges", 0) * (2 if out.get("id_bits", 32) == 64 else 1)
+        h_, m_ = agg[k].get("TCC_HIT_sum", 0.0), agg[k].get("TCC_MISS_sum", 0.0)
+        out["ring"] = {
+            "kernel": k, "launches": nl,
+            "fetch_bytes_raw_per_launch": f_ring, "write_bytes_per_launch": w_ring,
+            # gfx950: FETCH_SIZE reports half the bytes of the wide (16 B/lane) streaming edge read
+            # (MI355X_MICROARCH.md, HBM section): add that half back; random 4-B gathers uncalibrated
+            "hbm_bytes_per_launch": f_ring + e_ring / 2 + w_ring,
+            "l2_hit_rate": h_ / (h_ + m_) if h_ + m_ else None,
+            "tcc_requests_per_launch": (h_ + m_) / nl,
+            "memory_side_atomics_per_launch": agg[k].get("TCC_EA0_ATOMIC_sum", 0.0) / nl,
+        }
     # streaming edge read (8 B/edge, 16 B/lane loads) is under-reported 2x: add it back once
     edge_bytes = 8 * out.get("window_edges", 0)
     out["hbm_bytes_per_window"] = out["fold"]["fetch_bytes_raw_per_window"] + edge_bytes / 2 + out["fold"]["write_bytes_per_window"]

@@ -360,7 +360,7 @@ def test_replicated_exchange_single_process(oracle, torch_cuda, world, slots):
     want = oracle.run(s, d, W, partitions=world, emit=EMIT_DENSE, label_cap=cap)["labels"]
     cur = torch.cuda.current_stream()
     ranks = [DisjointSet(cap, id_bits=32, track_marks=True, stream=cur) for _ in range(world)]
-    bufs = [torch.empty(2 * cap, dtype=torch.int32, device="cuda") for _ in range(world)]
+    bufs = [torch.empty(4 * cap, dtype=torch.int32, device="cuda") for _ in range(world)]   # 2 x cap pairs
     cnt = torch.zeros(world, dtype=torch.int64, device="cuda")
     recv = torch.empty(2 * cap * world, dtype=torch.int32, device="cuda")
     ts = torch.from_numpy(s.astype(np.int32)).cuda()
