@@ -320,8 +320,9 @@ def main():
             "final_components": nc,
         }
         if world > 1:                                # rank 0's side of the exchange
+            overflows = None
             if comm is not None:
-                _, _, sent, recv, nex = comm.info()
+                _, _, sent, recv, nex, overflows = comm.info()
             else:
                 sent, recv, nex = tree.bytes_sent, tree.bytes_recv, (a.warmup + a.steps + 1) * nwin
             line["exchange"] = {
@@ -331,6 +332,7 @@ def main():
                 "bytes_sent_per_window": sent / max(nex, 1),
                 "bytes_recv_per_window": recv / max(nex, 1),
                 "wall_ms_per_window": elapsed / a.steps / nwin * 1e3,
+                "slot_overflows": overflows,
             }
         if verify is not None:
             line["verify"] = verify

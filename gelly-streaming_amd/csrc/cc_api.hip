@@ -693,10 +693,35 @@ int cc_info(gs_cc_t* h, CcInfo* out) {
     return GS_OK;
 }
 static int export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long* counter);
+// Fold the slots of a speculative all-gather (comm.hip): every slot but `skip`, pairs up to
+// min(count, cap) read on the device; marking is off for these folds (the others' deltas are theirs
+// to export). Big slots (young windows: components not yet joined) fold a short head of every
+// slot first (see kMergeHead), then the rest.
+int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int nslots, int skip, uint64_t cap) {
+    GS_TRY(check(h));
+    DeviceGuard g(h->device);
+    if (nslots <= 1 || cap == 0) return GS_OK;
+    h->compressed = false;
+    h->minkey_valid = false;
+    FoldArgs f{0, h->parent, nullptr, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, nullptr};
+    KTimer t(h, GS_K_MERGE);
+    const uint64_t head = cap > kMergeBulk ? std::min<uint64_t>(cap, kMergeHead) : 0;
+    if (head) {
+        const dim3 grid(grid_for(head, 256, 64), (unsigned)nslots);
+        klaunch(k_fold_slots, grid, dim3(256), h->stream, t.start(), nullptr, slots, slot_words, skip, (uint64_t)0, head, f);
+    }
+    const dim3 grid(grid_for(cap - head, 256, (unsigned)std::max(64, 4096 / nslots)), (unsigned)nslots);
+    klaunch(k_fold_slots, grid, dim3(256), h->stream, head ? nullptr : t.start(), t.stop(), slots, slot_words, skip, head, cap, f);
+    GS_HIP(hipGetLastError());
+    return GS_OK;
+}
+void cc_count_folded(gs_cc_t* h, uint64_t n) { h->edges_since_reset += n; }
+
 int cc_export_async(gs_cc_t* h, void* pairs, uint64_t cap, unsigned long long* dcount) {
     GS_TRY(check(h));
     if (!h->mark_buf || h->sparse) return fail(GS_ERR_UNSUPPORTED, "export: no marks on this handle");
-    if (cap < 2ull * h->cap) return fail(GS_ERR_CAPACITY, "export: capacity %llu < 2 x vertex capacity %u", (unsigned long long)cap, h->cap);
+    // (cap may be smaller than the log: the pending tail stays for the next export; the count word
+    // receives the whole pending number, so the caller can tell)
     DeviceGuard g(h->device);
     return export_launch(h, pairs, cap, dcount);
 }

@@ -825,6 +825,27 @@ __global__ __launch_bounds__(256) void k_merge_dense(const uint32_t* __restrict_
     }
 }
 
+// Folds received partial summaries laid out in slots (multi-GPU exchange, comm.hip): slot q =
+// [uint64 count][cap pairs (v, root)], slot_words 32-bit words apart; pairs [lo, min(count, hi))
+// of every slot but `skip` are unioned (DisjointSet.merge over the pairs). The counts are read on
+// the device, so the fold is enqueued before the host has seen them. Ids are range-checked (a
+// peer's buffer). blockIdx.y = slot.
+__global__ __launch_bounds__(256) void k_fold_slots(const uint32_t* __restrict__ slots, uint64_t slot_words, int skip,
+                                                    uint64_t lo, uint64_t hi, FoldArgs f) {
+    const int q = blockIdx.y;
+    if (q == skip) return;                           // uniform
+    const uint32_t* s = slots + (uint64_t)q * slot_words;
+    const unsigned long long cnt = *reinterpret_cast<const unsigned long long*>(s);
+    const uint64_t n = cnt < hi ? cnt : hi;
+    const uint32_t* pairs = s + 2;
+    FoldStats st;
+    for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t u[1] = {pairs[2 * i]}, v[1] = {pairs[2 * i + 1]};
+        const bool ok[1] = {u[0] < f.rc.cap && v[0] < f.rc.cap};
+        union_group<false, false, 1>(f, u, v, ok, st);
+    }
+}
+
 // Giant-component state (gs_cc_t::derr, cc_api.hip giant_state()): two slots of two words,
 // double-buffered by close parity, plus the hot set's owner:
 //   slot[0] giant: the root the next close builds gbits for (followed to its current root first);

@@ -39,6 +39,8 @@ struct CcInfo {
 };
 int cc_info(gs_cc_t* h, CcInfo* out);
 int cc_export_async(gs_cc_t* h, void* pairs, uint64_t cap, unsigned long long* dcount);
+int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int nslots, int skip, uint64_t cap);
+void cc_count_folded(gs_cc_t* h, uint64_t n);
 
 namespace {
 
@@ -48,6 +50,13 @@ __global__ void k_pad_pairs(uint2* __restrict__ buf, uint64_t n, uint64_t m) {
     const uint2 p = buf[0];
     for (uint64_t i = n + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x)
         buf[i] = p;
+}
+
+// the count words of P exchange slots -> out[0..P) (one small D2H copy for the host's check)
+__global__ void k_slot_counts(const uint32_t* __restrict__ slots, uint64_t slot_words, int P,
+                              unsigned long long* __restrict__ out) {
+    for (int q = threadIdx.x; q < P; q += blockDim.x)
+        out[q] = *reinterpret_cast<const unsigned long long*>(slots + (uint64_t)q * slot_words);
 }
 
 // ---- in-process group (tests): threads on one device ----
@@ -98,7 +107,9 @@ struct gs_comm {
     unsigned long long* dcnt = nullptr;            // [world + 1]: all-gathered counts, [world] own/received
     unsigned long long* hcnt = nullptr;            // pinned mirror
     bool root_marking_off = false;
-    uint64_t bytes_sent = 0, bytes_recv = 0, exchanges = 0;
+    uint64_t spec_slot = 0;                        // allgather: slot size of the speculative round (0: exact)
+    hipEvent_t ev_counts = nullptr;                // the speculative round's counts are on the host
+    uint64_t bytes_sent = 0, bytes_recv = 0, exchanges = 0, overflows = 0;
 };
 
 namespace {
@@ -211,7 +222,7 @@ int prepare(gs_comm_t* c, gs_cc_t* h, CcInfo* info) {
     if (c->cap_pairs < need) {
         if (c->sendbuf) (void)hipFree(c->sendbuf);
         c->sendbuf = nullptr;
-        if (hipMalloc(&c->sendbuf, (size_t)need * 8) != hipSuccess) {
+        if (hipMalloc(&c->sendbuf, (size_t)(need + 1) * 8) != hipSuccess) {     // + a count word
             (void)hipGetLastError();
             c->cap_pairs = 0;
             return fail(GS_ERR_NOMEM, "exchange buffer of %llu pairs", (unsigned long long)need);
@@ -248,9 +259,10 @@ int fold_slots(gs_cc_t* h, const uint32_t* buf, uint64_t m, const std::vector<ui
     return GS_OK;
 }
 
-// Replicated global summary: every rank folds the others' deltas, so every rank's giant filter is
-// the global one and its next delta holds only connectivity new to the whole job.
-int merge_allgather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
+// One exact exchange round of the replicated summary: counts all-gathered and read by the host,
+// deltas padded to the largest count and all-gathered, the others' slots folded with marking
+// paused. *maxc = the largest delta.
+int exchange_exact(gs_comm_t* c, gs_cc_t* h, const CcInfo& in, uint64_t* maxc) {
     const int P = c->world;
     hipStream_t s = in.stream;
     GS_TRY(cc_export_async(h, c->sendbuf, c->cap_pairs, c->dcnt + P));
@@ -260,6 +272,7 @@ int merge_allgather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
     std::vector<uint64_t> cnt(P);
     uint64_t m = 0;
     for (int q = 0; q < P; ++q) { cnt[q] = c->hcnt[q]; m = std::max(m, cnt[q]); }
+    *maxc = m;
     if (m) {
         const uint64_t n = cnt[c->rank];
         if (n && n < m)
@@ -277,7 +290,64 @@ int merge_allgather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
         c->bytes_sent += m * 8 * (P - 1);
         c->bytes_recv += m * 8 * (P - 1);
     }
-    return gs_cc_close_window(h);
+    return GS_OK;
+}
+
+// The slot size of the next speculative exchange: twice the largest delta just seen (at least 4K
+// pairs), the same on every rank (every rank saw every count).
+uint64_t next_slot(const gs_comm_t* c, uint64_t maxc) {
+    uint64_t S = std::max<uint64_t>(2 * maxc, 4096);
+    S = (S + 1023) & ~(uint64_t)1023;
+    return std::min<uint64_t>(S, c->cap_pairs - 1);
+}
+
+// Replicated global summary: every rank folds the others' deltas, so every rank's giant filter is
+// the global one and its next delta holds only connectivity new to the whole job.
+// Speculative single-collective round (once a slot size is known): every rank exports at most S
+// pairs behind a count word and the slots are all-gathered in ONE RCCL call; the others' slots
+// are folded and the window is closed with the counts read on the device, while the host checks
+// the counts it copied back. A delta larger than S (every rank sees the same counts, so all agree)
+// leaves its tail in the exporter's hook log; one exact round then carries it and the window is
+// closed again. The first window of a stream runs the exact round and sizes the slots.
+int merge_allgather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
+    const int P = c->world;
+    hipStream_t s = in.stream;
+    uint64_t maxc = 0;
+    const uint64_t S = c->spec_slot;
+    if (S == 0) {
+        GS_TRY(exchange_exact(c, h, in, &maxc));
+        GS_TRY(gs_cc_close_window(h));
+        c->spec_slot = next_slot(c, maxc);
+        return GS_OK;
+    }
+    const uint64_t slot_words = 2 + 2 * S;                       // [u64 count][S pairs]
+    uint32_t* send = c->sendbuf;
+    GS_TRY(cc_export_async(h, send + 2, S, reinterpret_cast<unsigned long long*>(send)));
+    GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)P * slot_words * 4));
+    GS_TRY(allgather(c, send, c->recvbuf, slot_words * 4, s));
+    hipLaunchKernelGGL(k_slot_counts, dim3(1), dim3(64), 0, s, (const uint32_t*)c->recvbuf, slot_words, P, c->dcnt);
+    GS_HIP(hipGetLastError());
+    GS_HIP(hipMemcpyAsync(c->hcnt, c->dcnt, P * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    GS_HIP(hipEventRecord(c->ev_counts, s));
+    GS_TRY(cc_fold_slots(h, c->recvbuf, slot_words, P, c->rank, S));
+    GS_TRY(gs_cc_close_window(h));                              // optimistic: no delta exceeded S
+    GS_HIP(hipEventSynchronize(c->ev_counts));                  // the GPU folds and closes meanwhile
+    uint64_t folded = 0;
+    for (int q = 0; q < P; ++q) {
+        maxc = std::max<uint64_t>(maxc, c->hcnt[q]);
+        if (q != c->rank) folded += std::min<uint64_t>(c->hcnt[q], S);
+    }
+    cc_count_folded(h, folded);
+    c->bytes_sent += slot_words * 4 * (P - 1);
+    c->bytes_recv += slot_words * 4 * (P - 1);
+    if (maxc > S) {                                             // a tail stayed behind: carry it
+        ++c->overflows;
+        uint64_t rest = 0;
+        GS_TRY(exchange_exact(c, h, in, &rest));
+        GS_TRY(gs_cc_close_window(h));
+    }
+    c->spec_slot = next_slot(c, maxc);
+    return GS_OK;
 }
 
 // windowAll: every other rank sends its delta straight to rank 0 (the Merger), which folds them
@@ -375,6 +445,7 @@ int merge_tree(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
 
 int alloc_common(gs_comm_t* c) {
     if (hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_counts, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->dcnt, (c->world + 1) * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&c->hcnt, (c->world + 1) * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
@@ -450,6 +521,7 @@ int gs_comm_destroy(gs_comm_t* c) {
     if (c->nccl) (void)ncclCommDestroy(c->nccl);
     if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
+    if (c->ev_counts) (void)hipEventDestroy(c->ev_counts);
     if (c->sendbuf) (void)hipFree(c->sendbuf);
     if (c->recvbuf) (void)hipFree(c->recvbuf);
     if (c->dcnt) (void)hipFree(c->dcnt);
@@ -458,8 +530,10 @@ int gs_comm_destroy(gs_comm_t* c) {
     return GS_OK;
 }
 
-int gs_comm_info(gs_comm_t* c, int* rank, int* world, uint64_t* bytes_sent, uint64_t* bytes_recv, uint64_t* exchanges) {
+int gs_comm_info(gs_comm_t* c, int* rank, int* world, uint64_t* bytes_sent, uint64_t* bytes_recv, uint64_t* exchanges,
+                 uint64_t* overflows) {
     if (!c) return fail(GS_ERR_INVALID, "null communicator");
+    if (overflows) *overflows = c->overflows;
     if (rank) *rank = c->rank;
     if (world) *world = c->world;
     if (bytes_sent) *bytes_sent = c->bytes_sent;

@@ -135,7 +135,7 @@ def lib() -> ctypes.CDLL:
         "gs_comm_create": [P(vp), vp, i32, i32, i32],
         "gs_comm_create_local": [P(vp), i32, i32],
         "gs_comm_destroy": [vp],
-        "gs_comm_info": [vp, P(i32), P(i32), P(u64), P(u64), P(u64)],
+        "gs_comm_info": [vp, P(i32), P(i32), P(u64), P(u64), P(u64), P(u64)],
         "gs_cc_merge_window": [vp, vp, i32],
     }
     for name, args in sig.items():

@@ -63,13 +63,14 @@ class Comm:
             raise RuntimeError("Comm is closed")
         return self._h
 
-    def info(self) -> Tuple[int, int, int, int, int]:
-        """(rank, world, bytes_sent, bytes_recv, exchanges)."""
+    def info(self) -> Tuple[int, int, int, int, int, int]:
+        """(rank, world, bytes_sent, bytes_recv, exchanges, overflows): overflows = speculative
+        all-gather rounds a delta outgrew (each followed by one exact round)."""
         r, w = ctypes.c_int(), ctypes.c_int()
-        s, v, e = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        s, v, e, o = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         call("gs_comm_info", self.handle, ctypes.byref(r), ctypes.byref(w), ctypes.byref(s), ctypes.byref(v),
-             ctypes.byref(e))
-        return r.value, w.value, s.value, v.value, e.value
+             ctypes.byref(e), ctypes.byref(o))
+        return r.value, w.value, s.value, v.value, e.value, o.value
 
     def close(self) -> None:
         if getattr(self, "_h", None) is not None:

@@ -157,18 +157,23 @@ int gs_cc_set_marking(gs_cc_t* h, int on);
  *   gs_cc_merge_window  after folding this rank's slice of a window: exchange this window's
  *                       partial summary (the handle needs GS_CC_TRACK_MARKS) and close the window.
  *     GS_MERGE_ALLGATHER  every rank keeps the GLOBAL summary (all-gather of deltas; every rank's
- *                         emission is the Merger's)
+ *                         emission is the Merger's). From the second window on ONE all-gather of
+ *                         slots sized from the last window's deltas (an outgrown slot costs one
+ *                         more exact round, decided alike on every rank)
  *     GS_MERGE_GATHER     windowAll: deltas to rank 0, which folds them and emits
  *     GS_MERGE_TREE       log2(P) pairwise rounds to rank 0 (SummaryTreeReduce.enhance)
- *   Every rank must call it once per window with the same mode. It synchronises the handle's
- *   stream once per window (delta sizes). In GATHER / TREE only rank 0's emission is the job's. */
+ *   Every rank must call it once per window with the same mode. It waits once per window for the
+ *   delta sizes. In GATHER / TREE only rank 0's emission is the job's. */
 typedef struct gs_comm gs_comm_t;
 enum { GS_MERGE_ALLGATHER = 0, GS_MERGE_GATHER = 1, GS_MERGE_TREE = 2 };
 int gs_comm_unique_id(void* id, uint64_t id_bytes);
 int gs_comm_create(gs_comm_t** out, const void* unique_id, int rank, int world, int device);
 int gs_comm_create_local(gs_comm_t** comms, int world, int device);
 int gs_comm_destroy(gs_comm_t* comm);
-int gs_comm_info(gs_comm_t* comm, int* rank, int* world, uint64_t* bytes_sent, uint64_t* bytes_recv, uint64_t* exchanges);
+/* rank, world size, payload bytes sent / received, windows merged, and speculative all-gather
+ * rounds whose slot a delta outgrew (each then ran one exact round) */
+int gs_comm_info(gs_comm_t* comm, int* rank, int* world, uint64_t* bytes_sent, uint64_t* bytes_recv, uint64_t* exchanges,
+                 uint64_t* overflows);
 int gs_cc_merge_window(gs_cc_t* h, gs_comm_t* comm, int mode);
 
 /* ---- instrumentation ----

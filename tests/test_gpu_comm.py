@@ -47,7 +47,7 @@ def test_rccl_world1(oracle, mode):
         got.append(ds.checksum()[0])
     assert got == [int(x) for x in want["checksums"]]
     np.testing.assert_array_equal(ds.dense().astype(np.int64), want["final"])
-    r, w, sent, recv, ex = comm.info()
+    r, w, sent, recv, ex, ov = comm.info()
     assert (r, w, ex) == (0, 1, len(got))
     ds.close()
     comm.close()
@@ -103,6 +103,8 @@ def test_local_group_vs_oracle(oracle, world, mode):
         assert sums[r] == [int(x) for x in want["checksums"]], "rank %d" % r
         np.testing.assert_array_equal(finals[r], want["final"])
     assert all(i[4] == len(want["checksums"]) for i in info)
+    if mode == "allgather":                  # every rank took the same speculative / exact decisions
+        assert len({i[5] for i in info}) == 1
 
 
 def test_local_group_young_windows_big_deltas(oracle):
@@ -115,6 +117,24 @@ def test_local_group_young_windows_big_deltas(oracle):
     for r in range(2):
         assert sums[r] == [int(x) for x in want["checksums"]]
         np.testing.assert_array_equal(finals[r], want["final"])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_local_group_speculative_slot_overflow(oracle, world):
+    """allgather's speculative slot is sized from the last window's deltas: a tiny first window
+    (one self-loop) then an Erdos-Renyi window whose deltas outgrow the 4K-pair slot — the exact
+    round must carry the tails (overflow counted on every rank), and every emission stays exact."""
+    cap = 1 << 16
+    W = 1 << 17
+    s1 = np.zeros(W, dtype=np.int64)                 # window 1: the self-loop (0, 0), W times
+    s2, d2 = oracle.gen_er(0, 3 * W, cap, 4)        # windows 2-4: 3 x 2^17 uniform edges
+    s = np.concatenate([s1, s2]); d = np.concatenate([s1, d2])
+    want = oracle.run(s, d, W, partitions=world, emit=EMIT_CHECKSUM, label_cap=cap, want_final=True)
+    sums, finals, info = _run_local(world, "allgather", s, d, cap, W)
+    for r in range(world):
+        assert sums[r] == [int(x) for x in want["checksums"]], "rank %d" % r
+        np.testing.assert_array_equal(finals[r], want["final"])
+    assert all(i[5] >= 1 for i in info) and len({i[5] for i in info}) == 1, info
 
 
 def test_merge_window_errors():
