@@ -102,8 +102,10 @@ struct gs_comm {
     // exchange buffers (device), sized at the first merge for the handle's capacity
     uint64_t cap_pairs = 0;
     uint32_t* sendbuf = nullptr;                   // cap_pairs pairs (2 x the handle's capacity)
-    uint32_t* recvbuf = nullptr;                   // grows: world * m pairs
+    uint32_t* recvbuf = nullptr;                   // exact rounds: grows to world * m pairs
     size_t recv_bytes = 0;
+    uint32_t* slotbuf = nullptr;                   // speculative rounds: world count-headed slots
+    size_t slot_bytes = 0;
     unsigned long long* dcnt = nullptr;            // [world + 1]: all-gathered counts, [world] own/received
     unsigned long long* hcnt = nullptr;            // pinned mirror
     bool root_marking_off = false;
@@ -204,9 +206,17 @@ struct Group {                                     // ncclGroupStart/End around 
     ~Group() { if (c && c->nccl) (void)ncclGroupEnd(); }
 };
 
-int ensure(void** p, size_t* have, size_t need) {
+// Grows a device buffer. Folds already enqueued on the stream may still read the old one (a
+// receive buffer is read by the fold kernels that follow its collective), so the stream drains
+// before the free.
+int ensure(void** p, size_t* have, size_t need, hipStream_t s) {
     if (*have >= need) return GS_OK;
-    if (*p) { GS_HIP(hipFree(*p)); *p = nullptr; *have = 0; }
+    if (*p) {
+        GS_HIP(hipStreamSynchronize(s));
+        GS_HIP(hipFree(*p));
+        *p = nullptr;
+        *have = 0;
+    }
     if (hipMalloc(p, need) != hipSuccess) { (void)hipGetLastError(); return fail(GS_ERR_NOMEM, "hipMalloc(%zu) failed", need); }
     *have = need;
     return GS_OK;
@@ -279,7 +289,7 @@ int exchange_exact(gs_comm_t* c, gs_cc_t* h, const CcInfo& in, uint64_t* maxc) {
             hipLaunchKernelGGL(k_pad_pairs, dim3((unsigned)std::min<uint64_t>((m - n + 255) / 256, 4096)), dim3(256), 0, s,
                                reinterpret_cast<uint2*>(c->sendbuf), n, m);
         GS_HIP(hipGetLastError());
-        GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)P * m * 8));
+        GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)P * m * 8, s));
         GS_TRY(allgather(c, c->sendbuf, c->recvbuf, m * 8, s));
         std::vector<char> skip(P, 0);
         skip[c->rank] = 1;
@@ -303,12 +313,14 @@ uint64_t next_slot(const gs_comm_t* c, uint64_t maxc) {
 
 // Replicated global summary: every rank folds the others' deltas, so every rank's giant filter is
 // the global one and its next delta holds only connectivity new to the whole job.
-// Speculative single-collective round (once a slot size is known): every rank exports at most S
-// pairs behind a count word and the slots are all-gathered in ONE RCCL call; the others' slots
-// are folded and the window is closed with the counts read on the device, while the host checks
-// the counts it copied back. A delta larger than S (every rank sees the same counts, so all agree)
-// leaves its tail in the exporter's hook log; one exact round then carries it and the window is
-// closed again. The first window of a stream runs the exact round and sizes the slots.
+// Speculative single-collective round (once a slot size S is known): every rank exports its WHOLE
+// delta behind a count word, right after its own fold, and the first S pairs of every rank are
+// all-gathered in ONE RCCL call; the others' slots are folded and the window is closed with the
+// counts read on the device while the host checks the counts it copied back. A delta larger than
+// S (every rank sees every count, so all agree) has its tail sent in one more all-gather, from the
+// same export: the pairs must be the exporter's state right after its own fold — re-exported
+// after folding the others' slots (marking paused), a root of its own that a foreign pair hooked
+// would vanish from its pairs. The first window of a stream runs the exact round and sizes S.
 int merge_allgather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
     const int P = c->world;
     hipStream_t s = in.stream;
@@ -322,28 +334,48 @@ int merge_allgather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
     }
     const uint64_t slot_words = 2 + 2 * S;                       // [u64 count][S pairs]
     uint32_t* send = c->sendbuf;
-    GS_TRY(cc_export_async(h, send + 2, S, reinterpret_cast<unsigned long long*>(send)));
-    GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)P * slot_words * 4));
-    GS_TRY(allgather(c, send, c->recvbuf, slot_words * 4, s));
-    hipLaunchKernelGGL(k_slot_counts, dim3(1), dim3(64), 0, s, (const uint32_t*)c->recvbuf, slot_words, P, c->dcnt);
+    GS_TRY(cc_export_async(h, send + 2, c->cap_pairs - 1, reinterpret_cast<unsigned long long*>(send)));
+    GS_TRY(ensure(reinterpret_cast<void**>(&c->slotbuf), &c->slot_bytes, (size_t)P * slot_words * 4, s));
+    GS_TRY(allgather(c, send, c->slotbuf, slot_words * 4, s));
+    hipLaunchKernelGGL(k_slot_counts, dim3(1), dim3(64), 0, s, (const uint32_t*)c->slotbuf, slot_words, P, c->dcnt);
     GS_HIP(hipGetLastError());
     GS_HIP(hipMemcpyAsync(c->hcnt, c->dcnt, P * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     GS_HIP(hipEventRecord(c->ev_counts, s));
-    GS_TRY(cc_fold_slots(h, c->recvbuf, slot_words, P, c->rank, S));
+    GS_TRY(cc_fold_slots(h, c->slotbuf, slot_words, P, c->rank, S));
     GS_TRY(gs_cc_close_window(h));                              // optimistic: no delta exceeded S
     GS_HIP(hipEventSynchronize(c->ev_counts));                  // the GPU folds and closes meanwhile
-    uint64_t folded = 0;
+    std::vector<uint64_t> tail(P, 0);
+    uint64_t folded = 0, mt = 0;
     for (int q = 0; q < P; ++q) {
-        maxc = std::max<uint64_t>(maxc, c->hcnt[q]);
-        if (q != c->rank) folded += std::min<uint64_t>(c->hcnt[q], S);
+        const uint64_t n = c->hcnt[q];
+        if (n > c->cap_pairs - 1) return fail(GS_ERR_CAPACITY, "rank %d delta of %llu pairs past the export buffer", q,
+                                              (unsigned long long)n);
+        maxc = std::max<uint64_t>(maxc, n);
+        tail[q] = n > S ? n - S : 0;
+        mt = std::max<uint64_t>(mt, tail[q]);
+        if (q != c->rank) folded += n;
     }
     cc_count_folded(h, folded);
     c->bytes_sent += slot_words * 4 * (P - 1);
     c->bytes_recv += slot_words * 4 * (P - 1);
-    if (maxc > S) {                                             // a tail stayed behind: carry it
+    if (mt) {                                                   // tails past S: one more all-gather
         ++c->overflows;
-        uint64_t rest = 0;
-        GS_TRY(exchange_exact(c, h, in, &rest));
+        uint32_t* t = send + 2 + 2 * S;                         // this rank's pairs [S, n)
+        const uint64_t n = tail[c->rank];
+        if (n && n < mt)
+            hipLaunchKernelGGL(k_pad_pairs, dim3((unsigned)std::min<uint64_t>((mt - n + 255) / 256, 4096)), dim3(256), 0, s,
+                               reinterpret_cast<uint2*>(t), n, mt);
+        GS_HIP(hipGetLastError());
+        GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)P * mt * 8, s));
+        GS_TRY(allgather(c, t, c->recvbuf, mt * 8, s));
+        std::vector<char> skip(P, 0);
+        skip[c->rank] = 1;
+        GS_TRY(gs_cc_set_marking(h, 0));
+        const int rc = fold_slots(h, c->recvbuf, mt, tail, skip);
+        GS_TRY(gs_cc_set_marking(h, 1));
+        GS_TRY(rc);
+        c->bytes_sent += mt * 8 * (P - 1);
+        c->bytes_recv += mt * 8 * (P - 1);
         GS_TRY(gs_cc_close_window(h));
     }
     c->spec_slot = next_slot(c, maxc);
@@ -380,7 +412,7 @@ int merge_gather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
     uint64_t total = 0, mx = 0;
     for (int q = 1; q < P; ++q) { cnt[q] = c->hcnt[q]; total += cnt[q]; mx = std::max(mx, cnt[q]); }
     if (total) {
-        GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)total * 8));
+        GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)total * 8, s));
         {
             Group g(c);
             uint64_t off = 0;
@@ -433,7 +465,7 @@ int merge_tree(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
             GS_HIP(hipStreamSynchronize(s));
             const uint64_t n = c->hcnt[0];
             if (n) {
-                GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)n * 8));
+                GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)n * 8, s));
                 GS_TRY(recv(c, c->recvbuf, n * 8, peer, s));
                 GS_TRY(gs_cc_fold_pairs32(h, c->recvbuf, n));
             }
@@ -524,6 +556,7 @@ int gs_comm_destroy(gs_comm_t* c) {
     if (c->ev_counts) (void)hipEventDestroy(c->ev_counts);
     if (c->sendbuf) (void)hipFree(c->sendbuf);
     if (c->recvbuf) (void)hipFree(c->recvbuf);
+    if (c->slotbuf) (void)hipFree(c->slotbuf);
     if (c->dcnt) (void)hipFree(c->dcnt);
     if (c->hcnt) (void)hipHostFree(c->hcnt);
     delete c;
