@@ -85,7 +85,11 @@ struct gs_cc {
     uint32_t* hot_cand = nullptr;        // hot-set admission candidates (2^kHotCandBits ids)
     uint32_t* warm = nullptr;            // warm set (2^warm_bits words, L2-resident), steady folds
     uint32_t warm_bits = 0;
-    uint32_t* wcnt = nullptr;            // warm build counters (16-bit, 2^(hot_bits-1) words)
+    uint32_t* wkeys = nullptr;           // warm build: sampled endpoint keys, then the (id, count) list
+    uint16_t* wpart = nullptr;           // warm build: keys by hash bucket
+    unsigned long long* wctl = nullptr;  // warm build: [0] keys, [1] list length, then bucket fills
+    uint64_t warm_sample = 0;            // edges a warm count launch samples
+    uint32_t warm_bcap = 0;              // keys per hash bucket
     int cus = 0;                         // compute units: k_fold_ring grid
     // GS_CC_SPARSE_IDS: id -> slot table; cap (above) = slots = 2^hbits + 1
     bool sparse = false;
@@ -215,20 +219,17 @@ constexpr unsigned kCompressGrid = 2048;
 // with gbits L2-resident the hot set's 128 KiB LDS fill per workgroup costs more than it saves
 // (RMAT-20 2^20-edge windows: ring 83 us, plain 61 us; ER 2^24: 141 vs 126 us).
 constexpr uint32_t kRingMinBits = 25;
-// warm set: counted in ring launch kWarmAt after reset (kWarmSample edges) and re-checked every
-// kWarmEvery-th launch (rebuilt only when invalid for the current giant); 4 band passes, hottest
-// first (2 bands: +0.17 ms per step; 2^24-edge samples: more hits, no faster once the count is paid)
-#if defined(GS_EXP_WS22)
-constexpr uint64_t kWarmAt = 3, kWarmEvery = 16, kWarmSample = 1ull << 22;
-#elif defined(GS_EXP_WS21)
-constexpr uint64_t kWarmAt = 3, kWarmEvery = 16, kWarmSample = 1ull << 21;
+// warm set: counted in ring launch kWarmAt after reset (the first warm_sample edges: kWarmSample,
+// at most capacity/8) and re-checked every kWarmEvery-th launch (rebuilt only when invalid for the
+// current giant); inserted in 4 count bands, hottest first
+#if defined(GS_EXP_WS24)
+constexpr uint64_t kWarmAt = 3, kWarmEvery = 16, kWarmSample = 1ull << 24;
 #else
 constexpr uint64_t kWarmAt = 3, kWarmEvery = 16, kWarmSample = 1ull << 23;
 #endif
 constexpr uint32_t kWarmBucketsMaxBits = 18;        // 2^18 x 4 B = 1 MiB table at RMAT-26 (2 MiB with
                                                     // 2^24-edge samples: 5 us less per steady window,
                                                     // 0.44 ms more count per step; profiles/r02_d)
-constexpr uint32_t kWarmBands[] = {0xFFFFFFFFu, 32u, 8u, 3u, 2u};
 constexpr uint32_t kHotThresh = 3;                  // sightings before hot-set admission (233 -> 229 us)
 // Young split: inside the young forest, close internally (compress + giant pick: no emission,
 // labels stay canonical) after capacity/16 edges, so the rest of the young window folds with the
@@ -312,6 +313,23 @@ static bool use_ring(const gs_cc_t* h) {
     return m == kFoldRing || (m == kFoldAuto && h->hot_bits >= dbg().ring_min_bits);
 }
 
+static WarmBuild warm_build_args(gs_cc_t* h) {
+    WarmBuild w;
+    w.keys = h->wkeys;
+    w.ctl = h->wctl;
+    w.cur = reinterpret_cast<uint32_t*>(h->wctl + 2);
+    w.part = h->wpart;
+    w.keys_cap = 2 * h->warm_sample;
+    w.keys_n = 0;
+    w.cap = h->warm_bcap;
+    w.B = h->hot_bits;
+    w.nbk = 1u << (h->hot_bits - kWarmLocalBits);
+    w.warm = h->warm;
+    w.warm_words = 1u << h->warm_bits;
+    w.valid = h->derr + 7;
+    return w;
+}
+
 template <typename IdT>
 void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     ensure_stats(h);
@@ -323,16 +341,16 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     ++h->ring_launches;
     hot.five = (h->hot_bits <= kHotBucketBits + 12) ? 1u : 0u;
     hot.thresh = kHotThresh;
-    // warm set: counted in this launch, then built by k_warm_build, at ring launch kWarmAt after
-    // reset and every kWarmEvery-th after it, each time only if the set is not valid for the
-    // current giant (device-gated)
+    // warm set: counted in this launch, then built (k_warm_part / count / insert), at ring launch
+    // kWarmAt after reset and every kWarmEvery-th after it, each time only if the set is not valid
+    // for the current giant (device-gated)
     const uint64_t launch_no = h->ring_launches - 1;
     const bool build = h->warm && launch_no >= kWarmAt && (launch_no - kWarmAt) % kWarmEvery == 0;
     hot.warm = h->warm;
     hot.warm_bits = h->warm_bits;
     hot.warm_valid = h->derr + 7;
-    hot.wcnt = build ? h->wcnt : nullptr;
-    hot.count_edges = build ? kWarmSample : 0;
+    hot.wkeys = build ? h->wkeys : nullptr;
+    hot.count_edges = build ? h->warm_sample : 0;
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
     f.mark_len = h->mark_ctr;
     KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_RING : h->fold_timer);
@@ -348,17 +366,17 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
         else klaunch(k_fold_ring<IdT, false, false>, grid, dim3(kHotThreads), h->stream, start, stop, a, b, f, hot);
     }
     if (build) {
-        // hottest band first: a full bucket then drops the colder ids
-        const uint32_t B = h->hot_bits;
-        const uint32_t wwords = 1u << h->warm_bits;
-        const uint32_t cwords = (uint32_t)((((uint64_t)1 << B) + 1) / 2);
-        klaunch(k_warm_clear, dim3(grid_for(wwords, 256, 2048)), dim3(256), h->stream, nullptr, nullptr, h->warm, wwords,
-                (const uint32_t*)(h->derr + 7));
-        constexpr int nb = (int)(sizeof(kWarmBands) / sizeof(kWarmBands[0])) - 1;
-        for (int i = 0; i < nb; ++i)
-            klaunch(k_warm_build, dim3(grid_for(cwords / 4 + 1, 256, 8192)), dim3(256), h->stream, nullptr, nullptr, h->wcnt, cwords,
-                    h->warm, B, h->warm_bits, kWarmBands[i + 1], kWarmBands[i], (const uint2*)h->hot, hot.five, (const uint32_t*)h->gbits, h->derr + 7, (int)(i == nb - 1));
-        klaunch(k_warm_done, dim3(1), dim3(1), h->stream, nullptr, t.stop(), h->derr + 7);
+        WarmBuild w = warm_build_args(h);
+        // the count launch wrote 512 keys per wave step of 256 edges over its first
+        // min(n, warm_sample) edges (k_fold_ring takes groups of 4 edges)
+        const uint64_t counted = std::min<uint64_t>(h->warm_sample, n / 4 * 4);
+        w.keys_n = (counted + 255) / 256 * 512;
+        klaunch(k_warm_part, dim3((unsigned)((w.keys_cap + kWarmPartTile - 1) / kWarmPartTile)), dim3(1024), h->stream, nullptr,
+                nullptr, w);
+        klaunch(k_warm_count, dim3(w.nbk), dim3(1024), h->stream, nullptr, nullptr, w);
+        klaunch(k_warm_insert, dim3(2048), dim3(256), h->stream, nullptr, nullptr, w, h->warm_bits, (const uint32_t*)h->gbits,
+                (const uint2*)h->hot, hot.five);
+        klaunch(k_warm_done, dim3(1), dim3(1024), h->stream, nullptr, t.stop(), w, h->derr + 7);
     }
 }
 
@@ -366,7 +384,11 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
 // reset where gbits outgrows L2 (ids >= 2^kRingMinBits), or at GSGPU_YOUNG_SPLIT
 static uint64_t next_young_split(const gs_cc_t* h, uint64_t done) {
     uint64_t s = dbg().young_split;
+#if defined(GS_EXP_YOUNGRING32)
+    if (s == ~0ull) s = (uint64_t)h->cap >= (1ull << std::min<uint32_t>(dbg().ring_min_bits, 63)) ? h->cap / 32 : 0;
+#else
     if (s == ~0ull) s = (uint64_t)h->cap >= (1ull << std::min<uint32_t>(dbg().ring_min_bits, 63)) ? h->cap / kYoungSplitDiv : 0;
+#endif
     return (s && done < s) ? s : 0;
 }
 
@@ -391,7 +413,13 @@ static void internal_close(gs_cc_t* h) {
 // launch first, then the rest in one launch.
 template <typename IdT, bool AOS>
 void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, size_t esz) {
+#if defined(GS_EXP_YOUNGRING)
+    const uint64_t young_limit = h->cap / kYoungSplitDiv;
+#elif defined(GS_EXP_YOUNGRING32)
+    const uint64_t young_limit = h->cap / 32;
+#else
     const uint64_t young_limit = h->cap / 4;
+#endif
     const size_t stride = AOS ? 2 * esz : esz;
     const bool aligned = ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
     uint64_t off = 0;
@@ -803,15 +831,27 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
             // warm set: only where gbits outgrows an XCD's 4 MiB L2 (with the ring fold), its table
             // L2-resident and at most 1/8 of gbits (8-bit slots need at least 2^(B-8) buckets)
             h->warm_bits = std::min<uint32_t>(kWarmBucketsMaxBits, bits - 6);
-            if (h->hot && bits >= dbg().ring_min_bits && bits <= h->warm_bits + 8) {
-                const size_t cbytes = (size_t)((((uint64_t)1 << bits) + 1) / 2) * 4;
+            if (h->hot && bits >= dbg().ring_min_bits && bits <= h->warm_bits + 8 && bits >= kWarmLocalBits &&
+                bits - kWarmLocalBits <= 13) {
+                h->warm_sample = std::min<uint64_t>(kWarmSample, h->cap / 8);
+                const uint32_t nbk = 1u << (bits - kWarmLocalBits);
+                h->warm_sample = (h->warm_sample + 255) / 256 * 256;        // whole wave steps
+                const uint64_t keys = 2 * h->warm_sample;
+                h->warm_bcap = (uint32_t)(keys / nbk + keys / nbk / 2 + 1024);   // 1.5 x the mean bucket
+                const size_t ctl = 2 * sizeof(unsigned long long) + (size_t)nbk * 4;
                 if (hipMalloc(&h->warm, (size_t)4 << h->warm_bits) != hipSuccess ||
-                    hipMalloc(&h->wcnt, cbytes) != hipSuccess || hipMemsetAsync(h->wcnt, 0, cbytes, h->stream) != hipSuccess) {
+                    hipMalloc(&h->wkeys, keys * 4) != hipSuccess ||
+                    hipMalloc(&h->wpart, (size_t)nbk * h->warm_bcap * 2) != hipSuccess ||
+                    hipMalloc(&h->wctl, ctl) != hipSuccess || hipMemsetAsync(h->wctl, 0, ctl, h->stream) != hipSuccess) {
                     (void)hipGetLastError();
                     if (h->warm) (void)hipFree(h->warm);
-                    if (h->wcnt) (void)hipFree(h->wcnt);
+                    if (h->wkeys) (void)hipFree(h->wkeys);
+                    if (h->wpart) (void)hipFree(h->wpart);
+                    if (h->wctl) (void)hipFree(h->wctl);
                     h->warm = nullptr;
-                    h->wcnt = nullptr;
+                    h->wkeys = nullptr;
+                    h->wpart = nullptr;
+                    h->wctl = nullptr;
                 }
             }
         }
@@ -841,7 +881,9 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->hot) (void)hipFree(h->hot);
     if (h->hot_cand) (void)hipFree(h->hot_cand);
     if (h->warm) (void)hipFree(h->warm);
-    if (h->wcnt) (void)hipFree(h->wcnt);
+    if (h->wkeys) (void)hipFree(h->wkeys);
+    if (h->wpart) (void)hipFree(h->wpart);
+    if (h->wctl) (void)hipFree(h->wctl);
     if (h->keys) (void)hipFree(h->keys);
     if (h->minkey) (void)hipFree(h->minkey);
     if (h->nkeys) (void)hipFree(h->nkeys);

@@ -324,7 +324,7 @@ struct HotArgs {
     uint32_t* warm = nullptr;                  // warm set (2^warm_bits words), nullptr = none
     uint32_t warm_bits = 0;                    // log2(warm buckets), B - 8 <= warm_bits <= B
     const uint32_t* warm_valid = nullptr;      // device word: warm set built for the current giant
-    uint32_t* wcnt = nullptr;                  // endpoint counters for the next warm build
+    uint32_t* wkeys = nullptr;                 // warm build: endpoint keys, 512 per wave step (count launches only)
     uint64_t count_edges = 0;                  // count this launch's first edges (if !*warm_valid)
 };
 
@@ -335,10 +335,12 @@ struct HotArgs {
 // probe: 2^wb buckets x 4 slots of 8 bits, h = v * kWarmMul mod 2^B (odd multiplier: a
 // bijection), bucket = h >> (B - wb), slot value = (h mod 2^(B - wb)) + 1; exact like the hot set. An LDS miss
 // probes it before gbits, so a warm hit costs an L2 hit instead of (half the time) an
-// Infinity-Cache line fill. Built from endpoint counts (16-bit, two per word) of one ring launch's
-// first count_edges edges (LDS misses confirmed in the giant), hottest first (k_warm_build);
+// Infinity-Cache line fill. Built from endpoint counts of one ring launch's
+// first count_edges edges (LDS misses confirmed in the giant), hottest first (k_warm_part below);
 // valid (hot.warm_valid) while the giant is the same component, like the hot set.
 constexpr uint32_t kWarmMul = 0x85EBCA6Bu;
+// count bands of a build, inserted hottest first (2 bands: +0.17 ms per RMAT-26 step)
+constexpr uint32_t kWarmBands[] = {0xFFFFFFFFu, 32u, 8u, 3u, 2u};
 // wb = log2(buckets); remainders of B - wb <= 8 bits, slot value r = rem + 1 in [1, 256]: the one
 // value that does not fit a byte (256: 1 id in 256 when B - wb = 8) never enters nor matches.
 __device__ __forceinline__ uint32_t warm_hash(uint32_t v, uint32_t B) { return (v * kWarmMul) & ((1u << B) - 1); }
@@ -369,9 +371,6 @@ __device__ inline void warm_insert(uint32_t* __restrict__ warm, uint32_t v, uint
         if (old == x) return;
         x = old;
     }
-}
-__device__ __forceinline__ void warm_count(uint32_t* __restrict__ wcnt, uint32_t v) {
-    atomicAdd(&wcnt[v >> 1], 1u << ((v & 1u) << 4));
 }
 
 // Admission cadence. Offering a launch's first 2^18 edges costs ~28 us per RMAT-26 window (the
@@ -408,7 +407,7 @@ __device__ __forceinline__ void hot_admit(const HotArgs& hot, uint32_t v) {
 template <bool STATS, int EPT, bool HOT>
 __device__ __forceinline__ void filter_group(const FoldArgs& f, const uint32_t (&u)[EPT], const uint32_t (&v)[EPT],
                                              bool (&ok)[EPT], const uint2* tab, const HotArgs& hot, bool insert,
-                                             bool warm, bool count, uint32_t (&gflag)[EPT]) {
+                                             bool warm, uint64_t count_slot, uint32_t (&gflag)[EPT]) {
     bool hu[EPT], hv[EPT];       // LDS hot-set hits
     bool mu[EPT], mv[EPT];       // known giant members without a gbits load (LDS or warm hits)
     uint32_t wu[EPT], wv[EPT];
@@ -449,12 +448,19 @@ __device__ __forceinline__ void filter_group(const FoldArgs& f, const uint32_t (
             if (ok[k] && !hv[k] && ((wv[k] >> (v[k] & 31)) & 1u)) hot_admit(hot, v[k]);
         }
     }
-    if (HOT && count) {
+    if (HOT && count_slot != ~0ull) {                // uniform: a warm count launch's sampled edges
+        // the wave's 4 x 64 edges own keys [count_slot * 512, +512): endpoints that count as
+        // u32x4 stores, kInvalid for the rest (no atomics: a shared length word would take one
+        // same-address atomic per wave step, 0.3 ms per count launch)
+        uint32_t m[2 * EPT];
 #pragma unroll
         for (int k = 0; k < EPT; ++k) {
-            if (ok[k] && !hu[k] && ((wu[k] >> (u[k] & 31)) & 1u)) warm_count(hot.wcnt, u[k]);
-            if (ok[k] && !hv[k] && ((wv[k] >> (v[k] & 31)) & 1u)) warm_count(hot.wcnt, v[k]);
+            m[2 * k] = (ok[k] && !hu[k] && ((wu[k] >> (u[k] & 31)) & 1u)) ? u[k] : kInvalid;
+            m[2 * k + 1] = (ok[k] && !hv[k] && ((wv[k] >> (v[k] & 31)) & 1u)) ? v[k] : kInvalid;
         }
+        u32x4* dst = reinterpret_cast<u32x4*>(hot.wkeys + count_slot * (128 * EPT) + (threadIdx.x & 63) * (2 * EPT));
+#pragma unroll
+        for (int q = 0; q < EPT / 2; ++q) dst[q] = u32x4{m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]};
     }
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
@@ -519,7 +525,7 @@ __device__ __forceinline__ void fold_group(const FoldArgs& f, bool filt, uint32_
     uint32_t nvalid = 0, nfilt = 0;
     if (STATS) for (int k = 0; k < EPT; ++k) nvalid += ok[k];
     uint32_t gflag[EPT];
-    if (filt) filter_group<STATS, EPT, false>(f, u, v, ok, nullptr, HotArgs{nullptr, 0, nullptr}, false, false, false, gflag);
+    if (filt) filter_group<STATS, EPT, false>(f, u, v, ok, nullptr, HotArgs{nullptr, 0, nullptr}, false, false, ~0ull, gflag);
     union_group<MARK, STATS, EPT>(f, u, v, ok, st);
     if (STATS) {
         for (int k = 0; k < EPT; ++k) nfilt += ok[k];
@@ -689,7 +695,7 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
     const uint32_t budget = hot.budget ? *hot.budget : 1u;
     const uint64_t sample_edges = (hot.periodic || budget) ? hot.sample_edges : 0;
     const bool warm_ok = filt && hot.warm && *hot.warm_valid != 0;                        // uniform
-    const uint64_t count_edges = (filt && hot.wcnt && hot.warm_valid && *hot.warm_valid == 0) ? hot.count_edges : 0;
+    const uint64_t count_edges = (filt && hot.wkeys && hot.warm_valid && *hot.warm_valid == 0) ? hot.count_edges : 0;
     __syncthreads();
     if (blockIdx.x == 0 && threadIdx.x == 0 && hot.budget && budget) *hot.budget = budget - 1;
     const int lane = threadIdx.x & 63;
@@ -718,7 +724,8 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
             if (bad) atomicOr(f.rc.err, 1u);
         }
         if (STATS) for (int k = 0; k < 4; ++k) nvalid += ok[k];
-        if (filt) filter_group<STATS, 4, true>(f, u, v, ok, tab, hot, g * 4 < sample_edges, warm_ok, g * 4 < count_edges, gf);
+        if (filt) filter_group<STATS, 4, true>(f, u, v, ok, tab, hot, g * 4 < sample_edges, warm_ok,
+                                               g0 * 4 < count_edges ? g0 / 64 : ~0ull, gf);
         if (gR == kInvalid) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) gf[k] = 0u;
@@ -759,56 +766,173 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
     }
 }
 
-// Warm build pass: every id whose count c (16-bit counters, two per word) lies in [lo, hi), that
-// gbits holds and that is not already in the hot set enters the warm set; passes run hottest band first so that full
-// buckets keep the hotter ids. The first pass (clear) zeroes the table first; the last (done)
-// zeroes the counters for the next build and marks the set valid. No-op while the set is valid.
-__global__ __launch_bounds__(256) void k_warm_clear(uint32_t* __restrict__ warm, uint32_t words, const uint32_t* __restrict__ valid) {
-    if (*valid) return;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < words; i += gridDim.x * blockDim.x) warm[i] = 0u;
+// Warm build without global counters (the count launch's per-endpoint atomicAdd into 2^B 16-bit
+// counters cost ~390 us and four scans of them ~400 us per RMAT-26 build): the count launch
+// writes its LDS-miss giant endpoints to a key list (512 slots per wave step); k_warm_part
+// scatters them by h = warm_hash(v) into 2^(B-16) buckets of 2^16 hash values (per-workgroup LDS
+// histogram, one atomicAdd per (workgroup, bucket) for the bucket cursor); k_warm_count counts a
+// bucket in LDS (2^16 16-bit counters = 128 KiB) and lists (v, count >= 2), v recovered from h by
+// the inverse multiplier; k_warm_insert inserts the list hottest band first. Every kernel is a
+// no-op while the set is valid (*valid), so the host schedules builds without reading it back.
+constexpr uint32_t kWarmLocalBits = 16;              // hash values per bucket: 2^16
+constexpr uint32_t kWarmPartTile = 1u << 16;          // keys per k_warm_part workgroup (64 per thread)
+constexpr uint32_t kWarmMaxBuckets = 1u << 13;        // B <= 29
+constexpr uint32_t inv_odd(uint32_t a) {
+    uint32_t x = a;                                  // Newton: 5 steps give 32 bits
+    for (int i = 0; i < 5; ++i) x *= 2u - a * x;
+    return x;
 }
-__global__ __launch_bounds__(256) void k_warm_build(uint32_t* __restrict__ wcnt, uint32_t nwords, uint32_t* __restrict__ warm,
-                                                    uint32_t B, uint32_t wb, uint32_t lo, uint32_t hi, const uint2* __restrict__ hot,
-                                                    uint32_t five, const uint32_t* __restrict__ gbits,
-                                                    uint32_t* __restrict__ valid, int done) {
-    if (*valid) return;                              // uniform (set by the last pass, after every read)
-    // 16 B of counters per lane (scalar 4-B reads: 61 us per pass over 128 MiB); most vectors are
-    // zero (2^23 sampled edges touch a fraction of 2^26 ids) and cost only the read
-    const uint32_t nvec = nwords / 4;
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nvec; q += stride) {
-        u32x4 c4 = reinterpret_cast<const u32x4*>(wcnt)[q];
-        if ((c4.x | c4.y | c4.z | c4.w) == 0u) continue;
-        const uint32_t cw[4] = {c4.x, c4.y, c4.z, c4.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t c = cw[j];
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const uint32_t ck = (c >> (16 * k)) & 0xFFFFu;
-                const uint32_t v = 2 * (4 * q + j) + k;
-                // gbits (the last close's giant, a subset of the current one): whatever the counts
-                // say, only a giant member can enter
-                if (ck >= lo && ck < hi && ((gbits[v >> 5] >> (v & 31)) & 1u) && !(hot && hot_probe(hot, v, B, five != 0)))
-                    warm_insert(warm, v, B, wb);
-            }
-        }
-        if (done) reinterpret_cast<u32x4*>(wcnt)[q] = u32x4{0u, 0u, 0u, 0u};
+constexpr uint32_t kWarmMulInv = inv_odd(kWarmMul);
+static_assert(kWarmMul * kWarmMulInv == 1u, "warm hash inverse");
+
+struct WarmBuild {
+    uint32_t* keys;                  // appended endpoint ids; after k_warm_part the (v, count) list
+    unsigned long long* ctl;         // [1] list length
+    uint32_t* cur;                   // per-bucket fill (nbk words)
+    uint16_t* part;                  // nbk buckets x cap local hash values
+    uint64_t keys_cap;               // key list capacity (2 x sampled edges)
+    uint64_t keys_n;                 // keys the count launch wrote (kInvalid where none)
+    uint32_t cap;                    // bucket capacity (keys past it are dropped: counts only rank)
+    uint32_t B;                      // ids < 2^B
+    uint32_t nbk;                    // 2^(B - 16) buckets
+    uint32_t* warm;                  // the warm table (zeroed by k_warm_part)
+    uint32_t warm_words;
+    const uint32_t* valid;
+};
+
+__global__ __launch_bounds__(1024) void k_warm_part(WarmBuild w) {
+    if (*w.valid) return;                            // uniform
+    __shared__ uint32_t hist[kWarmMaxBuckets];
+    __shared__ uint32_t base[kWarmMaxBuckets];
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < w.warm_words; i += gridDim.x * blockDim.x) w.warm[i] = 0u;
+    const uint64_t n = min(w.keys_n, w.keys_cap);
+    const uint64_t lo = (uint64_t)blockIdx.x * kWarmPartTile;
+    const uint64_t hi = min(n, lo + kWarmPartTile);
+    if (lo >= hi) return;                            // uniform
+    const uint32_t mask = (w.B >= 32) ? ~0u : ((1u << w.B) - 1);
+    for (uint32_t b = threadIdx.x; b < w.nbk; b += blockDim.x) hist[b] = 0u;
+    __syncthreads();
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        const uint32_t v = w.keys[i];
+        if (v != kInvalid) atomicAdd(&hist[((v * kWarmMul) & mask) >> kWarmLocalBits], 1u);
     }
-    for (uint32_t i = 4 * nvec + blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += stride) {   // tail words
-        const uint32_t c = wcnt[i];
-        if (!c) continue;
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < w.nbk; b += blockDim.x) {
+        const uint32_t c = hist[b];
+        base[b] = c ? atomicAdd(&w.cur[b], c) : 0u;
+        hist[b] = 0u;
+    }
+    __syncthreads();
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        const uint32_t v = w.keys[i];
+        if (v == kInvalid) continue;
+        const uint32_t h = (v * kWarmMul) & mask;
+        const uint32_t b = h >> kWarmLocalBits;
+        const uint32_t pos = base[b] + atomicAdd(&hist[b], 1u);
+        if (pos < w.cap) w.part[(uint64_t)b * w.cap + pos] = (uint16_t)(h & 0xFFFFu);
+    }
+}
+
+__device__ __forceinline__ uint32_t block_excl_scan_1024(uint32_t x, uint32_t* s_w, uint32_t* total) {
+    // exclusive prefix of x over a 1024-thread workgroup (s_w: 16 words of LDS)
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t incl = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) s_w[wid] = incl;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        const uint32_t t = s_w[w];
+        before += (w < wid) ? t : 0u;
+        all += t;
+    }
+    *total = all;
+    return before + incl - x;
+}
+
+// Counts one bucket's hash values in LDS and lists its ids seen twice or more (one global atomic
+// per workgroup: a wave-aggregated append per scan step put 0.5M same-address atomics on the list
+// length, 6 ms per build).
+__global__ __launch_bounds__(1024) void k_warm_count(WarmBuild w) {
+    if (*w.valid) return;                            // uniform
+    constexpr uint32_t kWords = 1u << (kWarmLocalBits - 1);   // 2^16 16-bit counters
+    constexpr uint32_t kPer = kWords / 1024;
+    __shared__ uint32_t cnt[kWords];
+    __shared__ uint32_t s_w[16];
+    __shared__ unsigned long long s_base;
+    const uint32_t b = blockIdx.x;
+    const uint32_t m = min(w.cur[b], w.cap);
+    if (m == 0) return;                              // uniform
+    for (uint32_t i = threadIdx.x; i < kWords; i += blockDim.x) cnt[i] = 0u;
+    __syncthreads();
+    const uint16_t* p = w.part + (uint64_t)b * w.cap;
+    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+        const uint32_t li = p[i];
+        const uint32_t sh = (li & 1u) << 4;
+        // counts saturate near 1024 (bands need 32): with at most 1024 racing adds past the
+        // check a 16-bit half never carries into its neighbour's
+        if (((cnt[li >> 1] >> sh) & 0xFFFFu) < 1024u) atomicAdd(&cnt[li >> 1], 1u << sh);
+    }
+    __syncthreads();
+    // thread t owns counter words [t * kPer, (t + 1) * kPer)
+    uint32_t mine = 0;
+    for (uint32_t j = 0; j < kPer; ++j) {
+        const uint32_t c = cnt[threadIdx.x * kPer + j];
+        mine += ((c & 0xFFFFu) >= 2u) + ((c >> 16) >= 2u);
+    }
+    uint32_t total;
+    const uint32_t off = block_excl_scan_1024(mine, s_w, &total);
+    if (total == 0) return;                          // uniform
+    if (threadIdx.x == 0) s_base = atomicAdd(&w.ctl[1], (unsigned long long)total);
+    __syncthreads();
+    uint2* out = reinterpret_cast<uint2*>(w.keys) + s_base + off;
+    const uint32_t mask = (w.B >= 32) ? ~0u : ((1u << w.B) - 1);
+    for (uint32_t j = 0; j < kPer; ++j) {
+        const uint32_t i = threadIdx.x * kPer + j;
+        const uint32_t c = cnt[i];
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const uint32_t ck = (c >> (16 * k)) & 0xFFFFu;
-            const uint32_t v = 2 * i + k;
-            if (ck >= lo && ck < hi && ((gbits[v >> 5] >> (v & 31)) & 1u) && !(hot && hot_probe(hot, v, B, five != 0)))
-                warm_insert(warm, v, B, wb);
+            if (ck >= 2u) {
+                const uint32_t h = (b << kWarmLocalBits) | (2 * i + k);
+                *out++ = make_uint2((h * kWarmMulInv) & mask, ck);
+            }
         }
-        if (done) wcnt[i] = 0u;
     }
 }
-__global__ void k_warm_done(uint32_t* __restrict__ valid) { *valid = 1u; }
+
+// Band inserts, hottest first (a full bucket then drops the colder ids). A listed id enters only
+// if gbits holds it — the count launch wrote only giant members, but the gbits check keeps the set
+// exact whatever the key slots hold (a count launch without a giant writes none) — and the hot set
+// (admitting meanwhile) does not.
+__global__ __launch_bounds__(256) void k_warm_insert(WarmBuild w, uint32_t wb, const uint32_t* __restrict__ gbits,
+                                                     const uint2* __restrict__ hot, uint32_t five) {
+    if (*w.valid) return;                            // uniform
+    const uint64_t n = w.ctl[1];
+    const uint2* list = reinterpret_cast<const uint2*>(w.keys);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (int j = 0; j < (int)(sizeof(kWarmBands) / sizeof(kWarmBands[0])) - 1; ++j) {
+        const uint32_t hi = kWarmBands[j], lo = kWarmBands[j + 1];
+        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+            const uint2 e = list[i];
+            if (e.y >= lo && e.y < hi && ((gbits[e.x >> 5] >> (e.x & 31)) & 1u) && !(hot && hot_probe(hot, e.x, w.B, five != 0)))
+                warm_insert(w.warm, e.x, w.B, wb);
+        }
+    }
+}
+
+// End of a build (or of a scheduled check that found the set valid): valid again, counters zeroed.
+__global__ __launch_bounds__(1024) void k_warm_done(WarmBuild w, uint32_t* __restrict__ valid) {
+    for (uint32_t b = threadIdx.x; b < w.nbk; b += blockDim.x) w.cur[b] = 0u;
+    if (threadIdx.x == 0) {
+        w.ctl[1] = 0;
+        *valid = 1u;
+    }
+}
 
 // DisjointSet.merge(other) with other given as a dense parent array: union(v, other[v]) for
 // every v in other (DisjointSet.java:127-131 iterates other.getMatches()).

@@ -3,6 +3,7 @@
 # the per-window profile of the headline stream per variant, alternating twice.
 # usage (repo root, GPU box): bash tools/exp_run.sh <tag> [windows]
 set -u
+shopt -s nullglob
 TAG=${1:-r02}; NW=${2:-40}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG/exp
 mkdir -p "$OUT"
