@@ -85,9 +85,9 @@ struct gs_cc {
     uint32_t* hot_cand = nullptr;        // hot-set admission candidates (2^kHotCandBits ids)
     uint32_t* warm = nullptr;            // warm set (2^warm_bits words, L2-resident), steady folds
     uint32_t warm_bits = 0;
-    uint32_t* wkeys = nullptr;           // warm build: sampled endpoint keys, then the (id, count) list
+    uint32_t* wkeys = nullptr;           // warm build: sampled endpoint key slots
     uint16_t* wpart = nullptr;           // warm build: keys by hash bucket
-    unsigned long long* wctl = nullptr;  // warm build: [0] keys, [1] list length, then bucket fills
+    unsigned long long* wctl = nullptr;  // warm build: [0] edges counted, then bucket fills (u32)
     uint64_t warm_sample = 0;            // edges a warm count launch samples
     uint32_t warm_bcap = 0;              // keys per hash bucket
     int cus = 0;                         // compute units: k_fold_ring grid
@@ -317,15 +317,14 @@ static WarmBuild warm_build_args(gs_cc_t* h) {
     WarmBuild w;
     w.keys = h->wkeys;
     w.ctl = h->wctl;
-    w.cur = reinterpret_cast<uint32_t*>(h->wctl + 2);
+    w.cur = reinterpret_cast<uint32_t*>(h->wctl + 1);
     w.part = h->wpart;
     w.keys_cap = 2 * h->warm_sample;
-    w.keys_n = 0;
     w.cap = h->warm_bcap;
     w.B = h->hot_bits;
     w.nbk = 1u << (h->hot_bits - kWarmLocalBits);
     w.warm = h->warm;
-    w.warm_words = 1u << h->warm_bits;
+    w.wb = h->warm_bits;
     w.valid = h->derr + 7;
     return w;
 }
@@ -350,6 +349,7 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     hot.warm_bits = h->warm_bits;
     hot.warm_valid = h->derr + 7;
     hot.wkeys = build ? h->wkeys : nullptr;
+    hot.wctl = h->wctl;
     hot.count_edges = build ? h->warm_sample : 0;
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
     f.mark_len = h->mark_ctr;
@@ -366,16 +366,10 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
         else klaunch(k_fold_ring<IdT, false, false>, grid, dim3(kHotThreads), h->stream, start, stop, a, b, f, hot);
     }
     if (build) {
-        WarmBuild w = warm_build_args(h);
-        // the count launch wrote 512 keys per wave step of 256 edges over its first
-        // min(n, warm_sample) edges (k_fold_ring takes groups of 4 edges)
-        const uint64_t counted = std::min<uint64_t>(h->warm_sample, n / 4 * 4);
-        w.keys_n = (counted + 255) / 256 * 512;
+        const WarmBuild w = warm_build_args(h);
         klaunch(k_warm_part, dim3((unsigned)((w.keys_cap + kWarmPartTile - 1) / kWarmPartTile)), dim3(1024), h->stream, nullptr,
                 nullptr, w);
         klaunch(k_warm_count, dim3(w.nbk), dim3(1024), h->stream, nullptr, nullptr, w);
-        klaunch(k_warm_insert, dim3(2048), dim3(256), h->stream, nullptr, nullptr, w, h->warm_bits, (const uint32_t*)h->gbits,
-                (const uint2*)h->hot, hot.five);
         klaunch(k_warm_done, dim3(1), dim3(1024), h->stream, nullptr, t.stop(), w, h->derr + 7);
     }
 }
@@ -832,13 +826,13 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
             // L2-resident and at most 1/8 of gbits (8-bit slots need at least 2^(B-8) buckets)
             h->warm_bits = std::min<uint32_t>(kWarmBucketsMaxBits, bits - 6);
             if (h->hot && bits >= dbg().ring_min_bits && bits <= h->warm_bits + 8 && bits >= kWarmLocalBits &&
-                bits - kWarmLocalBits <= 13) {
+                bits - kWarmLocalBits <= 13 && bits - h->warm_bits <= kWarmLocalBits) {
                 h->warm_sample = std::min<uint64_t>(kWarmSample, h->cap / 8);
                 const uint32_t nbk = 1u << (bits - kWarmLocalBits);
                 h->warm_sample = (h->warm_sample + 255) / 256 * 256;        // whole wave steps
                 const uint64_t keys = 2 * h->warm_sample;
-                h->warm_bcap = (uint32_t)(keys / nbk + keys / nbk / 2 + 1024);   // 1.5 x the mean bucket
-                const size_t ctl = 2 * sizeof(unsigned long long) + (size_t)nbk * 4;
+                h->warm_bcap = (uint32_t)((keys / nbk + keys / nbk / 2 + 1024 + 7) & ~7ull);  // 1.5 x the mean bucket
+                const size_t ctl = sizeof(unsigned long long) + (size_t)nbk * 4;
                 if (hipMalloc(&h->warm, (size_t)4 << h->warm_bits) != hipSuccess ||
                     hipMalloc(&h->wkeys, keys * 4) != hipSuccess ||
                     hipMalloc(&h->wpart, (size_t)nbk * h->warm_bcap * 2) != hipSuccess ||

@@ -325,6 +325,7 @@ struct HotArgs {
     uint32_t warm_bits = 0;                    // log2(warm buckets), B - 8 <= warm_bits <= B
     const uint32_t* warm_valid = nullptr;      // device word: warm set built for the current giant
     uint32_t* wkeys = nullptr;                 // warm build: endpoint keys, 512 per wave step (count launches only)
+    unsigned long long* wctl = nullptr;        // warm build: edges counted (written by count launches)
     uint64_t count_edges = 0;                  // count this launch's first edges (if !*warm_valid)
 };
 
@@ -339,8 +340,6 @@ struct HotArgs {
 // first count_edges edges (LDS misses confirmed in the giant), hottest first (k_warm_part below);
 // valid (hot.warm_valid) while the giant is the same component, like the hot set.
 constexpr uint32_t kWarmMul = 0x85EBCA6Bu;
-// count bands of a build, inserted hottest first (2 bands: +0.17 ms per RMAT-26 step)
-constexpr uint32_t kWarmBands[] = {0xFFFFFFFFu, 32u, 8u, 3u, 2u};
 // wb = log2(buckets); remainders of B - wb <= 8 bits, slot value r = rem + 1 in [1, 256]: the one
 // value that does not fit a byte (256: 1 id in 256 when B - wb = 8) never enters nor matches.
 __device__ __forceinline__ uint32_t warm_hash(uint32_t v, uint32_t B) { return (v * kWarmMul) & ((1u << B) - 1); }
@@ -351,28 +350,6 @@ __device__ __forceinline__ bool warm_probe(const uint32_t* __restrict__ warm, ui
     const uint32_t x = warm[h >> rb] ^ (r * 0x01010101u);
     return r <= 0xFFu && ((x - 0x01010101u) & ~x & 0x80808080u) != 0;    // a byte equal to r
 }
-__device__ inline void warm_insert(uint32_t* __restrict__ warm, uint32_t v, uint32_t B, uint32_t wb) {
-    const uint32_t h = warm_hash(v, B);
-    const uint32_t rb = B - wb;
-    const uint32_t r = (h & ((1u << rb) - 1)) + 1;
-    if (r > 0xFFu) return;
-    uint32_t* p = warm + (h >> rb);
-    uint32_t x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int attempt = 0; attempt < 8; ++attempt) {
-        int empty = -1;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t fk = (x >> (8 * k)) & 0xFFu;
-            if (fk == r) return;
-            if (fk == 0 && empty < 0) empty = k;
-        }
-        if (empty < 0) return;                               // bucket full
-        const uint32_t old = atomicCAS(p, x, x | (r << (8 * empty)));
-        if (old == x) return;
-        x = old;
-    }
-}
-
 // Admission cadence. Offering a launch's first 2^18 edges costs ~28 us per RMAT-26 window (the
 // candidate table's atomics); the hubs are stable, so a launch admits only while *budget > 0
 // (kHotAdmitLaunches after reset or after k_compress clears the set for a new giant) or when the
@@ -698,6 +675,8 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
     const uint64_t count_edges = (filt && hot.wkeys && hot.warm_valid && *hot.warm_valid == 0) ? hot.count_edges : 0;
     __syncthreads();
     if (blockIdx.x == 0 && threadIdx.x == 0 && hot.budget && budget) *hot.budget = budget - 1;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && hot.wkeys)            // key slots written below
+        *hot.wctl = (min(count_edges, n / 4 * 4) + 255) / 256 * 256;
     const int lane = threadIdx.x & 63;
     uint2* const ring = rings[threadIdx.x >> 6];
     uint32_t cnt = 0;                                // wave-uniform ring fill
@@ -767,36 +746,31 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
 }
 
 // Warm build without global counters (the count launch's per-endpoint atomicAdd into 2^B 16-bit
-// counters cost ~390 us and four scans of them ~400 us per RMAT-26 build): the count launch
-// writes its LDS-miss giant endpoints to a key list (512 slots per wave step); k_warm_part
-// scatters them by h = warm_hash(v) into 2^(B-16) buckets of 2^16 hash values (per-workgroup LDS
-// histogram, one atomicAdd per (workgroup, bucket) for the bucket cursor); k_warm_count counts a
-// bucket in LDS (2^16 16-bit counters = 128 KiB) and lists (v, count >= 2), v recovered from h by
-// the inverse multiplier; k_warm_insert inserts the list hottest band first. Every kernel is a
-// no-op while the set is valid (*valid), so the host schedules builds without reading it back.
+// counters cost ~390 us and four band scans of them ~400 us per RMAT-26 build): the count launch
+// writes its LDS-miss giant endpoints into key slots (512 per wave step, kInvalid where none);
+// k_warm_part scatters their hashes h = warm_hash(v) into 2^(B-16) buckets of 2^16 hash values
+// (per-workgroup LDS histogram, one atomicAdd per (workgroup, bucket) for the bucket cursor);
+// k_warm_count counts a bucket in LDS (2^16 16-bit counters = 128 KiB). A bucket's hash values
+// are exactly those of warm buckets [b << (16 - rb), (b + 1) << (16 - rb)) (warm bucket = h >> rb,
+// rb = B - wb <= 16), so the workgroup owns those table words: each is written once, with plain
+// stores, holding its 4 most counted ids (count >= 2) — no CAS inserts, no count bands, and the
+// exact top 4 per bucket instead of band order. Every kernel is a no-op while the set is valid
+// (*valid), so the host schedules builds without reading it back.
 constexpr uint32_t kWarmLocalBits = 16;              // hash values per bucket: 2^16
 constexpr uint32_t kWarmPartTile = 1u << 16;          // keys per k_warm_part workgroup (64 per thread)
 constexpr uint32_t kWarmMaxBuckets = 1u << 13;        // B <= 29
-constexpr uint32_t inv_odd(uint32_t a) {
-    uint32_t x = a;                                  // Newton: 5 steps give 32 bits
-    for (int i = 0; i < 5; ++i) x *= 2u - a * x;
-    return x;
-}
-constexpr uint32_t kWarmMulInv = inv_odd(kWarmMul);
-static_assert(kWarmMul * kWarmMulInv == 1u, "warm hash inverse");
 
 struct WarmBuild {
-    uint32_t* keys;                  // appended endpoint ids; after k_warm_part the (v, count) list
-    unsigned long long* ctl;         // [1] list length
+    uint32_t* keys;                  // key slots the count launch wrote
+    unsigned long long* ctl;         // [0] edges the count launch counted (0: none, e.g. no giant yet)
     uint32_t* cur;                   // per-bucket fill (nbk words)
     uint16_t* part;                  // nbk buckets x cap local hash values
-    uint64_t keys_cap;               // key list capacity (2 x sampled edges)
-    uint64_t keys_n;                 // keys the count launch wrote (kInvalid where none)
-    uint32_t cap;                    // bucket capacity (keys past it are dropped: counts only rank)
+    uint64_t keys_cap;               // key slot capacity (2 x sampled edges)
+    uint32_t cap;                    // bucket capacity, a multiple of 8 (keys past it are dropped: counts only rank)
     uint32_t B;                      // ids < 2^B
     uint32_t nbk;                    // 2^(B - 16) buckets
-    uint32_t* warm;                  // the warm table (zeroed by k_warm_part)
-    uint32_t warm_words;
+    uint32_t* warm;                  // the warm table
+    uint32_t wb;                     // log2(warm table words), B - 16 <= wb
     const uint32_t* valid;
 };
 
@@ -804,18 +778,30 @@ __global__ __launch_bounds__(1024) void k_warm_part(WarmBuild w) {
     if (*w.valid) return;                            // uniform
     __shared__ uint32_t hist[kWarmMaxBuckets];
     __shared__ uint32_t base[kWarmMaxBuckets];
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < w.warm_words; i += gridDim.x * blockDim.x) w.warm[i] = 0u;
-    const uint64_t n = min(w.keys_n, w.keys_cap);
+    const uint64_t n = min(2 * w.ctl[0], w.keys_cap);    // a multiple of 512
     const uint64_t lo = (uint64_t)blockIdx.x * kWarmPartTile;
     const uint64_t hi = min(n, lo + kWarmPartTile);
     if (lo >= hi) return;                            // uniform
     const uint32_t mask = (w.B >= 32) ? ~0u : ((1u << w.B) - 1);
     for (uint32_t b = threadIdx.x; b < w.nbk; b += blockDim.x) hist[b] = 0u;
-    __syncthreads();
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        const uint32_t v = w.keys[i];
-        if (v != kInvalid) atomicAdd(&hist[((v * kWarmMul) & mask) >> kWarmLocalBits], 1u);
+    // the tile's keys stay in registers: 16 x 16-B loads per thread, all issued before any use
+    // (a dependent load per loop step made the two passes latency-bound: 133 -> 99 us per build)
+    constexpr int kVec = kWarmPartTile / 4 / 1024;
+    const u32x4* src = reinterpret_cast<const u32x4*>(w.keys + lo);
+    const uint32_t nvec = (uint32_t)((hi - lo) / 4);
+    uint32_t hv[4 * kVec];
+#pragma unroll
+    for (int j = 0; j < kVec; ++j) {
+        const uint32_t vi = j * 1024 + threadIdx.x;
+        const u32x4 q = vi < nvec ? src[vi] : u32x4{kInvalid, kInvalid, kInvalid, kInvalid};
+        const uint32_t k4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hv[4 * j + e] = k4[e] == kInvalid ? kInvalid : (k4[e] * kWarmMul) & mask;
     }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4 * kVec; ++j)
+        if (hv[j] != kInvalid) atomicAdd(&hist[hv[j] >> kWarmLocalBits], 1u);
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < w.nbk; b += blockDim.x) {
         const uint32_t c = hist[b];
@@ -823,105 +809,95 @@ __global__ __launch_bounds__(1024) void k_warm_part(WarmBuild w) {
         hist[b] = 0u;
     }
     __syncthreads();
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        const uint32_t v = w.keys[i];
-        if (v == kInvalid) continue;
-        const uint32_t h = (v * kWarmMul) & mask;
-        const uint32_t b = h >> kWarmLocalBits;
-        const uint32_t pos = base[b] + atomicAdd(&hist[b], 1u);
-        if (pos < w.cap) w.part[(uint64_t)b * w.cap + pos] = (uint16_t)(h & 0xFFFFu);
-    }
-}
-
-__device__ __forceinline__ uint32_t block_excl_scan_1024(uint32_t x, uint32_t* s_w, uint32_t* total) {
-    // exclusive prefix of x over a 1024-thread workgroup (s_w: 16 words of LDS)
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t incl = x;
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
+    for (int j = 0; j < 4 * kVec; ++j) {
+        if (hv[j] == kInvalid) continue;
+        const uint32_t b = hv[j] >> kWarmLocalBits;
+        const uint32_t pos = base[b] + atomicAdd(&hist[b], 1u);
+        if (pos < w.cap) w.part[(uint64_t)b * w.cap + pos] = (uint16_t)(hv[j] & 0xFFFFu);
     }
-    if (lane == 63) s_w[wid] = incl;
-    __syncthreads();
-    uint32_t before = 0, all = 0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
-        const uint32_t t = s_w[w];
-        before += (w < wid) ? t : 0u;
-        all += t;
-    }
-    *total = all;
-    return before + incl - x;
 }
 
-// Counts one bucket's hash values in LDS and lists its ids seen twice or more (one global atomic
-// per workgroup: a wave-aggregated append per scan step put 0.5M same-address atomics on the list
-// length, 6 ms per build).
 __global__ __launch_bounds__(1024) void k_warm_count(WarmBuild w) {
     if (*w.valid) return;                            // uniform
     constexpr uint32_t kWords = 1u << (kWarmLocalBits - 1);   // 2^16 16-bit counters
-    constexpr uint32_t kPer = kWords / 1024;
     __shared__ uint32_t cnt[kWords];
-    __shared__ uint32_t s_w[16];
-    __shared__ unsigned long long s_base;
     const uint32_t b = blockIdx.x;
     const uint32_t m = min(w.cur[b], w.cap);
-    if (m == 0) return;                              // uniform
     for (uint32_t i = threadIdx.x; i < kWords; i += blockDim.x) cnt[i] = 0u;
     __syncthreads();
-    const uint16_t* p = w.part + (uint64_t)b * w.cap;
-    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-        const uint32_t li = p[i];
-        const uint32_t sh = (li & 1u) << 4;
-        // counts saturate near 1024 (bands need 32): with at most 1024 racing adds past the
-        // check a 16-bit half never carries into its neighbour's
-        if (((cnt[li >> 1] >> sh) & 0xFFFFu) < 1024u) atomicAdd(&cnt[li >> 1], 1u << sh);
-    }
-    __syncthreads();
-    // thread t owns counter words [t * kPer, (t + 1) * kPer)
-    uint32_t mine = 0;
-    for (uint32_t j = 0; j < kPer; ++j) {
-        const uint32_t c = cnt[threadIdx.x * kPer + j];
-        mine += ((c & 0xFFFFu) >= 2u) + ((c >> 16) >= 2u);
-    }
-    uint32_t total;
-    const uint32_t off = block_excl_scan_1024(mine, s_w, &total);
-    if (total == 0) return;                          // uniform
-    if (threadIdx.x == 0) s_base = atomicAdd(&w.ctl[1], (unsigned long long)total);
-    __syncthreads();
-    uint2* out = reinterpret_cast<uint2*>(w.keys) + s_base + off;
-    const uint32_t mask = (w.B >= 32) ? ~0u : ((1u << w.B) - 1);
-    for (uint32_t j = 0; j < kPer; ++j) {
-        const uint32_t i = threadIdx.x * kPer + j;
-        const uint32_t c = cnt[i];
+    // 8 hash values per 16-B load (w.cap is a multiple of 8), a thread's loads issued together
+    const u32x4* p = reinterpret_cast<const u32x4*>(w.part + (uint64_t)b * w.cap);
+    const uint32_t nv = (m + 7) / 8;
+    for (uint32_t v0 = 0; v0 < nv; v0 += 4 * 1024) {
+        u32x4 q[4];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const uint32_t ck = (c >> (16 * k)) & 0xFFFFu;
-            if (ck >= 2u) {
-                const uint32_t h = (b << kWarmLocalBits) | (2 * i + k);
-                *out++ = make_uint2((h * kWarmMulInv) & mask, ck);
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t vi = v0 + j * 1024 + threadIdx.x;
+            q[j] = vi < nv ? p[vi] : u32x4{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t vi = v0 + j * 1024 + threadIdx.x;
+            const uint32_t w4[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                if (vi * 8 + e >= m) continue;
+                const uint32_t li = (w4[e >> 1] >> ((e & 1) * 16)) & 0xFFFFu;
+                const uint32_t sh = (li & 1u) << 4;
+                // counts saturate near 1024: with at most 1024 racing adds past the check a
+                // 16-bit half never carries into its neighbour's
+                if (((cnt[li >> 1] >> sh) & 0xFFFFu) < 1024u) atomicAdd(&cnt[li >> 1], 1u << sh);
             }
         }
     }
-}
-
-// Band inserts, hottest first (a full bucket then drops the colder ids). A listed id enters only
-// if gbits holds it — the count launch wrote only giant members, but the gbits check keeps the set
-// exact whatever the key slots hold (a count launch without a giant writes none) — and the hot set
-// (admitting meanwhile) does not.
-__global__ __launch_bounds__(256) void k_warm_insert(WarmBuild w, uint32_t wb, const uint32_t* __restrict__ gbits,
-                                                     const uint2* __restrict__ hot, uint32_t five) {
-    if (*w.valid) return;                            // uniform
-    const uint64_t n = w.ctl[1];
-    const uint2* list = reinterpret_cast<const uint2*>(w.keys);
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (int j = 0; j < (int)(sizeof(kWarmBands) / sizeof(kWarmBands[0])) - 1; ++j) {
-        const uint32_t hi = kWarmBands[j], lo = kWarmBands[j + 1];
-        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-            const uint2 e = list[i];
-            if (e.y >= lo && e.y < hi && ((gbits[e.x >> 5] >> (e.x & 31)) & 1u) && !(hot && hot_probe(hot, e.x, w.B, five != 0)))
-                warm_insert(w.warm, e.x, w.B, wb);
+    __syncthreads();
+    // warm word t of this bucket: its 2^rb hash values are local [t << rb, (t + 1) << rb); slot
+    // value r = low rb bits + 1 (r = 256 does not fit a byte and never enters; warm_probe never
+    // matches it). Four lanes per word each keep the top 4 of a quarter as packed (count << 16 | r)
+    // keys, sorted; two bitonic merges over lanes ^1 and ^2 leave the word's top 4 (one lane per
+    // word scanning all 2^rb counters: 167 us per build).
+    const uint32_t rb = w.B - w.wb;
+    const uint32_t words = 1u << (kWarmLocalBits - rb);
+    const uint32_t qw = 1u << (rb - 3);              // counter words per quarter (2 counters each)
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t task = threadIdx.x; task < 4 * words; task += blockDim.x) {   // groups of 4 lanes stay whole
+        const uint32_t t = task >> 2, q = task & 3;
+        uint32_t top[4] = {0u, 0u, 0u, 0u};
+        const uint32_t base = (t << (rb - 1)) + q * qw;
+        for (uint32_t j = 0; j < qw; ++j) {
+            const uint32_t jj = (j + lane) & (qw - 1);   // rotated start: lanes spread over banks
+            const uint32_t c2 = cnt[base + jj];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t c = (c2 >> (16 * k)) & 0xFFFFu;
+                const uint32_t r = 2 * (q * qw + jj) + k + 1;
+                uint32_t x = (c >= 2u && r <= 0xFFu) ? ((c << 16) | r) : 0u;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {        // sorted insertion, descending
+                    const uint32_t hi = max(top[i], x);
+                    x = min(top[i], x);
+                    top[i] = hi;
+                }
+            }
         }
+#pragma unroll
+        for (int off = 1; off <= 2; off <<= 1) {
+            uint32_t o[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[i] = __shfl_xor(top[i], off, 64);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) top[i] = max(top[i], o[3 - i]);   // bitonic: the 4 largest
+            uint32_t x0 = max(top[0], top[2]), x2 = min(top[0], top[2]);
+            uint32_t x1 = max(top[1], top[3]), x3 = min(top[1], top[3]);
+            top[0] = max(x0, x1);
+            top[1] = min(x0, x1);
+            top[2] = max(x2, x3);
+            top[3] = min(x2, x3);
+        }
+        if (q == 0)
+            w.warm[((uint64_t)b << (kWarmLocalBits - rb)) + t] =
+                (top[0] & 0xFFu) | ((top[1] & 0xFFu) << 8) | ((top[2] & 0xFFu) << 16) | ((top[3] & 0xFFu) << 24);
     }
 }
 
@@ -929,7 +905,7 @@ __global__ __launch_bounds__(256) void k_warm_insert(WarmBuild w, uint32_t wb, c
 __global__ __launch_bounds__(1024) void k_warm_done(WarmBuild w, uint32_t* __restrict__ valid) {
     for (uint32_t b = threadIdx.x; b < w.nbk; b += blockDim.x) w.cur[b] = 0u;
     if (threadIdx.x == 0) {
-        w.ctl[1] = 0;
+        w.ctl[0] = 0;
         *valid = 1u;
     }
 }
