@@ -221,15 +221,11 @@ constexpr unsigned kCompressGrid = 2048;
 constexpr uint32_t kRingMinBits = 25;
 // warm set: counted in ring launch kWarmAt after reset (the first warm_sample edges: kWarmSample,
 // at most capacity/8) and re-checked every kWarmEvery-th launch (rebuilt only when invalid for the
-// current giant); inserted in 4 count bands, hottest first
-#if defined(GS_EXP_WS24)
-constexpr uint64_t kWarmAt = 3, kWarmEvery = 16, kWarmSample = 1ull << 24;
-#else
-constexpr uint64_t kWarmAt = 3, kWarmEvery = 16, kWarmSample = 1ull << 23;
-#endif
-constexpr uint32_t kWarmBucketsMaxBits = 18;        // 2^18 x 4 B = 1 MiB table at RMAT-26 (2 MiB with
-                                                    // 2^24-edge samples: 5 us less per steady window,
-                                                    // 0.44 ms more count per step; profiles/r02_d)
+// current giant). Launch 2 (RMAT-26 window 4): windows 2-12 35 us less than launch 3, as launch 0
+// or 1 (profiles/r02_ab_experiments.txt r02_w); 2^24-edge samples gained nothing (r02_u)
+constexpr uint64_t kWarmAt = 2, kWarmEvery = 16, kWarmSample = 1ull << 23;
+constexpr uint32_t kWarmBucketsMaxBits = 18;        // 2^18 x 4 B = 1 MiB table at RMAT-26 (2 MiB: 2-4 us
+                                                    // slower per steady window, r02_u)
 constexpr uint32_t kHotThresh = 3;                  // sightings before hot-set admission (233 -> 229 us)
 // Young split: inside the young forest, close internally (compress + giant pick: no emission,
 // labels stay canonical) after capacity/16 edges, so the rest of the young window folds with the

@@ -25,6 +25,66 @@ def load(passdir):
     return vals, calls
 
 
+def fold_sequence(passdir):
+    """Counters of each fold launch (k_fold / k_fold_ring) in dispatch order."""
+    files = glob.glob(os.path.join(passdir, "**", "*counter_collection.csv"), recursive=True)
+    per = defaultdict(lambda: defaultdict(float))
+    name = {}
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            if "k_fold" not in k:
+                continue
+            d = int(r.get("Dispatch_Id") or r.get("Correlation_Id"))
+            per[d][r["Counter_Name"]] += float(r["Counter_Value"])
+            name[d] = k
+    return [(name[d], per[d]) for d in sorted(per)]
+
+
+def young_windows(root, window_edges):
+    """Per-window fold counters of the first bench step: window 1 = the two young k_fold launches
+    (split at capacity/16), window w >= 2 = its k_fold_ring launch; windows 13.. averaged."""
+    seqs = [fold_sequence(p) for p in sorted(glob.glob(os.path.join(root, "p*"))) if os.path.isdir(p)]
+    seqs = [q for q in seqs if q]
+    if not seqs:
+        return None
+    n = min(len(q) for q in seqs)
+    launches = []
+    for i in range(n):
+        c = {}
+        for q in seqs:
+            c.update(q[i][1])
+        launches.append((seqs[0][i][0], c))
+    wins = []
+    i = 0
+    while i < n and len(wins) < 64:
+        k, c = launches[i]
+        group = [c]
+        if "k_fold_ring" not in k and i + 1 < n and "k_fold_ring" not in launches[i + 1][0] and not wins:
+            group.append(launches[i + 1][1])     # window 1: young head + rest
+            i += 1
+        i += 1
+        tot = defaultdict(float)
+        for g in group:
+            for kk, vv in g.items():
+                tot[kk] += vv
+        wins.append(tot)
+    rows = []
+    for w, t in enumerate(wins, 1):
+        h, m = t.get("TCC_HIT_sum", 0.0), t.get("TCC_MISS_sum", 0.0)
+        rows.append({"window": w, "fetch_bytes_raw": t.get("FETCH_SIZE", 0.0) * 1024,
+                     "write_bytes": t.get("WRITE_SIZE", 0.0) * 1024,
+                     "hbm_bytes": t.get("FETCH_SIZE", 0.0) * 1024 + 4 * window_edges + t.get("WRITE_SIZE", 0.0) * 1024,
+                     "tcc_requests": h + m, "l2_hit_rate": h / (h + m) if h + m else None,
+                     "memory_side_atomics": t.get("TCC_EA0_ATOMIC_sum", 0.0)})
+    steady = rows[12:]
+    avg = {k: sum(r[k] for r in steady) / len(steady) for k in ("fetch_bytes_raw", "write_bytes", "hbm_bytes",
+                                                              "tcc_requests", "memory_side_atomics")} if steady else None
+    return {"windows_1_12": rows[:12], "steady_mean_13_on": avg,
+            "note": "per window of the first bench step; hbm_bytes adds back half the 8 B/edge stream "
+                    "(gfx950 FETCH_SIZE reports wide streaming reads at 1/2)"}
+
+
 def main():
     root = sys.argv[1]
     agg = defaultdict(dict)
@@ -78,6 +138,7 @@ def main():
             "tcc_requests_per_launch": (h_ + m_) / nl,
             "memory_side_atomics_per_launch": agg[k].get("TCC_EA0_ATOMIC_sum", 0.0) / nl,
         }
+    out["per_window"] = young_windows(root, out.get("window_edges", 0))
     # streaming edge read (8 B/edge, 16 B/lane loads) is under-reported 2x: add it back once
     edge_bytes = 8 * out.get("window_edges", 0)
     out["hbm_bytes_per_window"] = out["fold"]["fetch_bytes_raw_per_window"] + edge_bytes / 2 + out["fold"]["write_bytes_per_window"]

@@ -10,7 +10,11 @@ st = [int(r["Start_Timestamp"]) for r in rows]
 en = [int(r["End_Timestamp"]) for r in rows]
 # the timed steps: the rows between the first and the last k_stats-free stretch; take the second
 # full step (warmup 1 + timed 2): a step starts at k_fold after a reset fill
-starts = [i for i in range(1, len(rows)) if name[i].startswith("k_fold<") and "fill" in name[i - 1]]
+def after_reset(i):          # gs_cc_reset's memsets: several fills right before the step's first fold
+    return i >= 3 and all("fill" in name[j] for j in range(i - 3, i))
+
+
+starts = [i for i in range(1, len(rows)) if name[i].startswith("k_fold<") and after_reset(i)]
 if len(starts) < 3:
     sys.exit("need >= 3 steps in the trace")
 a, b = starts[1], starts[2]
