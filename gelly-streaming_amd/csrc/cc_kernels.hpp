@@ -472,21 +472,39 @@ __device__ __forceinline__ void union_group(const FoldArgs& f, const uint32_t (&
 // in the young forest the giant root gR is hooked again and again, and every walk from a stand-in
 // gR then halves a shared word (x = a hub, or gR's own word when the walk starts at gR):
 // one same-address atomic per edge, window 1 1.3 -> 2.7 ms; taking gR itself for a root instead
-// fails every hook CAS on gR's word once it is hooked (14 ms). A/B in profiles/r01_v12
+// fails every hook CAS on gR's word once it is hooked (14 ms). A/B in profiles/r01_v12.
+// An endpoint outside the giant next to one inside is first claimed straight under gR (below):
+// windows 2-12 -158 us, steady -2.5 us per window (profiles/r02_ab_experiments.txt r02_aa).
 template <bool MARK, bool STATS, int EPT>
 __device__ __forceinline__ void union_group_g(const FoldArgs& f, const uint32_t (&u)[EPT], const uint32_t (&v)[EPT],
                                               const bool (&ok)[EPT], const uint32_t (&gflag)[EPT], uint32_t gR,
                                               FoldStats& st) {
     uint32_t pu[EPT], pv[EPT];
+    // one endpoint in the giant, the other x > gR: claim x straight under gR with a CAS from
+    // kInvalid instead of gathering parent[x] first. Success = x was never touched, and hanging a
+    // fresh singleton below any giant member (gR < x keeps parent[x] < x) is its union with the
+    // giant; failure returns parent[x], the word the gather would have read.
+    bool claimed[EPT];
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
-        pu[k] = !ok[k] ? 0u : (gflag[k] & 1u) ? gR : f.parent[u[k]];
-        pv[k] = !ok[k] ? 0u : (gflag[k] & 2u) ? gR : f.parent[v[k]];
+        const bool cu = ok[k] && gflag[k] == 2u && u[k] > gR;      // v in the giant, u outside
+        const bool cv = ok[k] && gflag[k] == 1u && v[k] > gR;      // u in the giant, v outside
+        pu[k] = !ok[k] ? 0u : (gflag[k] & 1u) ? gR : cu ? atomicCAS(&f.parent[u[k]], kInvalid, gR) : f.parent[u[k]];
+        pv[k] = !ok[k] ? 0u : (gflag[k] & 2u) ? gR : cv ? atomicCAS(&f.parent[v[k]], kInvalid, gR) : f.parent[v[k]];
+        claimed[k] = (cu && pu[k] == kInvalid) || (cv && pv[k] == kInvalid);
     }
     uint32_t m[EPT];
 #pragma unroll
-    for (int k = 0; k < EPT; ++k)
-        m[k] = ok[k] ? union_edge<MARK, STATS>(f.parent, f.sbits, u[k], v[k], pu[k], pv[k], &st, f.halve != 0) : kInvalid;
+    for (int k = 0; k < EPT; ++k) {
+        if (claimed[k]) {
+            const uint32_t x = (gflag[k] == 2u) ? u[k] : v[k];
+            set_seen(f.sbits, x);
+            if (STATS) { ++st.inits; ++st.hooks; }
+            m[k] = MARK ? x : kInvalid;
+        } else {
+            m[k] = ok[k] ? union_edge<MARK, STATS>(f.parent, f.sbits, u[k], v[k], pu[k], pv[k], &st, f.halve != 0) : kInvalid;
+        }
+    }
     if (MARK) log_append<EPT>(f.mark, f.mark_len, m);
 }
 
