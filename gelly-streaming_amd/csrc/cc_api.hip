@@ -374,11 +374,7 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
 // reset where gbits outgrows L2 (ids >= 2^kRingMinBits), or at GSGPU_YOUNG_SPLIT
 static uint64_t next_young_split(const gs_cc_t* h, uint64_t done) {
     uint64_t s = dbg().young_split;
-#if defined(GS_EXP_YOUNGRING32)
-    if (s == ~0ull) s = (uint64_t)h->cap >= (1ull << std::min<uint32_t>(dbg().ring_min_bits, 63)) ? h->cap / 32 : 0;
-#else
     if (s == ~0ull) s = (uint64_t)h->cap >= (1ull << std::min<uint32_t>(dbg().ring_min_bits, 63)) ? h->cap / kYoungSplitDiv : 0;
-#endif
     return (s && done < s) ? s : 0;
 }
 
@@ -403,13 +399,9 @@ static void internal_close(gs_cc_t* h) {
 // launch first, then the rest in one launch.
 template <typename IdT, bool AOS>
 void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, size_t esz) {
-#if defined(GS_EXP_YOUNGRING)
-    const uint64_t young_limit = h->cap / kYoungSplitDiv;
-#elif defined(GS_EXP_YOUNGRING32)
-    const uint64_t young_limit = h->cap / 32;
-#else
+    // window 1 of the headline stays in k_fold after its young split: the ring fold there (hot set
+    // empty, the giant root hooked again and again) took 2.06 ms instead of 1.19 (r02_n)
     const uint64_t young_limit = h->cap / 4;
-#endif
     const size_t stride = AOS ? 2 * esz : esz;
     const bool aligned = ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
     uint64_t off = 0;
