@@ -306,6 +306,7 @@ def main():
                              "frac": per_edge * W_rank / (fold_win_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                              "ms_per_window": fold_win_ms, "young_launches": young_n // max(a.steps, 1),
                              "definition": "every UpdateCC launch of a window (young k_fold + steady k_fold_ring)"},
+                "requests": request_roofline(a, W_rank, avg_ms) if kernel == "k_fold_ring" else None,
                 "wall": {"achieved": wall_gbs, "frac": wall_gbs / (world * HBM_PEAK_GBS),
                          "alg_bytes_per_step": alg_step,
                          "definition": "BASELINE.md: sum over windows of (%d E_w + %d |V_seen,w|) / wall time / "
@@ -370,6 +371,43 @@ def traffic_per_launch(a, W_rank):
     except Exception:
         return None
     return None
+
+
+def request_roofline(a, W_rank, avg_ms):
+    """The bound the steady fold actually meets: L2 requests, not bytes. Per k_fold_ring launch,
+    the PMC passes (profiles/fold_traffic.json: TCC requests and hit rate) split into L2 hits, the
+    edge stream and random L2 misses; tools/request_lab.hip measured what this chip sustains for
+    each (profiles/r02_request_lab.json: random 4-B loads over an L2-resident table, over a table
+    in Infinity Cache, a streaming read). Bound = max(hits / hit rate, stream bytes / stream rate +
+    random misses / miss rate): hits and misses are served by different units and overlap."""
+    lab_path = os.path.join(ROOT, "profiles", "r02_request_lab.json")
+    if not (os.path.exists(a.traffic_json) and os.path.exists(lab_path)):
+        return None
+    try:
+        tj, lab = json.load(open(a.traffic_json)), json.load(open(lab_path))
+        if not (tj.get("window_edges") == W_rank and tj.get("scale") == a.scale and tj.get("id_bits", 32) == a.id_bits):
+            return None
+        ring = tj["ring"]
+        req, hit = ring["tcc_requests_per_launch"], ring["l2_hit_rate"]
+        hits, misses = req * hit, req * (1.0 - hit)
+        stream_bytes = W_rank * (8 if a.id_bits == 32 else 16)
+        stream_req = stream_bytes / 64.0
+        hit_gps, miss_gps = lab["rand4B_1MiB_32w_Gps"], lab["rand4B_64MiB_32w_Gps"]
+        stream_tbps = lab["stream_read_TBps"]
+        t_hits = hits / (hit_gps * 1e3)                                   # us
+        t_miss = stream_bytes / (stream_tbps * 1e6) + max(misses - stream_req, 0.0) / (miss_gps * 1e3)
+        bound_us = max(t_hits, t_miss)
+        return {"bound": "l2-requests", "kernel": "k_fold_ring", "l2_hits_per_launch": hits,
+                "l2_misses_per_launch": misses, "stream_requests_per_launch": stream_req,
+                "hit_rate_peak_Gps": hit_gps, "miss_rate_peak_Gps": miss_gps, "stream_peak_TBps": stream_tbps,
+                "hits_us": t_hits, "misses_us": t_miss, "bound_us": bound_us, "avg_launch_us": avg_ms * 1e3,
+                "frac": bound_us / (avg_ms * 1e3),
+                "definition": "max(L2 hits / 1-MiB random-load rate, edge stream / stream rate + other L2 misses / "
+                              "Infinity-Cache random-load rate) per launch (PMC counts: profiles/fold_traffic.json; "
+                              "rates measured by tools/request_lab.hip: profiles/r02_request_lab.json) / the "
+                              "launch's average duration"}
+    except Exception:
+        return None
 
 
 def torch_min_labels(src, dst, V):

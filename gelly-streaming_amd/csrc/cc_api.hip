@@ -76,6 +76,7 @@ struct gs_cc {
     size_t tmp_bytes = 0;
     bool compressed = true;
     bool sbits_stale = false;            // a young launch skipped the seen bits: the next close rebuilds them
+    bool young_count = false;            // the young split just closed: the next young launch counts the warm set
     uint64_t edges_since_reset = 0;      // drives the young-forest launch split (fold_impl)
     uint64_t ring_launches = 0;          // ring fold launches since reset (hot-set admission cadence)
     uint64_t closes = 0;                 // compressions since reset (giant re-sampled every kPickEvery)
@@ -91,6 +92,9 @@ struct gs_cc {
     uint64_t warm_sample = 0;            // edges a warm count launch samples
     uint32_t warm_bcap = 0;              // keys per hash bucket
     int cus = 0;                         // compute units: k_fold_ring grid
+    uint2* rq = nullptr;                 // routed fold: part queues A -> B, then B -> C (2 x parts x rq_cap)
+    uint64_t rq_cap = 0;                 // entries per part queue
+    uint32_t* rcnt = nullptr;            // routed fold: list lengths [2][grid][parts] + the admission flag
     // GS_CC_SPARSE_IDS: id -> slot table; cap (above) = slots = 2^hbits + 1
     bool sparse = false;
     int64_t* keys = nullptr;             // 2^hbits slot keys (INT64_MIN = empty)
@@ -223,8 +227,16 @@ constexpr uint32_t kRingMinBits = 25;
 // at most capacity/8) and re-checked every kWarmEvery-th launch (rebuilt only when invalid for the
 // current giant). Launch 2 (RMAT-26 window 4): windows 2-12 35 us less than launch 3, as launch 0
 // or 1 (profiles/r02_ab_experiments.txt r02_w); 2^24-edge samples gained nothing (r02_u)
+#ifdef GS_EXP_S24
+constexpr uint64_t kWarmAt = 2, kWarmEvery = 16, kWarmSample = 1ull << 24;
+#else
 constexpr uint64_t kWarmAt = 2, kWarmEvery = 16, kWarmSample = 1ull << 23;
-constexpr uint32_t kWarmBucketsMaxBits = 18;        // 2^18 x 4 B = 1 MiB table at RMAT-26 (2 MiB: 2-4 us
+#endif
+#ifdef GS_EXP_W19
+constexpr uint32_t kWarmBucketsMaxBits = 19;
+#else
+constexpr uint32_t kWarmBucketsMaxBits = 18;
+#endif
                                                     // slower per steady window, r02_u)
 constexpr uint32_t kHotThresh = 3;                  // sightings before hot-set admission (233 -> 229 us)
 // Young split: inside the young forest, close internally (compress + giant pick: no emission,
@@ -268,6 +280,20 @@ static void ensure_stats(gs_cc_t* h) {
     }
 }
 
+#ifdef GS_EXP_LAB_DOUBLESEEN
+constexpr size_t kLabSeenExtra = 8u << 20;
+#else
+constexpr size_t kLabSeenExtra = 0;
+#endif
+static WarmBuild warm_build_args(gs_cc_t* h);
+static void launch_warm_build(gs_cc_t* h, hipEvent_t stop);
+
+#ifdef GS_EXP_EARLYWARM
+constexpr bool kEarlyWarm = true;
+#else
+constexpr bool kEarlyWarm = false;
+#endif
+
 template <typename IdT, bool AOS>
 void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool young = false) {
     const int ept = young ? kYoungEpt : kEdgesPerThread;
@@ -288,6 +314,20 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
         f.work = reinterpret_cast<unsigned long long*>(h->derr + kWorkWord);
         (void)hipMemsetAsync(f.work, 0, sizeof(unsigned long long), h->stream);
     }
+#if defined(GS_EXP_YHALVE0)
+    if (young) f.halve = 0;
+#elif defined(GS_EXP_YHALVE8)
+    if (young) f.halve = 8;
+#endif
+    // the young launch right after the young split sees the giant filter first: it counts the warm
+    // set's sample, which is built right after it (window 2 on, not from ring launch kWarmAt on)
+    const bool count = kEarlyWarm && young && h->young_count && h->warm && !AOS && !h->dstats;
+    h->young_count = false;
+    if (count) {
+        f.wkeys = h->wkeys;
+        f.wctl = h->wctl;
+        f.count_edges = h->warm_sample;
+    }
     const bool vec = std::is_same<IdT, uint32_t>::value && !AOS &&
                      ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
     KTimer t(h, h->fold_timer);
@@ -299,6 +339,7 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
     else if (h->mark) { if (vec) GS_LAUNCH_FOLD(true, true, 4, false); else GS_LAUNCH_FOLD(true, false, 4, false); }
     else { if (vec) GS_LAUNCH_FOLD(false, true, 4, false); else GS_LAUNCH_FOLD(false, false, 4, false); }
 #undef GS_LAUNCH_FOLD
+    if (count) launch_warm_build(h, nullptr);
 }
 
 // Steady-state fold (mature forest, aligned device uint32 SoA): k_fold_ring (LDS hot set + warm set
@@ -307,6 +348,14 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
 static bool use_ring(const gs_cc_t* h) {
     const int m = dbg().fold_mode;
     return m == kFoldRing || (m == kFoldAuto && h->hot_bits >= dbg().ring_min_bits);
+}
+
+static void launch_warm_build(gs_cc_t* h, hipEvent_t stop) {
+    const WarmBuild w = warm_build_args(h);
+    klaunch(k_warm_part, dim3((unsigned)((w.keys_cap + kWarmPartTile - 1) / kWarmPartTile)), dim3(1024), h->stream, nullptr,
+            nullptr, w);
+    klaunch(k_warm_count, dim3(w.nbk), dim3(1024), h->stream, nullptr, nullptr, w);
+    klaunch(k_warm_done, dim3(1), dim3(1024), h->stream, nullptr, stop, w, h->derr + 7);
 }
 
 static WarmBuild warm_build_args(gs_cc_t* h) {
@@ -361,13 +410,68 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
         if (st) klaunch(k_fold_ring<IdT, false, true>, grid, dim3(kHotThreads), h->stream, start, stop, a, b, f, hot);
         else klaunch(k_fold_ring<IdT, false, false>, grid, dim3(kHotThreads), h->stream, start, stop, a, b, f, hot);
     }
-    if (build) {
-        const WarmBuild w = warm_build_args(h);
-        klaunch(k_warm_part, dim3((unsigned)((w.keys_cap + kWarmPartTile - 1) / kWarmPartTile)), dim3(1024), h->stream, nullptr,
-                nullptr, w);
-        klaunch(k_warm_count, dim3(w.nbk), dim3(1024), h->stream, nullptr, nullptr, w);
-        klaunch(k_warm_done, dim3(1), dim3(1024), h->stream, nullptr, t.stop(), w, h->derr + 7);
+    if (build) launch_warm_build(h, t.stop());
+}
+
+#ifdef GS_EXP_ROUTE
+constexpr bool kRoute = true;
+#else
+constexpr bool kRoute = false;
+#endif
+
+// Routed steady fold (cc_kernels.hpp k_route_a / k_route_bc): the giant filter from LDS slices of
+// gbits instead of L2 lookups. Queues hold 4x a part's mean share (a tile past that is decided in
+// place from global gbits).
+static bool use_route(const gs_cc_t* h) {
+    return kRoute && h->hot && !h->dstats && h->cap <= 0x80000000u && h->hot_bits <= kSliceBits + 9;
+}
+
+template <typename IdT>
+int launch_fold_route(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
+    const uint32_t parts = 1u << (h->hot_bits > kSliceBits ? h->hot_bits - kSliceBits : 0);
+    const uint32_t grid = (uint32_t)std::min(std::max(h->cus, 1), (int)kMaxRouteGrid);
+    const uint64_t need = 4 * (n / ((uint64_t)grid * parts)) + 512;          // 4x a list's mean share
+    if (!h->rcnt) {
+        GS_HIP(hipMalloc(&h->rcnt, (2 * (size_t)kMaxRouteGrid * kMaxParts + 64) * sizeof(uint32_t)));
     }
+    if (need > h->rq_cap) {
+        if (h->rq) {
+            GS_HIP(hipStreamSynchronize(h->stream));
+            GS_HIP(hipFree(h->rq));
+            h->rq = nullptr;
+        }
+        if (hipMalloc(&h->rq, 2 * (size_t)grid * parts * need * sizeof(uint2)) != hipSuccess) {
+            (void)hipGetLastError();
+            h->rq_cap = 0;
+            return fail(GS_ERR_NOMEM, "routed fold lists (%llu entries) allocation failed",
+                        (unsigned long long)(2 * (uint64_t)grid * parts * need));
+        }
+        h->rq_cap = need;
+    }
+    HotArgs hot{h->hot, h->hot_bits, h->hot_cand};
+    hot.sample_edges = kHotSampleEdges;
+    hot.budget = h->derr + 6;
+    hot.periodic = (h->ring_launches % kHotAdmitEvery == kHotAdmitEvery - 1) ? 1u : 0u;
+    ++h->ring_launches;
+    hot.five = (h->hot_bits <= kHotBucketBits + 12) ? 1u : 0u;
+    hot.thresh = kHotThresh;
+    FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
+    f.mark_len = h->mark_ctr;
+    RouteArgs r{h->rq, h->rq + (size_t)grid * parts * h->rq_cap, h->rcnt,
+                reinterpret_cast<unsigned long long*>(h->rcnt + 2 * (size_t)kMaxRouteGrid * kMaxParts),
+                h->rq_cap, parts, (uint32_t)((h->cap + 31) / 32)};
+    KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_RING : h->fold_timer);
+    const dim3 g(grid), blk(kRouteThreads);
+    if (h->mark) {
+        klaunch(k_route_a<IdT, true, false>, g, blk, h->stream, t.start(), nullptr, a, b, f, hot, r);
+        klaunch(k_route_bc<true, true, false>, g, blk, h->stream, nullptr, nullptr, f, hot, r);
+        klaunch(k_route_bc<false, true, false>, g, blk, h->stream, nullptr, t.stop(), f, hot, r);
+    } else {
+        klaunch(k_route_a<IdT, false, false>, g, blk, h->stream, t.start(), nullptr, a, b, f, hot, r);
+        klaunch(k_route_bc<true, false, false>, g, blk, h->stream, nullptr, nullptr, f, hot, r);
+        klaunch(k_route_bc<false, false, false>, g, blk, h->stream, nullptr, t.stop(), f, hot, r);
+    }
+    return GS_OK;
 }
 
 // Young-forest split points (dense ids, SoA folds): one internal close at capacity/16 edges since
@@ -418,7 +522,10 @@ void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, siz
             launch_fold<IdT, AOS>(h, a + off * stride, b ? b + off * esz : nullptr, m, true);
             h->edges_since_reset += m;
             off += m;
-            if (sp && h->edges_since_reset == sp && off < n) internal_close(h);
+            if (sp && h->edges_since_reset == sp && off < n) {
+                internal_close(h);
+                h->young_count = true;
+            }
             continue;
         }
         if (AOS) {
@@ -431,7 +538,10 @@ void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, siz
         m = std::min(m, kInternalCloseEdges);
         if (h->hot && use_ring(h) && aligned && m >= 4) {
             m &= ~(uint64_t)3;                          // the ring fold takes groups of 4 edges
-            launch_fold_ring<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
+            if (use_route(h))
+                (void)launch_fold_route<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
+            else
+                launch_fold_ring<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
         } else {
             launch_fold<IdT, AOS>(h, a + off * stride, b + off * esz, m, false);
         }
@@ -783,7 +893,7 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
         if (hipMalloc(&h->mark_ctr, 128) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "hook log counter allocation failed")); }
         h->mark = h->mark_buf;
     }
-    if (hipMalloc(&h->gbits, mark_bytes(h->cap)) != hipSuccess || hipMalloc(&h->sbits, mark_bytes(h->cap)) != hipSuccess ||
+    if (hipMalloc(&h->gbits, mark_bytes(h->cap)) != hipSuccess || hipMalloc(&h->sbits, mark_bytes(h->cap) + kLabSeenExtra) != hipSuccess ||
         hipMalloc(&h->derr, kDerrBytes) != hipSuccess || hipMalloc(&h->dscratch, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&h->hscratch, 8 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
@@ -863,6 +973,8 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->hot) (void)hipFree(h->hot);
     if (h->hot_cand) (void)hipFree(h->hot_cand);
     if (h->warm) (void)hipFree(h->warm);
+    if (h->rq) (void)hipFree(h->rq);
+    if (h->rcnt) (void)hipFree(h->rcnt);
     if (h->wkeys) (void)hipFree(h->wkeys);
     if (h->wpart) (void)hipFree(h->wpart);
     if (h->wctl) (void)hipFree(h->wctl);
@@ -911,6 +1023,7 @@ int gs_cc_reset(gs_cc_t* h) {
     h->sbits_stale = false;
     h->minkey_valid = false;
     h->edges_since_reset = 0;
+    h->young_count = false;
     h->closes = 0;
     h->ring_launches = 0;
     return GS_OK;
