@@ -12,6 +12,9 @@
 
 #include "cc_kernels.hpp"
 #include "sparse_ids.hpp"
+#ifdef GS_EXP_ROUTE
+#include "route_fold.hpp"
+#endif
 
 #include <hipcub/hipcub.hpp>
 
@@ -76,7 +79,6 @@ struct gs_cc {
     size_t tmp_bytes = 0;
     bool compressed = true;
     bool sbits_stale = false;            // a young launch skipped the seen bits: the next close rebuilds them
-    bool young_count = false;            // the young split just closed: the next young launch counts the warm set
     uint64_t edges_since_reset = 0;      // drives the young-forest launch split (fold_impl)
     uint64_t ring_launches = 0;          // ring fold launches since reset (hot-set admission cadence)
     uint64_t closes = 0;                 // compressions since reset (giant re-sampled every kPickEvery)
@@ -227,16 +229,8 @@ constexpr uint32_t kRingMinBits = 25;
 // at most capacity/8) and re-checked every kWarmEvery-th launch (rebuilt only when invalid for the
 // current giant). Launch 2 (RMAT-26 window 4): windows 2-12 35 us less than launch 3, as launch 0
 // or 1 (profiles/r02_ab_experiments.txt r02_w); 2^24-edge samples gained nothing (r02_u)
-#ifdef GS_EXP_S24
-constexpr uint64_t kWarmAt = 2, kWarmEvery = 16, kWarmSample = 1ull << 24;
-#else
 constexpr uint64_t kWarmAt = 2, kWarmEvery = 16, kWarmSample = 1ull << 23;
-#endif
-#ifdef GS_EXP_W19
-constexpr uint32_t kWarmBucketsMaxBits = 19;
-#else
 constexpr uint32_t kWarmBucketsMaxBits = 18;
-#endif
                                                     // slower per steady window, r02_u)
 constexpr uint32_t kHotThresh = 3;                  // sightings before hot-set admission (233 -> 229 us)
 // Young split: inside the young forest, close internally (compress + giant pick: no emission,
@@ -280,19 +274,9 @@ static void ensure_stats(gs_cc_t* h) {
     }
 }
 
-#ifdef GS_EXP_LAB_DOUBLESEEN
-constexpr size_t kLabSeenExtra = 8u << 20;
-#else
-constexpr size_t kLabSeenExtra = 0;
-#endif
 static WarmBuild warm_build_args(gs_cc_t* h);
 static void launch_warm_build(gs_cc_t* h, hipEvent_t stop);
 
-#ifdef GS_EXP_EARLYWARM
-constexpr bool kEarlyWarm = true;
-#else
-constexpr bool kEarlyWarm = false;
-#endif
 
 template <typename IdT, bool AOS>
 void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool young = false) {
@@ -314,20 +298,6 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
         f.work = reinterpret_cast<unsigned long long*>(h->derr + kWorkWord);
         (void)hipMemsetAsync(f.work, 0, sizeof(unsigned long long), h->stream);
     }
-#if defined(GS_EXP_YHALVE0)
-    if (young) f.halve = 0;
-#elif defined(GS_EXP_YHALVE8)
-    if (young) f.halve = 8;
-#endif
-    // the young launch right after the young split sees the giant filter first: it counts the warm
-    // set's sample, which is built right after it (window 2 on, not from ring launch kWarmAt on)
-    const bool count = kEarlyWarm && young && h->young_count && h->warm && !AOS && !h->dstats;
-    h->young_count = false;
-    if (count) {
-        f.wkeys = h->wkeys;
-        f.wctl = h->wctl;
-        f.count_edges = h->warm_sample;
-    }
     const bool vec = std::is_same<IdT, uint32_t>::value && !AOS &&
                      ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
     KTimer t(h, h->fold_timer);
@@ -339,7 +309,6 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
     else if (h->mark) { if (vec) GS_LAUNCH_FOLD(true, true, 4, false); else GS_LAUNCH_FOLD(true, false, 4, false); }
     else { if (vec) GS_LAUNCH_FOLD(false, true, 4, false); else GS_LAUNCH_FOLD(false, false, 4, false); }
 #undef GS_LAUNCH_FOLD
-    if (count) launch_warm_build(h, nullptr);
 }
 
 // Steady-state fold (mature forest, aligned device uint32 SoA): k_fold_ring (LDS hot set + warm set
@@ -414,16 +383,11 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
 }
 
 #ifdef GS_EXP_ROUTE
-constexpr bool kRoute = true;
-#else
-constexpr bool kRoute = false;
-#endif
-
 // Routed steady fold (cc_kernels.hpp k_route_a / k_route_bc): the giant filter from LDS slices of
 // gbits instead of L2 lookups. Queues hold 4x a part's mean share (a tile past that is decided in
 // place from global gbits).
 static bool use_route(const gs_cc_t* h) {
-    return kRoute && h->hot && !h->dstats && h->cap <= 0x80000000u && h->hot_bits <= kSliceBits + 9;
+    return h->hot && !h->dstats && h->cap <= 0x80000000u && h->hot_bits <= kSliceBits + 9;
 }
 
 template <typename IdT>
@@ -473,6 +437,7 @@ int launch_fold_route(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     }
     return GS_OK;
 }
+#endif  // GS_EXP_ROUTE
 
 // Young-forest split points (dense ids, SoA folds): one internal close at capacity/16 edges since
 // reset where gbits outgrows L2 (ids >= 2^kRingMinBits), or at GSGPU_YOUNG_SPLIT
@@ -522,10 +487,7 @@ void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, siz
             launch_fold<IdT, AOS>(h, a + off * stride, b ? b + off * esz : nullptr, m, true);
             h->edges_since_reset += m;
             off += m;
-            if (sp && h->edges_since_reset == sp && off < n) {
-                internal_close(h);
-                h->young_count = true;
-            }
+            if (sp && h->edges_since_reset == sp && off < n) internal_close(h);
             continue;
         }
         if (AOS) {
@@ -538,9 +500,11 @@ void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, siz
         m = std::min(m, kInternalCloseEdges);
         if (h->hot && use_ring(h) && aligned && m >= 4) {
             m &= ~(uint64_t)3;                          // the ring fold takes groups of 4 edges
+#ifdef GS_EXP_ROUTE
             if (use_route(h))
                 (void)launch_fold_route<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
             else
+#endif
                 launch_fold_ring<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
         } else {
             launch_fold<IdT, AOS>(h, a + off * stride, b + off * esz, m, false);
@@ -893,7 +857,7 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
         if (hipMalloc(&h->mark_ctr, 128) != hipSuccess) { (void)hipGetLastError(); return bail(fail(GS_ERR_NOMEM, "hook log counter allocation failed")); }
         h->mark = h->mark_buf;
     }
-    if (hipMalloc(&h->gbits, mark_bytes(h->cap)) != hipSuccess || hipMalloc(&h->sbits, mark_bytes(h->cap) + kLabSeenExtra) != hipSuccess ||
+    if (hipMalloc(&h->gbits, mark_bytes(h->cap)) != hipSuccess || hipMalloc(&h->sbits, mark_bytes(h->cap)) != hipSuccess ||
         hipMalloc(&h->derr, kDerrBytes) != hipSuccess || hipMalloc(&h->dscratch, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&h->hscratch, 8 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
@@ -1023,7 +987,6 @@ int gs_cc_reset(gs_cc_t* h) {
     h->sbits_stale = false;
     h->minkey_valid = false;
     h->edges_since_reset = 0;
-    h->young_count = false;
     h->closes = 0;
     h->ring_launches = 0;
     return GS_OK;

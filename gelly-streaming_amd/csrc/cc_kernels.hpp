@@ -34,15 +34,10 @@ namespace gsgpu {
 // walk ever indexes parent[kInvalid].
 // halve = false: a read-only walk (no stores into words other walks share: in a young forest the
 // halving atomics on hub ancestors serialise at the memory-side atomic unit).
-#ifdef GS_EXP_NTPARENT
-__device__ __forceinline__ uint32_t pload(const uint32_t* p) { return __builtin_nontemporal_load(p); }
-#else
-__device__ __forceinline__ uint32_t pload(const uint32_t* p) { return *p; }
-#endif
 __device__ __forceinline__ uint32_t find_root(uint32_t* __restrict__ parent, uint32_t x, uint32_t px, bool halve = true) {
     if (px >= x) return x;
     uint32_t prev = x, cur = px, next;
-    while (cur > (next = pload(&parent[cur]))) {
+    while (cur > (next = parent[cur])) {
         if (halve) __hip_atomic_fetch_min(&parent[prev], next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         prev = cur;
         cur = next;
@@ -62,11 +57,6 @@ __device__ __forceinline__ void set_mark(uint32_t* __restrict__ mark, uint32_t v
 // launch_fold) — one device-scope atomic less per new vertex
 __device__ __forceinline__ void set_seen(uint32_t* __restrict__ sbits, uint32_t v) {
     if (sbits) set_mark(sbits, v);
-#ifdef GS_EXP_LAB_DOUBLESEEN
-    // timing lab (results unchanged): one more atomicOr per seen bit, into a dummy bitmap 8 MiB
-    // past sbits (allocated with the bitmap in this build; ids < 2^26), to price the seen-bit atomics
-    if (sbits) set_mark(sbits + (2u << 20), v & ((1u << 26) - 1));
-#endif
 }
 
 // Read-only root walk (no writes) for find() on const state.
@@ -132,7 +122,7 @@ __device__ __forceinline__ uint32_t union_edge(uint32_t* __restrict__ parent, ui
             if (old == kInvalid) {
                 set_seen(sbits, lo);
             } else if (old != lo) {                 // initialised and hooked meanwhile
-                const uint32_t r = find_root(parent, old, pload(&parent[old]), halve);
+                const uint32_t r = find_root(parent, old, parent[old], halve);
                 if (uhi) rv = r; else ru = r;
                 continue;
             }
@@ -150,7 +140,7 @@ __device__ __forceinline__ uint32_t union_edge(uint32_t* __restrict__ parent, ui
         if (old == kInvalid) { hf = true; continue; }   // defensive: never reached by a walk result
         // hi was hooked meanwhile: continue from its true parent (old < hi, strictly
         // decreasing, so the loop ends)
-        const uint32_t r = find_root(parent, old, pload(&parent[old]), halve);
+        const uint32_t r = find_root(parent, old, parent[old], halve);
         if (uhi) ru = r; else rv = r;
     }
     return kInvalid;
@@ -226,9 +216,6 @@ struct FoldArgs {
     uint32_t halve = 1;          // path halving in root walks (find_root)
     unsigned long long* work = nullptr;   // k_fold: dynamic chunk counter (young forest), or null
     unsigned long long* mark_len = nullptr;   // MARK: the hook log's length word (mark = the log)
-    uint32_t* wkeys = nullptr;            // k_fold warm count: key slots (2 per edge), or null
-    unsigned long long* wctl = nullptr;   // k_fold warm count: edges counted (written by the launch)
-    uint64_t count_edges = 0;             // k_fold warm count: count this launch's first edges
 };
 
 // ---- LDS hot set (steady state) ----
@@ -243,7 +230,7 @@ struct FoldArgs {
 // Exactness (and k_compress clearing the table when the giant becomes another component) is
 // needed for CORRECTNESS, not only speed: a hit stands in for v's gbits bit, a hit on both
 // endpoints drops the edge, and a hit on one endpoint makes the survivor's union start from the
-// giant root instead of parent[v] (union_group_g). The same holds for warm_probe.
+// giant root instead of parent[v] (union_group_g). The same holds for the warm set.
 // Entries are only ever added (a 0 half-word CASed to a remainder) and every entry is a vertex
 // whose gbits bit was set, i.e. a member of the giant component; components only merge until
 // reset, so an entry stays a member while the giant is the same component (k_pick_giant clears
@@ -264,22 +251,9 @@ __device__ __forceinline__ uint32_t hot_hash(uint32_t v, uint32_t B) {
 // 5 x 12 bits packed in the bucket's 64 bits: 80 K entries instead of 64 K (an ideal
 // frequency-ordered set answers 35.3 % instead of 32.4 % of an RMAT-26 window's lookups). The
 // one remainder that does not fit (r + 1 = 4096) can never enter: 1 id in 4096.
-__device__ __forceinline__ bool hot_probe(const uint2* tab, uint32_t v, uint32_t B, bool five) {
-    const uint32_t h = hot_hash(v, B);
-    const uint32_t rb = B - kHotBucketBits;
-    const uint2 w = tab[h >> rb];
-    const uint32_t r = (h & ((1u << rb) - 1)) + 1;
-    if (five) {
-        const uint64_t x = ((uint64_t)w.y << 32) | w.x;
-        return ((x & 0xFFFu) == r) | (((x >> 12) & 0xFFFu) == r) | (((x >> 24) & 0xFFFu) == r) |
-               (((x >> 36) & 0xFFFu) == r) | (((x >> 48) & 0xFFFu) == r);
-    }
-    return ((w.x & 0xFFFFu) == r) | ((w.x >> 16) == r) | ((w.y & 0xFFFFu) == r) | ((w.y >> 16) == r);
-}
-
-// hot_probe in two halves, so a thread's LDS bucket reads all issue before the first compare
-// (one lgkmcnt wait for the group instead of one per endpoint). five is uniform: both formats
-// are compared and selected without a branch.
+// A probe in two halves (bucket index + slot value, then the compare), so a thread's LDS bucket
+// reads all issue before the first compare. five is uniform: both formats are compared and
+// selected without a branch.
 __device__ __forceinline__ uint32_t hot_bucket(uint32_t v, uint32_t B, uint32_t& r) {
     const uint32_t h = hot_hash(v, B);
     const uint32_t rb = B - kHotBucketBits;
@@ -373,17 +347,10 @@ constexpr uint32_t kWarmMul = 0x85EBCA6Bu;
 // wb = log2(buckets); remainders of B - wb <= 8 bits, slot value r = rem + 1 in [1, 256]: the one
 // value that does not fit a byte (256: 1 id in 256 when B - wb = 8) never enters nor matches.
 __device__ __forceinline__ uint32_t warm_hash(uint32_t v, uint32_t B) { return (v * kWarmMul) & ((1u << B) - 1); }
-__device__ __forceinline__ bool warm_probe(const uint32_t* __restrict__ warm, uint32_t v, uint32_t B, uint32_t wb) {
-    const uint32_t h = warm_hash(v, B);
-    const uint32_t rb = B - wb;
-    const uint32_t r = (h & ((1u << rb) - 1)) + 1;
-    const uint32_t x = warm[h >> rb] ^ (r * 0x01010101u);
-    return r <= 0xFFu && ((x - 0x01010101u) & ~x & 0x80808080u) != 0;    // a byte equal to r
-}
-// warm_probe in two halves (word index + slot value, then the compare on the loaded word), so the
-// probes of a thread's LDS misses are all in flight together: written as `hit || warm_probe(..)`
-// the short-circuit put each load in a branch of its own with its wait inside, one L2 round trip
-// after the other (8 per thread and pass of the ring fold)
+// A warm probe in two halves (word index + slot value, then the compare on the loaded word), so
+// the probes of a thread's LDS misses are all in flight together (written as one `hit || probe`
+// expression, the short-circuit put each load in a branch of its own with its wait inside: one L2
+// round trip after the other, 8 per thread and pass of the ring fold)
 __device__ __forceinline__ uint32_t warm_word(uint32_t v, uint32_t B, uint32_t wb, uint32_t& r) {
     const uint32_t h = warm_hash(v, B);
     const uint32_t rb = B - wb;
@@ -432,42 +399,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* p, uin
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)(bytes < kNoLoad ? bytes : kNoLoad), 0x00020000);
 }
 
-#ifdef GS_EXP_GBNT
-constexpr int kGbitsPolicy = 2;                      // nt
-#else
-constexpr int kGbitsPolicy = 0;
-#endif
-
-struct NoPrefetch {
-    __device__ __forceinline__ void operator()() const {}
-};
-
-// pre(): issued right after the gbits loads (the ring fold's next edge loads go out there, so they
-// are younger than every lookup this group waits for: vmcnt counts in issue order)
-template <bool STATS, int EPT, bool HOT, typename Pre = NoPrefetch>
+template <bool STATS, int EPT, bool HOT>
 __device__ __forceinline__ void filter_group(const FoldArgs& f, const uint32_t (&u)[EPT], const uint32_t (&v)[EPT],
                                              bool (&ok)[EPT], const uint2* tab, const HotArgs& hot, bool insert,
-                                             bool warm, uint64_t count_slot, uint32_t (&gflag)[EPT],
-                                             const Pre& pre = Pre{}) {
+                                             bool warm, uint64_t count_slot, uint32_t (&gflag)[EPT]) {
     bool hu[EPT], hv[EPT];       // LDS hot-set hits
     bool mu[EPT], mv[EPT];       // known giant members without a gbits load (LDS or warm hits)
     uint32_t wu[EPT], wv[EPT];
-#ifdef GS_EXP_SERIALPROBE
-#pragma unroll
-    for (int k = 0; k < EPT; ++k) {
-        hu[k] = HOT && hot_probe(tab, u[k], hot.bits, hot.five != 0);
-        hv[k] = HOT && hot_probe(tab, v[k], hot.bits, hot.five != 0);
-        mu[k] = hu[k];
-        mv[k] = hv[k];
-    }
-    if (HOT && warm) {
-#pragma unroll
-        for (int k = 0; k < EPT; ++k) {
-            mu[k] = hu[k] || warm_probe(hot.warm, u[k], hot.bits, hot.warm_bits);
-            mv[k] = hv[k] || warm_probe(hot.warm, v[k], hot.bits, hot.warm_bits);
-        }
-    }
-#else
     if (HOT) {
         // every LDS bucket read of the group, then the compares
         uint2 bu[EPT], bv[EPT];
@@ -511,13 +449,12 @@ __device__ __forceinline__ void filter_group(const FoldArgs& f, const uint32_t (
             mv[k] = hv[k] | warm_match(xv[k], rv[k]);
         }
     }
-#endif
     if (HOT) {                                       // branch-free, as the warm probes
         const __amdgpu_buffer_rsrc_t gr = buffer_rsrc(f.gbits, (((uint64_t)f.rc.cap + 31) >> 5) << 2);
 #pragma unroll
         for (int k = 0; k < EPT; ++k) {
-            const uint32_t xu = __builtin_amdgcn_raw_buffer_load_b32(gr, mu[k] ? kNoLoad : (u[k] >> 5) << 2, 0, kGbitsPolicy);
-            const uint32_t xv = __builtin_amdgcn_raw_buffer_load_b32(gr, mv[k] ? kNoLoad : (v[k] >> 5) << 2, 0, kGbitsPolicy);
+            const uint32_t xu = __builtin_amdgcn_raw_buffer_load_b32(gr, mu[k] ? kNoLoad : (u[k] >> 5) << 2, 0, 0);
+            const uint32_t xv = __builtin_amdgcn_raw_buffer_load_b32(gr, mv[k] ? kNoLoad : (v[k] >> 5) << 2, 0, 0);
             wu[k] = mu[k] ? ~0u : xu;
             wv[k] = mv[k] ? ~0u : xv;
         }
@@ -528,7 +465,6 @@ __device__ __forceinline__ void filter_group(const FoldArgs& f, const uint32_t (
             wv[k] = mv[k] ? ~0u : f.gbits[v[k] >> 5];
         }
     }
-    pre();
 
     if (HOT && STATS) {
         uint32_t nh = 0, nw = 0;
@@ -575,8 +511,8 @@ __device__ __forceinline__ void union_group(const FoldArgs& f, const uint32_t (&
     uint32_t pu[EPT], pv[EPT];
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
-        pu[k] = ok[k] ? pload(&f.parent[u[k]]) : 0u;
-        pv[k] = ok[k] ? pload(&f.parent[v[k]]) : 0u;
+        pu[k] = ok[k] ? f.parent[u[k]] : 0u;
+        pv[k] = ok[k] ? f.parent[v[k]] : 0u;
     }
     uint32_t m[EPT];
 #pragma unroll
@@ -612,8 +548,8 @@ __device__ __forceinline__ void union_group_g(const FoldArgs& f, const uint32_t 
     for (int k = 0; k < EPT; ++k) {
         const bool cu = ok[k] && gflag[k] == 2u && u[k] > gR;      // v in the giant, u outside
         const bool cv = ok[k] && gflag[k] == 1u && v[k] > gR;      // u in the giant, v outside
-        pu[k] = !ok[k] ? 0u : (gflag[k] & 1u) ? gR : cu ? atomicCAS(&f.parent[u[k]], kInvalid, gR) : pload(&f.parent[u[k]]);
-        pv[k] = !ok[k] ? 0u : (gflag[k] & 2u) ? gR : cv ? atomicCAS(&f.parent[v[k]], kInvalid, gR) : pload(&f.parent[v[k]]);
+        pu[k] = !ok[k] ? 0u : (gflag[k] & 1u) ? gR : cu ? atomicCAS(&f.parent[u[k]], kInvalid, gR) : f.parent[u[k]];
+        pv[k] = !ok[k] ? 0u : (gflag[k] & 2u) ? gR : cv ? atomicCAS(&f.parent[v[k]], kInvalid, gR) : f.parent[v[k]];
         claimed[k] = (cu && pu[k] == kInvalid) || (cv && pv[k] == kInvalid);
     }
     uint32_t m[EPT];
@@ -635,7 +571,7 @@ __device__ __forceinline__ void union_group_g(const FoldArgs& f, const uint32_t 
 // ok[k] false = nothing to do for edge k).
 template <bool MARK, bool STATS, int EPT>
 __device__ __forceinline__ void fold_group(const FoldArgs& f, bool filt, uint32_t (&u)[EPT], uint32_t (&v)[EPT],
-                                           bool (&ok)[EPT], FoldStats& st, uint64_t e0) {
+                                           bool (&ok)[EPT], FoldStats& st) {
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
         if (!ok[k]) { u[k] = 0; v[k] = 0; }
@@ -643,24 +579,7 @@ __device__ __forceinline__ void fold_group(const FoldArgs& f, bool filt, uint32_
     uint32_t nvalid = 0, nfilt = 0;
     if (STATS) for (int k = 0; k < EPT; ++k) nvalid += ok[k];
     uint32_t gflag[EPT];
-    bool ok0[EPT];
-#pragma unroll
-    for (int k = 0; k < EPT; ++k) ok0[k] = ok[k];
     if (filt) filter_group<STATS, EPT, false>(f, u, v, ok, nullptr, HotArgs{nullptr, 0, nullptr}, false, false, ~0ull, gflag);
-    // warm count (the young launch after the young split, while it is the giant filter's first):
-    // edge e's endpoints in the giant go to key slots 2e, 2e + 1 (kInvalid otherwise), as the ring
-    // fold's count launch writes them
-    if (f.wkeys && filt && e0 + EPT <= f.count_edges) {
-        uint32_t m[2 * EPT];
-#pragma unroll
-        for (int k = 0; k < EPT; ++k) {
-            m[2 * k] = (ok0[k] && (gflag[k] & 1u)) ? u[k] : kInvalid;
-            m[2 * k + 1] = (ok0[k] && (gflag[k] & 2u)) ? v[k] : kInvalid;
-        }
-#pragma unroll
-        for (int q = 0; q < EPT / 2; ++q)
-            reinterpret_cast<u32x4*>(f.wkeys + 2 * e0)[q] = u32x4{m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]};
-    }
     union_group<MARK, STATS, EPT>(f, u, v, ok, st);
     if (STATS) {
         for (int k = 0; k < EPT; ++k) nfilt += ok[k];
@@ -714,7 +633,7 @@ __device__ __forceinline__ void fold_edges_at(const IdT* __restrict__ a, const I
         }
     }
     if (bad) atomicOr(f.rc.err, 1u);
-    fold_group<MARK, STATS, EPT>(f, filt, u, v, ok, st, e0);
+    fold_group<MARK, STATS, EPT>(f, filt, u, v, ok, st);
 }
 
 // UpdateCC over a batch. Each thread takes EPT consecutive edges per pass: endpoint reads are
@@ -731,8 +650,6 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
     const bool filt = *f.giant != kInvalid;          // wave-uniform
     FoldStats st;
     const uint64_t groups = (n + EPT - 1) / EPT;
-    if (f.wkeys && blockIdx.x == 0 && threadIdx.x == 0)          // edges whose key slots are written
-        *f.wctl = filt ? min(f.count_edges, n) / 256 * 256 : 0;
     if (f.work) {
         __shared__ unsigned long long s_base;
         for (;;) {
@@ -824,12 +741,6 @@ struct Raw4<int64_t> {
     }
 };
 
-#ifdef GS_EXP_PIPE
-constexpr bool kRingPrefetch = true;
-#else
-constexpr bool kRingPrefetch = false;
-#endif
-
 template <typename IdT, bool MARK, bool STATS>
 __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict__ a, const IdT* __restrict__ b,
                                                            FoldArgs f, HotArgs hot) {
@@ -861,26 +772,16 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
     const uint64_t groups = n / 4;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint64_t nvalid = 0, nkept = 0;
-    const uint64_t first = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
-    // kRingPrefetch: the wave's next group, loaded one pass ahead. The index is clamped instead of
-    // branched on (a lane past the end reloads the last group and never uses it), so the loads are
-    // unconditional and the waits in front of them count them exactly.
-    Raw4<IdT> ra, rb;
-    if (kRingPrefetch && groups > 0) {
-        ra.load(a, min(first + lane, groups - 1));
-        rb.load(b, min(first + lane, groups - 1));
-    }
-    for (uint64_t g0 = first; g0 < groups; g0 += stride) {
+    for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < groups; g0 += stride) {
         const uint64_t g = g0 + lane;
         uint32_t u[4] = {0, 0, 0, 0}, v[4] = {0, 0, 0, 0};
         bool ok[4] = {false, false, false, false};
         uint32_t gf[4] = {0u, 0u, 0u, 0u};
         if (g < groups) {
             bool oka[4] = {true, true, true, true}, okb[4] = {true, true, true, true};
-            if (!kRingPrefetch) {
-                ra.load(a, g);
-                rb.load(b, g);
-            }
+            Raw4<IdT> ra, rb;
+            ra.load(a, g);
+            rb.load(b, g);
             ra.unpack(u, oka, f.rc.cap);
             rb.unpack(v, okb, f.rc.cap);
             bool bad = false;
@@ -893,15 +794,8 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
             if (bad) atomicOr(f.rc.err, 1u);
         }
         if (STATS) for (int k = 0; k < 4; ++k) nvalid += ok[k];
-        const auto pre = [&]() {
-            if (kRingPrefetch) {
-                ra.load(a, min(g + stride, groups - 1));
-                rb.load(b, min(g + stride, groups - 1));
-            }
-        };
         if (filt) filter_group<STATS, 4, true>(f, u, v, ok, tab, hot, g * 4 < sample_edges, warm_ok,
-                                               g0 * 4 < count_edges ? g0 / 64 : ~0ull, gf, pre);
-        else pre();
+                                               g0 * 4 < count_edges ? g0 / 64 : ~0ull, gf);
         if (gR == kInvalid) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) gf[k] = 0u;
@@ -938,316 +832,6 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
         atomicAdd(&f.stats[2], (unsigned long long)st.early);
         atomicAdd(&f.stats[3], (unsigned long long)st.hooks);
         atomicAdd(&f.stats[4], (unsigned long long)st.casfail);
-        atomicAdd(&f.stats[5], (unsigned long long)st.inits);
-    }
-}
-
-// ---- routed steady fold: the giant filter out of LDS slices of gbits ----
-// The ring fold's filter is bound by L2 requests: ~10 M gbits lookups per RMAT-26 window miss an
-// XCD's 4 MiB L2 half the time (8 MiB bitmap) and random misses run at ~59 G/s chip-wide
-// (tools/request_lab.hip), the warm set's L2 hits at ~260 G/s. Here no filter lookup leaves the CU:
-//   A (k_route_a): streams the edges, drops those whose endpoints both hit the LDS hot set, and
-//      appends the rest to per-part lists by their first endpoint the hot set did not answer
-//      (part = id >> 20: 2^20 vertices, 128 KiB of gbits);
-//   B (k_route_bc<true>): a workgroup loads its part's gbits slice into LDS and decides each listed
-//      edge from it: the looked-up endpoint outside the giant -> survivor; inside and the other
-//      endpoint known -> dropped; inside and the other unknown -> listed for the other's part;
-//   C (k_route_bc<false>): as B for those (the second endpoint).
-// Survivors go through the wave-private LDS rings and union_group_g as in k_fold_ring.
-// Lists: every workgroup of a launch owns one region of cap entries per part (append cursor in
-// LDS: no global atomic, no barrier), written (u | hu << 31, v | hv << 31) with bit 31 = that
-// endpoint is a known giant member (ids < 2^31 on this path); its counts go to cnt[] at the end.
-// An entry past its region's capacity is decided in place from global gbits (a skewed stream
-// degrades to the ring fold's filter).
-constexpr uint32_t kSliceBits = 20;                  // vertices per part: 2^20 bits = 128 KiB of LDS
-constexpr uint32_t kSliceWords = 1u << (kSliceBits - 5);
-constexpr uint32_t kMaxParts = 512;                  // ids < 2^29
-constexpr uint32_t kMaxRouteGrid = 1024;
-constexpr int kRouteThreads = 1024;
-constexpr int kBcN = 2;                              // entries per lane and work item in B / C (VGPR budget)
-constexpr uint32_t kRouteChunk = 64 * kBcN;          // entries per wave work item in B / C
-
-struct RouteArgs {
-    uint2* qa;                     // A's lists: [grid][parts][cap]
-    uint2* qb;                     // B's lists: [grid][parts][cap]
-    uint32_t* cnt;                 // [2][grid][parts] list lengths (A's, then B's)
-    unsigned long long* flags;     // [0]: this launch admits into the hot set (written by A)
-    uint64_t cap;                  // entries per list
-    uint32_t parts;                // 2^(B - kSliceBits), at least 1
-    uint32_t gwords;               // gbits words (capacity / 32, rounded up)
-};
-
-__device__ __forceinline__ bool gbit(const uint32_t* __restrict__ gbits, uint32_t v) {
-    return (gbits[v >> 5] >> (v & 31)) & 1u;
-}
-
-// 16-B copy of `words` 32-bit words global -> LDS by the whole workgroup, 8 loads in flight per
-// thread before any store (a load-store loop waits one round trip per step); zero past `avail`
-template <uint32_t WORDS>
-__device__ __forceinline__ void lds_fill(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, uint64_t avail) {
-    constexpr uint32_t kVecs = WORDS / 4;
-    const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
-    u32x4* d4 = reinterpret_cast<u32x4*>(dst);
-    for (uint32_t v0 = 0; v0 < kVecs; v0 += 8 * kRouteThreads) {
-        u32x4 q[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t vi = v0 + j * kRouteThreads + threadIdx.x;
-            q[j] = (vi < kVecs && 4ull * vi + 4 <= avail) ? s4[vi] : u32x4{0u, 0u, 0u, 0u};
-            if (vi < kVecs && 4ull * vi < avail && 4ull * vi + 4 > avail) {       // a partial last vector
-                const uint32_t* w = src + 4ull * vi;
-                q[j] = u32x4{w[0], 4ull * vi + 1 < avail ? w[1] : 0u, 4ull * vi + 2 < avail ? w[2] : 0u, 0u};
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t vi = v0 + j * kRouteThreads + threadIdx.x;
-            if (vi < kVecs) d4[vi] = q[j];
-        }
-    }
-}
-
-// Survivors into the wave's ring (one call per wave step, uniform), as k_fold_ring does
-template <bool MARK, bool STATS, int N>
-__device__ __forceinline__ void ring_push(const FoldArgs& f, uint2* ring, uint32_t& cnt, const uint32_t (&u)[N],
-                                          const uint32_t (&v)[N], const bool (&ok)[N], const uint32_t (&gf)[N],
-                                          uint32_t gR, FoldStats& st) {
-    const int lane = threadIdx.x & 63;
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < N; ++k) c += ok[k];
-    uint32_t incl = c;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
-    }
-    const uint32_t wtot = __shfl(incl, 63, 64);
-    if (wtot == 0) return;                           // uniform
-    if (wtot > kRingCap / 2) {                       // young window: union in place
-        union_group_g<MARK, STATS, N>(f, u, v, ok, gf, gR, st);
-        return;
-    }
-    if (cnt + wtot > kRingCap) ring_flush<MARK, STATS>(f, ring, cnt, kRingCap - wtot, st, gR);
-    uint32_t pos = cnt + incl - c;
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-        if (!ok[k]) continue;
-        ring[pos] = make_uint2(u[k] | ((gf[k] & 1u) << 31), v[k] | ((gf[k] >> 1) << 31));
-        ++pos;
-    }
-    cnt += wtot;
-    if (cnt >= 64) ring_flush<MARK, STATS>(f, ring, cnt, cnt - 64, st, gR);
-}
-
-// A: stream + LDS hot set + append to the part lists. One 1024-thread workgroup per CU; waves run
-// free (no barrier until the end).
-template <typename IdT, bool MARK, bool STATS>
-__global__ __launch_bounds__(kRouteThreads) void k_route_a(const IdT* __restrict__ a, const IdT* __restrict__ b,
-                                                           FoldArgs f, HotArgs hot, RouteArgs r) {
-    __shared__ uint2 tab[kHotBuckets];
-    __shared__ uint32_t lcur[kMaxParts];
-    __shared__ uint2 rings[kRouteThreads / 64][kRingCap];          // survivors of overfull lists (rare)
-    const uint64_t n = f.n;
-    const bool filt = *f.giant != kInvalid;          // uniform (the host routes only past the young forest)
-    if (filt) lds_fill<2 * kHotBuckets>(reinterpret_cast<uint32_t*>(tab), reinterpret_cast<const uint32_t*>(hot.table), 2 * kHotBuckets);
-    else for (uint32_t i = threadIdx.x; i < kHotBuckets; i += blockDim.x) tab[i] = make_uint2(0u, 0u);
-    for (uint32_t p = threadIdx.x; p < r.parts; p += blockDim.x) lcur[p] = 0u;
-    const uint32_t gR = f.giant[1];
-    const uint32_t budget = hot.budget ? *hot.budget : 1u;
-    __syncthreads();
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (hot.budget && budget) *hot.budget = budget - 1;
-        r.flags[0] = (hot.periodic || budget) ? 1ull : 0ull;            // B and C admit this launch
-    }
-    const int lane = threadIdx.x & 63;
-    uint2* const ring = rings[threadIdx.x >> 6];
-    uint2* const mine = r.qa + (uint64_t)blockIdx.x * r.parts * r.cap;
-    uint32_t cnt = 0;
-    FoldStats st;
-    const uint64_t groups = n / 4;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < groups; g0 += stride) {
-        const uint64_t g = g0 + lane;
-        uint32_t u[4] = {0, 0, 0, 0}, v[4] = {0, 0, 0, 0};
-        bool ok[4] = {false, false, false, false};
-        if (g < groups) {
-            bool oka[4] = {true, true, true, true}, okb[4] = {true, true, true, true};
-            Raw4<IdT> ra, rb;
-            ra.load(a, g);
-            rb.load(b, g);
-            ra.unpack(u, oka, f.rc.cap);
-            rb.unpack(v, okb, f.rc.cap);
-            bool bad = false;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                ok[k] = oka[k] && okb[k];
-                bad |= !ok[k];
-                if (!ok[k]) { u[k] = 0; v[k] = 0; }
-            }
-            if (bad) atomicOr(f.rc.err, 1u);
-        }
-        uint2 bu[4], bv[4];
-        uint32_t ru[4], rv[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            bu[k] = tab[hot_bucket(u[k], hot.bits, ru[k])];
-            bv[k] = tab[hot_bucket(v[k], hot.bits, rv[k])];
-        }
-        bool spill[4], hu[4], hv[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            hu[k] = hot_match(bu[k], ru[k], hot.five != 0);
-            hv[k] = hot_match(bv[k], rv[k], hot.five != 0);
-            spill[k] = false;
-            if (!ok[k] || (hu[k] && hv[k])) continue;                   // dropped: both in the giant
-            const uint32_t part = (hu[k] ? v[k] : u[k]) >> kSliceBits;
-            const uint32_t pos = atomicAdd(&lcur[part], 1u);
-            if (pos < r.cap) mine[(uint64_t)part * r.cap + pos] = make_uint2(u[k] | ((uint32_t)hu[k] << 31), v[k] | ((uint32_t)hv[k] << 31));
-            else spill[k] = true;
-        }
-        uint32_t gf[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {                                  // overfull list: decide in place
-            const bool gu = spill[k] && (hu[k] || gbit(f.gbits, u[k]));
-            const bool gv = spill[k] && (hv[k] || gbit(f.gbits, v[k]));
-            gf[k] = gR == kInvalid ? 0u : ((uint32_t)gu | ((uint32_t)gv << 1));
-            spill[k] = spill[k] && !(gu && gv);
-        }
-        ring_push<MARK, STATS, 4>(f, ring, cnt, u, v, spill, gf, gR, st);
-    }
-    ring_flush<MARK, STATS>(f, ring, cnt, 0, st, gR);
-    __syncthreads();
-    for (uint32_t p = threadIdx.x; p < r.parts; p += blockDim.x)
-        r.cnt[(uint64_t)blockIdx.x * r.parts + p] = (uint32_t)min((uint64_t)lcur[p], r.cap);
-    if (STATS) {
-        atomicAdd(&f.stats[3], (unsigned long long)st.hooks);
-        atomicAdd(&f.stats[5], (unsigned long long)st.inits);
-    }
-}
-
-// B / C: the part's gbits slice in LDS. gridDim / parts workgroups share a part (with more parts
-// than workgroups, a workgroup takes parts in rounds); a workgroup reads the part's lists of every
-// other wpp-th producer workgroup, cut into work items of kRouteChunk entries that its waves take
-// in turn. FWD (B) looks up an entry's first unknown endpoint: outside the giant -> survivor;
-// inside with the other endpoint known -> dropped; inside with the other unknown -> listed for the
-// other's part. !FWD (C) looks up the listed entry's v (u confirmed in B).
-template <bool FWD, bool MARK, bool STATS>
-__global__ __launch_bounds__(kRouteThreads) void k_route_bc(FoldArgs f, HotArgs hot, RouteArgs r) {
-    __shared__ uint32_t slice[kSliceWords];
-    __shared__ uint32_t lcur[kMaxParts];
-    __shared__ uint32_t ipre[kMaxRouteGrid + 1];     // work items before list j
-    __shared__ uint2 rings[kRouteThreads / 64][kRingCap];
-    const uint32_t gR = f.giant[1];
-    const uint2* const q = FWD ? r.qa : r.qb;
-    const uint32_t* const qn = FWD ? r.cnt : r.cnt + (uint64_t)gridDim.x * r.parts;
-    const bool admit = hot.table && r.flags[0] != 0;
-    // admission: the first entries of every list, about 2 x sample_edges endpoint offers in all
-    const uint64_t sample = 2 * hot.sample_edges / ((uint64_t)gridDim.x * r.parts);
-    if (FWD)
-        for (uint32_t p = threadIdx.x; p < r.parts; p += blockDim.x) lcur[p] = 0u;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint2* const ring = rings[wave];
-    uint2* const mine = r.qb + (uint64_t)blockIdx.x * r.parts * r.cap;
-    uint32_t cnt = 0;
-    FoldStats st;
-    const uint32_t wpp = max(1u, gridDim.x / r.parts);             // workgroups per part
-    const uint32_t pstride = gridDim.x / wpp;
-    const uint32_t sub = blockIdx.x % wpp;
-    const uint32_t nlist = (gridDim.x - sub + wpp - 1) / wpp;       // producer lists this workgroup reads
-    const uint32_t rounds = (r.parts + pstride - 1) / pstride;
-    for (uint32_t rd = 0; rd < rounds; ++rd) {
-        const uint32_t p = blockIdx.x / wpp + rd * pstride;
-        const bool live = p < r.parts && blockIdx.x / wpp < pstride;      // uniform
-        __syncthreads();                             // the previous round's readers are done
-        if (live) {
-            lds_fill<kSliceWords>(slice, f.gbits + (uint64_t)p * kSliceWords,
-                                  r.gwords > p * kSliceWords ? r.gwords - (uint64_t)p * kSliceWords : 0);
-            // work items per list, then an exclusive scan by wave 0
-            for (uint32_t j = threadIdx.x; j < nlist; j += blockDim.x)
-                ipre[j + 1] = (qn[(uint64_t)(sub + j * wpp) * r.parts + p] + kRouteChunk - 1) / kRouteChunk;
-        } else {
-            for (uint32_t j = threadIdx.x; j < nlist; j += blockDim.x) ipre[j + 1] = 0u;
-        }
-        __syncthreads();
-        if (wave == 0) {
-            uint32_t carry = 0;
-            for (uint32_t j0 = 0; j0 < nlist; j0 += 64) {
-                uint32_t x = (j0 + lane < nlist) ? ipre[j0 + lane + 1] : 0u;
-#pragma unroll
-                for (int off = 1; off < 64; off <<= 1) {
-                    const uint32_t y = __shfl_up(x, off, 64);
-                    if (lane >= off) x += y;
-                }
-                if (j0 + lane < nlist) ipre[j0 + lane + 1] = x + carry;
-                carry += __shfl(x, 63, 64);
-            }
-            if (lane == 0) ipre[0] = 0u;
-        }
-        __syncthreads();
-        const uint32_t items = ipre[nlist];
-        const uint32_t base_v = p << kSliceBits;
-        for (uint32_t it = wave; it < items; it += kRouteThreads / 64) {
-            uint32_t lo = 0, hi = nlist;             // list j: ipre[j] <= it < ipre[j + 1]
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (ipre[mid] <= it) lo = mid; else hi = mid;
-            }
-            const uint32_t prod = sub + lo * wpp;
-            const uint32_t len = qn[(uint64_t)prod * r.parts + p];
-            const uint32_t e0 = (it - ipre[lo]) * kRouteChunk;
-            const uint2* const lp = q + ((uint64_t)prod * r.parts + p) * r.cap;
-            uint32_t u[kBcN], v[kBcN], gf[kBcN];
-            bool ok[kBcN];
-            uint2 ent[kBcN];
-            bool inr[kBcN];
-#pragma unroll
-            for (int k = 0; k < kBcN; ++k) {
-                const uint32_t i = e0 + k * 64 + lane;
-                inr[k] = i < len;                    // (e0 + 256 bounds the item)
-                ent[k] = inr[k] ? lp[i] : make_uint2(0u, 0u);
-            }
-            bool spill[kBcN];
-#pragma unroll
-            for (int k = 0; k < kBcN; ++k) {
-                const bool in = inr[k];
-                const bool hu = in && (ent[k].x >> 31), hv = in && (ent[k].y >> 31);
-                u[k] = in ? ent[k].x & 0x7FFFFFFFu : 0u;
-                v[k] = in ? ent[k].y & 0x7FFFFFFFu : 0u;
-                const uint32_t x = (FWD && !hu) ? u[k] : v[k];         // the endpoint this part answers
-                const uint32_t lx = x - base_v;
-                const bool gx = in && ((slice[(lx >> 5) & (kSliceWords - 1)] >> (lx & 31)) & 1u);
-                if (admit && gx && e0 + k * 64 + lane < sample) hot_admit(hot, x);
-                ok[k] = in && !gx;                                   // survivor: x outside the giant
-                gf[k] = gR == kInvalid ? 0u : FWD ? ((uint32_t)hu | ((uint32_t)hv << 1)) : 1u;
-                spill[k] = false;
-                if (FWD && gx && !hu && !hv) {                       // u inside, v unknown: v's part
-                    const uint32_t part = v[k] >> kSliceBits;
-                    const uint32_t pos = atomicAdd(&lcur[part], 1u);
-                    if (pos < r.cap) mine[(uint64_t)part * r.cap + pos] = make_uint2(u[k] | (1u << 31), v[k]);
-                    else spill[k] = true;
-                }
-            }
-            if (FWD) {
-#pragma unroll
-                for (int k = 0; k < kBcN; ++k) {     // overfull list: v from global gbits
-                    if (spill[k]) {
-                        ok[k] = !gbit(f.gbits, v[k]);
-                        gf[k] = gR == kInvalid ? 0u : 1u;
-                    }
-                }
-            }
-            ring_push<MARK, STATS, kBcN>(f, ring, cnt, u, v, ok, gf, gR, st);
-        }
-    }
-    ring_flush<MARK, STATS>(f, ring, cnt, 0, st, gR);
-    if (FWD) {
-        __syncthreads();
-        for (uint32_t p = threadIdx.x; p < r.parts; p += blockDim.x)
-            r.cnt[(uint64_t)gridDim.x * r.parts + (uint64_t)blockIdx.x * r.parts + p] = (uint32_t)min((uint64_t)lcur[p], r.cap);
-    }
-    if (STATS) {
-        atomicAdd(&f.stats[3], (unsigned long long)st.hooks);
         atomicAdd(&f.stats[5], (unsigned long long)st.inits);
     }
 }
@@ -1360,7 +944,7 @@ __global__ __launch_bounds__(1024) void k_warm_count(WarmBuild w) {
     }
     __syncthreads();
     // warm word t of this bucket: its 2^rb hash values are local [t << rb, (t + 1) << rb); slot
-    // value r = low rb bits + 1 (r = 256 does not fit a byte and never enters; warm_probe never
+    // value r = low rb bits + 1 (r = 256 does not fit a byte and never enters; warm_match never
     // matches it). Four lanes per word each keep the top 4 of a quarter as packed (count << 16 | r)
     // keys, sorted; two bitonic merges over lanes ^1 and ^2 leave the word's top 4 (one lane per
     // word scanning all 2^rb counters: 167 us per build).
@@ -1555,22 +1139,12 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                                                   uint32_t* __restrict__ gbits, uint32_t* __restrict__ sbits,
                                                   const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                   uint32_t* __restrict__ owner, uint2* __restrict__ hot, int rebuild_seen) {
-    __shared__ uint32_t s_g, s_inc, s_clear, s_relabel;
+    __shared__ uint32_t s_g, s_inc, s_clear;
     if (threadIdx.x == 0) {
         const uint32_t g0 = in[0];
         const uint32_t g = (g0 == kInvalid) ? kInvalid : find_root_ro(parent, g0);
         s_g = g;
         s_inc = (g != kInvalid && g == in[1] && !rebuild_seen) ? 1u : 0u;
-        s_relabel = 0u;
-#ifdef GS_EXP_RELABEL
-        // the giant's root moved (its old root, the one gbits were built for, was hooked below a
-        // smaller root of the same component): every gbits member is relabelled to g by its
-        // word's owner, the rest as in the incremental close
-        if (!s_inc && g != kInvalid && in[1] != kInvalid && !rebuild_seen && find_root_ro(parent, in[1]) == g) {
-            s_inc = 1u;
-            s_relabel = 1u;
-        }
-#endif
         s_clear = 0;
         if (blockIdx.x == 0) {
             if (g != kInvalid) {
@@ -1594,14 +1168,9 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
     const int lane = threadIdx.x & 63;
     if (s_inc) {                                     // one bitmap word (32 vertices) per thread
         const uint32_t nwords = (uint32_t)((n + 31) >> 5);
-        const bool relabel = s_relabel != 0;
         for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += gridDim.x * blockDim.x) {
-            const uint32_t gw = gbits[w];
-            uint32_t cand = sbits[w] & ~gw;
+            uint32_t cand = sbits[w] & ~gbits[w];
             uint32_t add = 0;
-            if (relabel) {
-                for (uint32_t m = gw; m; m &= m - 1) parent[(w << 5) + (uint32_t)(__ffs(m) - 1)] = g;
-            }
             // up to 8 stragglers at a time, their parent and grandparent reads issued back to
             // back (one at a time: a young Erdos-Renyi window's close, ~32 stragglers per word,
             // spent 121 us per 2^24 ids in dependent loads)
