@@ -3,6 +3,9 @@ configuration (the library reads its debug variables once per process; csrc/cc_a
 
 * test_headline_config_production: RMAT-26 EF16, 2^24-edge windows, production defaults — windows
   1..6 bit-exact vs the C oracle, final labels vs an independent torch CC (tests/headline_check.py).
+* test_headline_config_eight_ranks_one_gpu: the same stream as BASELINE config 3's 8-GPU strong
+  layout (2^24-edge global windows, 2^21 edges per rank), 8 ranks through the C-ABI exchange on
+  one GPU (tests/headline_ranks_check.py).
 * test_variant_parity: every golden stream, RMAT-21, ER-21 and the giant-switch stream, per window
   vs the C oracle, under production defaults and under each forced variant (tests/variant_check.py).
 * test_fold_variants_verified: bench.py --verify (RMAT-22, 2^20-edge windows) under each variant.
@@ -37,6 +40,17 @@ def test_headline_config_production():
     assert r["oracle_checksums_equal"], r
     assert r["final_equals_torch_cc"] and r["labels_minimal_idempotent"], r
     assert r["ok"], r
+
+
+def test_headline_config_eight_ranks_one_gpu():
+    """BASELINE config 3's 8-rank strong layout at full scale through the C-ABI exchange
+    (in-process transport): per-window checksums vs the oracle, replicas equal, final vs torch CC."""
+    out = subprocess.check_output([sys.executable, os.path.join(HERE, "headline_ranks_check.py")], env=_env({}),
+                                  timeout=900)
+    r = _last_json(out)
+    print(r)
+    assert not r["hung"] and not r["errors"], r
+    assert r["oracle_checksums_equal"] and r["replicas_equal"] and r["final_equals_torch_cc"], r
 
 
 VARIANTS = {
