@@ -709,6 +709,38 @@ __device__ __forceinline__ void ring_flush(const FoldArgs& f, uint2* ring, uint3
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
+// 16-B copy of WORDS 32-bit words global -> LDS by a 1024-thread workgroup, 8 loads in flight per
+// thread before any store: the element loop it replaces (load, wait, store) waited one round trip
+// per step, 16 of them to fill the hot set at every ring launch
+constexpr uint32_t kFillThreads = 1024;
+// 16-B copy of `words` 32-bit words global -> LDS by the whole workgroup, 8 loads in flight per
+// thread before any store (a load-store loop waits one round trip per step); zero past `avail`
+template <uint32_t WORDS>
+__device__ __forceinline__ void lds_fill(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, uint64_t avail) {
+    constexpr uint32_t kVecs = WORDS / 4;
+    const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
+    u32x4* d4 = reinterpret_cast<u32x4*>(dst);
+    for (uint32_t v0 = 0; v0 < kVecs; v0 += 8 * kFillThreads) {
+        u32x4 q[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t vi = v0 + j * kFillThreads + threadIdx.x;
+            q[j] = (vi < kVecs && 4ull * vi + 4 <= avail) ? s4[vi] : u32x4{0u, 0u, 0u, 0u};
+            if (vi < kVecs && 4ull * vi < avail && 4ull * vi + 4 > avail) {       // a partial last vector
+                const uint32_t* w = src + 4ull * vi;
+                q[j] = u32x4{w[0], 4ull * vi + 1 < avail ? w[1] : 0u, 4ull * vi + 2 < avail ? w[2] : 0u, 0u};
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t vi = v0 + j * kFillThreads + threadIdx.x;
+            if (vi < kVecs) d4[vi] = q[j];
+        }
+    }
+}
+
+
+
 // 4 consecutive ids of an aligned SoA stream, loaded raw (load) and range-checked as uint32 where
 // they are used (unpack): int64 ids take two 16-B loads; a negative or >= cap id fails the range
 // check either way. Split so the ring fold can issue a group's loads one pass ahead.
@@ -744,13 +776,11 @@ struct Raw4<int64_t> {
 template <typename IdT, bool MARK, bool STATS>
 __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict__ a, const IdT* __restrict__ b,
                                                            FoldArgs f, HotArgs hot) {
-    __shared__ uint2 tab[kHotBuckets];
+    __shared__ __attribute__((aligned(16))) uint2 tab[kHotBuckets];
     __shared__ uint2 rings[kHotThreads / 64][kRingCap];
     const uint64_t n = f.n;
     const bool filt = *f.giant != kInvalid;          // uniform
-    if (filt) {
-        for (uint32_t i = threadIdx.x; i < kHotBuckets; i += blockDim.x) tab[i] = hot.table[i];
-    }
+    if (filt) lds_fill<2 * kHotBuckets>(reinterpret_cast<uint32_t*>(tab), reinterpret_cast<const uint32_t*>(hot.table), 2 * kHotBuckets);
     // the root gbits were built for (= the giant's label at the last close); survivors' giant
     // flags use it in place of a parent[] read (union_group_g). Off (kInvalid) without a filter
     // or for ids >= 2^31 (the ring's flag bit)

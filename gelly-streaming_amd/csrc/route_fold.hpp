@@ -48,32 +48,6 @@ __device__ __forceinline__ bool gbit(const uint32_t* __restrict__ gbits, uint32_
     return (gbits[v >> 5] >> (v & 31)) & 1u;
 }
 
-// 16-B copy of `words` 32-bit words global -> LDS by the whole workgroup, 8 loads in flight per
-// thread before any store (a load-store loop waits one round trip per step); zero past `avail`
-template <uint32_t WORDS>
-__device__ __forceinline__ void lds_fill(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, uint64_t avail) {
-    constexpr uint32_t kVecs = WORDS / 4;
-    const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
-    u32x4* d4 = reinterpret_cast<u32x4*>(dst);
-    for (uint32_t v0 = 0; v0 < kVecs; v0 += 8 * kRouteThreads) {
-        u32x4 q[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t vi = v0 + j * kRouteThreads + threadIdx.x;
-            q[j] = (vi < kVecs && 4ull * vi + 4 <= avail) ? s4[vi] : u32x4{0u, 0u, 0u, 0u};
-            if (vi < kVecs && 4ull * vi < avail && 4ull * vi + 4 > avail) {       // a partial last vector
-                const uint32_t* w = src + 4ull * vi;
-                q[j] = u32x4{w[0], 4ull * vi + 1 < avail ? w[1] : 0u, 4ull * vi + 2 < avail ? w[2] : 0u, 0u};
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t vi = v0 + j * kRouteThreads + threadIdx.x;
-            if (vi < kVecs) d4[vi] = q[j];
-        }
-    }
-}
-
 // Survivors into the wave's ring (one call per wave step, uniform), as k_fold_ring does
 template <bool MARK, bool STATS, int N>
 __device__ __forceinline__ void ring_push(const FoldArgs& f, uint2* ring, uint32_t& cnt, const uint32_t (&u)[N],
@@ -112,7 +86,7 @@ __device__ __forceinline__ void ring_push(const FoldArgs& f, uint2* ring, uint32
 template <typename IdT, bool MARK, bool STATS>
 __global__ __launch_bounds__(kRouteThreads) void k_route_a(const IdT* __restrict__ a, const IdT* __restrict__ b,
                                                            FoldArgs f, HotArgs hot, RouteArgs r) {
-    __shared__ uint2 tab[kHotBuckets];
+    __shared__ __attribute__((aligned(16))) uint2 tab[kHotBuckets];
     __shared__ uint32_t lcur[kMaxParts];
     __shared__ uint2 rings[kRouteThreads / 64][kRingCap];          // survivors of overfull lists (rare)
     const uint64_t n = f.n;
@@ -214,7 +188,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route_a(const IdT* __restrict
 // other's part. !FWD (C) looks up the listed entry's v (u confirmed in B).
 template <bool FWD, bool MARK, bool STATS>
 __global__ __launch_bounds__(kRouteThreads) void k_route_bc(FoldArgs f, HotArgs hot, RouteArgs r) {
-    __shared__ uint32_t slice[kSliceWords];
+    __shared__ __attribute__((aligned(16))) uint32_t slice[kSliceWords];
     __shared__ uint32_t lcur[kMaxParts];
     __shared__ uint32_t ipre[kMaxRouteGrid + 1];     // work items before list j
     __shared__ uint32_t llen[kMaxRouteGrid];         // list j's length
