@@ -365,7 +365,7 @@ __device__ __forceinline__ bool warm_match(uint32_t w, uint32_t r) {
 // candidate table's atomics); the hubs are stable, so a launch admits only while *budget > 0
 // (kHotAdmitLaunches after reset or after k_compress clears the set for a new giant) or when the
 // host's periodic refresh (every kHotAdmitEvery ring launches) asks: steady window 266 -> 240 us.
-constexpr uint32_t kHotAdmitLaunches = 8;
+constexpr uint32_t kHotAdmitLaunches = 4;           // 8 -> 4: windows 2-12 -110 us, steady = (r02_ax/ay)
 // every 64th (was 16th): 0.4-0.8 % faster per step on RMAT-26 (round-1 sweep: 16 / 32 / 64 /
 // never = 18.77 / 18.68 / 18.65 / 18.61 ms); a refresh is kept for streams whose hubs drift
 constexpr uint32_t kHotAdmitEvery = 64;
