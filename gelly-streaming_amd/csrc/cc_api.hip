@@ -628,15 +628,18 @@ void report_fold_stats(gs_cc_t* h) {
     (void)hipMemsetAsync(h->dstats, 0, sizeof(c), h->stream);
 }
 
+constexpr uint64_t kEarlyPicks = 4;
+
 int compress_impl(gs_cc_t* h) {
     report_fold_stats(h);
     if (h->compressed) return GS_OK;
     {
         KTimer t(h, GS_K_COMPRESS);
         // re-sample the giant every kPickEvery closes (and, while there may be none yet, before
-        // each of the first 2 * kPickEvery closes); otherwise k_compress follows it itself
+        // each of the first kEarlyPicks closes); otherwise k_compress follows it itself. (Early
+        // picks before the first 16 closes cost 66 us per RMAT-26 step in no-op launches: r02_az.)
         const bool force = h->closes % kPickEvery == 0;
-        const bool pick = force || h->closes < 2 * kPickEvery;
+        const bool pick = force || h->closes < kEarlyPicks;
         uint32_t* in = giant_state(h);
         if (pick)
             klaunch(k_pick_giant, dim3(1), dim3(1024), h->stream, t.start(), nullptr, (const uint32_t*)h->parent, h->cap,
