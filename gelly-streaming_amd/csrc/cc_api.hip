@@ -68,6 +68,7 @@ struct gs_cc {
     unsigned long long* mark_ctr = nullptr;   // [log length, export cursor], a 128-B line of its own
     uint32_t* gbits = nullptr;           // giant-component filter bitmap (1 bit per vertex)
     uint32_t* sbits = nullptr;           // seen bitmap (1 bit per vertex), set on first touch
+    uint32_t* cbits = nullptr;           // ring folds: first touches claimed under the giant root
     uint32_t* derr = nullptr;            // derr[0] deferred device error flags; derr[1..5] giant state
     unsigned long long* dscratch = nullptr;  // reduction outputs (8 words)
     unsigned long long* hscratch = nullptr;  // pinned mirror
@@ -274,6 +275,14 @@ static void ensure_stats(gs_cc_t* h) {
     }
 }
 
+// Vertices a ring fold claims straight under the giant root go to their own bitmap (cbits); the
+// next incremental close sets their gbits bits without reading parent[] (experiment build CBITS
+// until measured on the GPU)
+#ifdef GS_EXP_CBITS
+constexpr bool kUseCbits = true;
+#else
+constexpr bool kUseCbits = false;
+#endif
 static WarmBuild warm_build_args(gs_cc_t* h);
 static void launch_warm_build(gs_cc_t* h, hipEvent_t stop);
 
@@ -367,6 +376,7 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     hot.count_edges = build ? h->warm_sample : 0;
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
     f.mark_len = h->mark_ctr;
+    f.cbits = kUseCbits ? h->cbits : nullptr;
     KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_RING : h->fold_timer);
     const bool st = h->dstats != nullptr;
     const dim3 grid(grid_for(n / 4, kHotThreads, (unsigned)std::max(h->cus, 1)));
@@ -647,7 +657,7 @@ int compress_impl(gs_cc_t* h) {
         ++h->closes;
         klaunch(k_compress, dim3(grid_for(h->cap, 1024, kCompressGrid)), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
                 h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot,
-                (int)h->sbits_stale);
+                (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr);
         h->sbits_stale = false;
     }
     GS_HIP(hipGetLastError());
@@ -861,6 +871,7 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
         h->mark = h->mark_buf;
     }
     if (hipMalloc(&h->gbits, mark_bytes(h->cap)) != hipSuccess || hipMalloc(&h->sbits, mark_bytes(h->cap)) != hipSuccess ||
+        hipMalloc(&h->cbits, mark_bytes(h->cap)) != hipSuccess ||
         hipMalloc(&h->derr, kDerrBytes) != hipSuccess || hipMalloc(&h->dscratch, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&h->hscratch, 8 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
@@ -936,6 +947,7 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->derr) (void)hipFree(h->derr);
     if (h->gbits) (void)hipFree(h->gbits);
     if (h->sbits) (void)hipFree(h->sbits);
+    if (h->cbits) (void)hipFree(h->cbits);
     if (h->dstats) (void)hipFree(h->dstats);
     if (h->hot) (void)hipFree(h->hot);
     if (h->hot_cand) (void)hipFree(h->hot_cand);
@@ -970,6 +982,7 @@ int gs_cc_reset(gs_cc_t* h) {
     if (h->mark_ctr) GS_HIP(hipMemsetAsync(h->mark_ctr, 0, 2 * sizeof(unsigned long long), h->stream));
     GS_HIP(hipMemsetAsync(h->gbits, 0, mark_bytes(h->cap), h->stream));
     GS_HIP(hipMemsetAsync(h->sbits, 0, mark_bytes(h->cap), h->stream));
+    GS_HIP(hipMemsetAsync(h->cbits, 0, mark_bytes(h->cap), h->stream));
     // giant state (cc_kernels.hpp, giant_state()): both slots no giant / gbits built for none,
     // hot set owner none
     GS_HIP(hipMemsetAsync(h->derr + 1, 0xFF, 5 * sizeof(uint32_t), h->stream));

@@ -216,6 +216,7 @@ struct FoldArgs {
     uint32_t halve = 1;          // path halving in root walks (find_root)
     unsigned long long* work = nullptr;   // k_fold: dynamic chunk counter (young forest), or null
     unsigned long long* mark_len = nullptr;   // MARK: the hook log's length word (mark = the log)
+    uint32_t* cbits = nullptr;   // ring folds: vertices claimed straight under the giant root (k_compress)
 };
 
 // ---- LDS hot set (steady state) ----
@@ -557,7 +558,11 @@ __device__ __forceinline__ void union_group_g(const FoldArgs& f, const uint32_t 
     for (int k = 0; k < EPT; ++k) {
         if (claimed[k]) {
             const uint32_t x = (gflag[k] == 2u) ? u[k] : v[k];
-            set_seen(f.sbits, x);
+            // a claimed vertex is a depth-1 child of gR, the root the next incremental close labels
+            // the giant with: that close only sets its gbits bit (cbits, no parent[] read); a close
+            // that is a full pass reads every parent[] word anyway. Without cbits: the seen bit.
+            if (f.cbits) set_mark(f.cbits, x);
+            else set_seen(f.sbits, x);
             if (STATS) { ++st.inits; ++st.hooks; }
             m[k] = MARK ? x : kInvalid;
         } else {
@@ -1168,7 +1173,8 @@ __global__ __launch_bounds__(1024) void k_pick_giant(const uint32_t* __restrict_
 __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent, uint32_t n,
                                                   uint32_t* __restrict__ gbits, uint32_t* __restrict__ sbits,
                                                   const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                  uint32_t* __restrict__ owner, uint2* __restrict__ hot, int rebuild_seen) {
+                                                  uint32_t* __restrict__ owner, uint2* __restrict__ hot, int rebuild_seen,
+                                                  uint32_t* __restrict__ cbits) {
     __shared__ uint32_t s_g, s_inc, s_clear;
     if (threadIdx.x == 0) {
         const uint32_t g0 = in[0];
@@ -1200,7 +1206,9 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
         const uint32_t nwords = (uint32_t)((n + 31) >> 5);
         for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += gridDim.x * blockDim.x) {
             uint32_t cand = sbits[w] & ~gbits[w];
-            uint32_t add = 0;
+            // vertices claimed under the giant root since the last close: already labelled g
+            uint32_t add = cbits ? cbits[w] : 0u;
+            if (add) cbits[w] = 0u;
             // up to 8 stragglers at a time, their parent and grandparent reads issued back to
             // back (one at a time: a young Erdos-Renyi window's close, ~32 stragglers per word,
             // spent 121 us per 2^24 ids in dependent loads)
@@ -1272,7 +1280,10 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                 sw |= __shfl_xor(sw, 1, 64);
                 sw |= __shfl_xor(sw, 2, 64);
                 sw |= __shfl_xor(sw, 4, 64);
-                if ((lane & 7) == 0 && base < n) sbits[base >> 5] = sw;
+                if ((lane & 7) == 0 && base < n) {
+                    sbits[base >> 5] = sw;
+                    if (cbits) cbits[base >> 5] = 0u;    // this pass labelled the claimed vertices too
+                }
             }
         }
     }
