@@ -324,7 +324,7 @@ def main():
                                        "(P x 8 TB/s)" % (per_edge, label_b)},
             },
             "kernels": {
-                "fold_share": (young_ms + ring_ms) / (elapsed * 1e3),
+                "fold_share": (young_ms + ring_ms) / (elapsed / a.steps * 1e3),     # timed: the last step's folds
                 "compress_ms_per_window": comp_ms / max(comp_n, 1),
                 "compress_share": comp_ms / (elapsed / a.steps * 1e3),
             },
