@@ -230,7 +230,7 @@ constexpr uint32_t kRingMinBits = 25;
 // at most capacity/8) and re-checked every kWarmEvery-th launch (rebuilt only when invalid for the
 // current giant). Launch 2 (RMAT-26 window 4): windows 2-12 35 us less than launch 3, as launch 0
 // or 1 (profiles/r02_ab_experiments.txt r02_w); 2^24-edge samples gained nothing (r02_u)
-constexpr uint64_t kWarmAt = 2, kWarmEvery = 16, kWarmSample = 1ull << 23;
+constexpr uint64_t kWarmAt = 2, kWarmEvery = 64, kWarmSample = 1ull << 23;   // every 16 -> 64: r02_bg
 constexpr uint32_t kWarmBucketsMaxBits = 18;
                                                     // slower per steady window, r02_u)
 constexpr uint32_t kHotThresh = 3;                  // sightings before hot-set admission (233 -> 229 us)

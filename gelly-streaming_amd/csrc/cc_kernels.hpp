@@ -1091,7 +1091,7 @@ __global__ __launch_bounds__(256) void k_fold_slots(const uint32_t* __restrict__
 // there is no giant yet).
 constexpr int kPickSamples = 1024;
 constexpr int kPickSlots = 2048;
-constexpr int kPickEvery = 8;
+constexpr int kPickEvery = 16;              // 8 -> 16: closes -40 us per step (r02_bg)
 
 struct PickLds {
     uint32_t keys[kPickSlots];
