@@ -221,7 +221,7 @@ constexpr uint64_t kMergeBulk = 1ull << 20;   // smaller batches: one launch (a 
                                               // summary rarely joins big components)
 // k_compress grid: the incremental close is a bitmap scan; 16384 workgroups cost 140 us more per
 // 64-window step than 2048 (young closes: 8192-65536 gave the same sum as 2048)
-constexpr unsigned kCompressGrid = 2048;
+constexpr unsigned kCompressGrid = 2048;          // 1024-8192 swept: 2048 fastest (r02_bl/bm)
 // Steady ring fold and its warm set from ids >= 2^kRingMinBits (gbits outgrows an XCD's 4 MiB L2):
 // with gbits L2-resident the hot set's 128 KiB LDS fill per workgroup costs more than it saves
 // (RMAT-20 2^20-edge windows: ring 83 us, plain 61 us; ER 2^24: 141 vs 126 us).
