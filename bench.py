@@ -11,7 +11,7 @@ Workload (BASELINE.json metric "streaming CC edges/sec (RMAT-26) at 1/2/4/8 MI35
       93-106), so each GPU holds E/P edges.
   --scaling weak: every rank folds 2^30 edges; global window = P x 2^24 edges of a P x 2^30 stream.
   N > 1: the exchange runs under the C ABI (gs_cc_merge_window over RCCL, csrc/comm.hip) with
-  --dist-backend nccl; --dist-backend gloo runs the Python exchange (gsgpu/tree.py) over host
+  --dist-backend nccl; --dist-backend gloo runs the Python exchange (tests/gloo_tree.py) over host
   staging, for several ranks on one GPU.
 One step = one whole pass over the stream from an empty summary (reset included).
 
@@ -38,7 +38,8 @@ import torch.distributed as dist  # noqa: E402
 
 import gsgpu  # noqa: E402
 from gsgpu import gen  # noqa: E402
-from gsgpu._abi import GS_K_COMPRESS, GS_K_EXPORT, GS_K_FOLD, GS_K_MERGE, GS_K_RING, GS_TIMING_MASK  # noqa: E402
+from gsgpu._abi import (GS_K_COMPRESS, GS_K_EXPORT, GS_K_FOLD, GS_K_MERGE, GS_K_RING, GS_K_ROUTE,  # noqa: E402
+                        GS_TIMING_MASK, lib_source_sha)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "streaming CC edges/sec (RMAT-26) at 1/2/4/8 MI355X + % of HBM roofline"
@@ -153,7 +154,8 @@ def main():
     if world > 1 and a.dist_backend == "nccl":
         comm = gsgpu.Comm.from_process_group(local)                  # C ABI: gs_comm_create (RCCL)
     elif world > 1:
-        from gsgpu.tree import AllgatherMerge, GatherMerge, TreeMerge
+        sys.path.insert(0, os.path.join(ROOT, "tests"))          # test mode: the Python exchange model
+        from gloo_tree import AllgatherMerge, GatherMerge, TreeMerge
         cls = {"allgather": AllgatherMerge, "gather": GatherMerge, "tree": TreeMerge}[a.merge]
         tree = cls(ds, capacity_pairs=V, device=dev)
     gather = tree is not None and a.merge == "gather"
@@ -170,7 +172,7 @@ def main():
         else:
             ds.close_window()
 
-    fold_mask = GS_TIMING_MASK | (1 << GS_K_FOLD) | (1 << GS_K_RING) | \
+    fold_mask = GS_TIMING_MASK | (1 << GS_K_FOLD) | (1 << GS_K_RING) | (1 << GS_K_ROUTE) | \
         ((1 << GS_K_MERGE) | (1 << GS_K_EXPORT) if world > 1 else 0)
 
     def step():
@@ -203,6 +205,8 @@ def main():
     elapsed = time.perf_counter() - t0
     young_ms, young_n = ds.kernel_time(GS_K_FOLD)
     ring_ms, ring_n = ds.kernel_time(GS_K_RING)
+    route_ms, route_n = ds.kernel_time(GS_K_ROUTE)
+    young_e, ring_e, route_e = (ds.kernel_units(k) for k in (GS_K_FOLD, GS_K_RING, GS_K_ROUTE))
     merge_ms, _ = ds.kernel_time(GS_K_MERGE)
     export_ms, _ = ds.kernel_time(GS_K_EXPORT)
     ds.timing(False)
@@ -256,18 +260,21 @@ def main():
         label_b = 4 if a.id_bits == 32 else 8
         total_edges = a.steps * E_rank * world
         folds = nwin                                  # the timed launches: the last step's
-        ring_avg = ring_ms / ring_n if ring_n else None
-        fold_win_ms = (young_ms + ring_ms) / max(folds, 1) or float("nan")
-        ring_edges = W_rank - (W_rank % 4)
-        if ring_avg:
-            kernel, avg_ms = "k_fold_ring", ring_avg
-            alg_launch = per_edge * ring_edges
-        else:                                        # no steady ring launches (small ids: plain k_fold)
-            kernel, avg_ms = "k_fold (every window)", fold_win_ms
-            alg_launch = per_edge * W_rank
+        fold_win_ms = (young_ms + ring_ms + route_ms) / max(folds, 1) or float("nan")
+        # the dominant kernel: the steady fold (the routed fold's four launches, or k_fold_ring),
+        # bytes per launch from the edges each timed launch actually folded (the library cuts a
+        # long fold call into launches of at most 2^24 edges)
+        if route_n and route_ms >= ring_ms:
+            kernel, avg_ms, n_l, e_l = ROUTE_NAME, route_ms / route_n, route_n, route_e / route_n
+        elif ring_n:
+            kernel, avg_ms, n_l, e_l = "k_fold_ring", ring_ms / ring_n, ring_n, ring_e / ring_n
+        else:                                        # no steady launches (small ids: plain k_fold)
+            kernel, avg_ms, n_l, e_l = "k_fold (every window)", fold_win_ms, folds, W_rank
         if not avg_ms:                               # --no-fold-timing
             avg_ms = float("nan")
+        alg_launch = per_edge * e_l
         achieved = alg_launch / (avg_ms * 1e-3) / 1e9
+        prof, prof_note = steady_profile(a, kernel, e_l)
         alg_step = per_edge * E_rank * world + label_b * seen_sum          # BASELINE.md B_alg per step
         wall_gbs = alg_step * a.steps / elapsed / 1e9
         nv, nc = ds.stats()
@@ -305,26 +312,28 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic_per_launch(a, W_rank) if kernel == "k_fold_ring" else None,
+                "traffic": prof.get("hbm_bytes_per_launch") if prof else None,
+                "traffic_source": prof_note,
                 "kernel": kernel,
                 "alg_bytes_per_launch": alg_launch,
+                "edges_per_launch": e_l,
                 "avg_launch_ms": avg_ms,
-                "launches": ring_n if ring_avg else folds,
-                "definition": "dominant kernel: %d B per edge (edge read + 2 parent words, SURVEY.md 8(d)) x edges "
-                              "per launch / its average launch duration (HIP events on the launch stream, the "
-                              "last step of the timed region)" % per_edge,
+                "launches": n_l,
+                "definition": "dominant kernel: %d B per edge (edge read + 2 parent words, SURVEY.md 8(d)) x the "
+                              "edges each launch folded / its average launch duration (HIP events on the launch "
+                              "stream, the last step of the timed region)" % per_edge,
                 "fold_all": {"achieved": per_edge * W_rank / (fold_win_ms * 1e-3) / 1e9,
                              "frac": per_edge * W_rank / (fold_win_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                              "ms_per_window": fold_win_ms, "young_launches": young_n,
                              "definition": "every UpdateCC launch of a window (young k_fold + steady k_fold_ring)"},
-                "requests": request_roofline(a, W_rank, avg_ms) if kernel == "k_fold_ring" else None,
+                "requests": request_roofline(prof, avg_ms) if prof else None,
                 "wall": {"achieved": wall_gbs, "frac": wall_gbs / (world * HBM_PEAK_GBS),
                          "alg_bytes_per_step": alg_step,
                          "definition": "BASELINE.md: sum over windows of (%d E_w + %d |V_seen,w|) / wall time / "
                                        "(P x 8 TB/s)" % (per_edge, label_b)},
             },
             "kernels": {
-                "fold_share": (young_ms + ring_ms) / (elapsed / a.steps * 1e3),     # timed: the last step's folds
+                "fold_share": (young_ms + ring_ms + route_ms) / (elapsed / a.steps * 1e3),   # timed: the last step's folds
                 "compress_ms_per_window": comp_ms / max(comp_n, 1),
                 "compress_share": comp_ms / (elapsed / a.steps * 1e3),
             },
@@ -370,53 +379,52 @@ def _pow2(x: int) -> str:
     return str(x)
 
 
-def traffic_per_launch(a, W_rank):
-    """HBM bytes per k_fold_ring launch from the committed PMC passes (profiles/pmc_traffic.py), if
-    they were taken on this configuration."""
+ROUTE_NAME = "routed fold (k_sift + k_probe<B> + k_probe<C> + k_union_surv)"
+
+
+def steady_profile(a, kernel, edges_per_launch):
+    """PMC counts of the dominant kernel from the committed profile (profiles/pmc_traffic.py), only
+    if they were taken on this configuration AND on these kernel sources (the profile carries the
+    lib_source_sha of the library it measured; any kernel change makes it stale and drops it)."""
     if not os.path.exists(a.traffic_json):
-        return None
+        return None, "no profile"
     try:
         tj = json.load(open(a.traffic_json))
-        if tj.get("window_edges") == W_rank and tj.get("scale") == a.scale and tj.get("id_bits", 32) == a.id_bits:
-            return tj.get("ring", {}).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
-    return None
+    except Exception as e:
+        return None, "unreadable profile: %r" % (e,)
+    st = tj.get("steady") or {}
+    sha = lib_source_sha()
+    if tj.get("lib_source_sha") != sha:
+        return None, "stale: profile of library %s, this library %s" % (tj.get("lib_source_sha"), sha)
+    if (tj.get("scale"), tj.get("id_bits", 32), st.get("kernel")) != (a.scale, a.id_bits, kernel) or \
+            abs(st.get("edges_per_launch", 0) - edges_per_launch) > 4:
+        return None, "profile of another configuration"
+    return st, "%s (PMC, library %s)" % (os.path.relpath(a.traffic_json, ROOT), sha)
 
 
-def request_roofline(a, W_rank, avg_ms):
-    """The bound the steady fold actually meets: L2 requests, not bytes. Per k_fold_ring launch,
-    the PMC passes (profiles/fold_traffic.json: TCC requests and hit rate) split into L2 hits, the
-    edge stream and random L2 misses; tools/request_lab.hip measured what this chip sustains for
-    each (profiles/r02_request_lab.json: random 4-B loads over an L2-resident table, over a table
-    in Infinity Cache, a streaming read). Bound = max(hits / hit rate, stream bytes / stream rate +
-    random misses / miss rate): hits and misses are served by different units and overlap."""
+def request_roofline(prof, avg_ms):
+    """What bounds the steady fold besides bytes: L2 requests. Per launch, the PMC passes give its TCC
+    requests and its HBM bytes; tools/request_lab.hip measured what this chip sustains:
+    random 4-B loads over an L2-resident table (the request rate of L2 channels) and a streaming
+    read. Bound = max(requests / L2 request rate, HBM bytes / stream rate): the two are served by
+    different units and overlap."""
     lab_path = os.path.join(ROOT, "profiles", "r02_request_lab.json")
-    if not (os.path.exists(a.traffic_json) and os.path.exists(lab_path)):
+    if not os.path.exists(lab_path):
         return None
     try:
-        tj, lab = json.load(open(a.traffic_json)), json.load(open(lab_path))
-        if not (tj.get("window_edges") == W_rank and tj.get("scale") == a.scale and tj.get("id_bits", 32) == a.id_bits):
-            return None
-        ring = tj["ring"]
-        req, hit = ring["tcc_requests_per_launch"], ring["l2_hit_rate"]
-        hits, misses = req * hit, req * (1.0 - hit)
-        stream_bytes = W_rank * (8 if a.id_bits == 32 else 16)
-        stream_req = stream_bytes / 64.0
-        hit_gps, miss_gps = lab["rand4B_1MiB_32w_Gps"], lab["rand4B_64MiB_32w_Gps"]
-        stream_tbps = lab["stream_read_TBps"]
-        t_hits = hits / (hit_gps * 1e3)                                   # us
-        t_miss = stream_bytes / (stream_tbps * 1e6) + max(misses - stream_req, 0.0) / (miss_gps * 1e3)
-        bound_us = max(t_hits, t_miss)
-        return {"bound": "l2-requests", "kernel": "k_fold_ring", "l2_hits_per_launch": hits,
-                "l2_misses_per_launch": misses, "stream_requests_per_launch": stream_req,
-                "hit_rate_peak_Gps": hit_gps, "miss_rate_peak_Gps": miss_gps, "stream_peak_TBps": stream_tbps,
-                "hits_us": t_hits, "misses_us": t_miss, "bound_us": bound_us, "avg_launch_us": avg_ms * 1e3,
+        lab = json.load(open(lab_path))
+        req, hbm = prof["tcc_requests_per_launch"], prof["hbm_bytes_per_launch"]
+        req_gps, stream_tbps = lab["rand4B_1MiB_32w_Gps"], lab["stream_read_TBps"]
+        t_req = req / (req_gps * 1e3)                                     # us
+        t_bytes = hbm / (stream_tbps * 1e6)
+        bound_us = max(t_req, t_bytes)
+        return {"bound": "l2-requests" if t_req >= t_bytes else "hbm-bytes", "tcc_requests_per_launch": req,
+                "hbm_bytes_per_launch": hbm, "request_peak_Gps": req_gps, "stream_peak_TBps": stream_tbps,
+                "requests_us": t_req, "bytes_us": t_bytes, "bound_us": bound_us, "avg_launch_us": avg_ms * 1e3,
                 "frac": bound_us / (avg_ms * 1e3),
-                "definition": "max(L2 hits / 1-MiB random-load rate, edge stream / stream rate + other L2 misses / "
-                              "Infinity-Cache random-load rate) per launch (PMC counts: profiles/fold_traffic.json; "
-                              "rates measured by tools/request_lab.hip: profiles/r02_request_lab.json) / the "
-                              "launch's average duration"}
+                "definition": "max(TCC requests / L2 random-request rate, PMC HBM bytes / streaming-read rate) per "
+                              "launch (counts: profiles/fold_traffic.json; rates: tools/request_lab.hip, "
+                              "profiles/r02_request_lab.json) / the launch's average duration"}
     except Exception:
         return None
 

@@ -10,11 +10,10 @@
 
 #include <hip/hip_ext.h>
 
+#include "cc_internal.hpp"
 #include "cc_kernels.hpp"
+#include "route.hpp"
 #include "sparse_ids.hpp"
-#ifdef GS_EXP_ROUTE
-#include "route_fold.hpp"
-#endif
 
 #include <hipcub/hipcub.hpp>
 
@@ -83,6 +82,7 @@ struct gs_cc {
     uint64_t edges_since_reset = 0;      // drives the young-forest launch split (fold_impl)
     uint64_t ring_launches = 0;          // ring fold launches since reset (hot-set admission cadence)
     uint64_t closes = 0;                 // compressions since reset (giant re-sampled every kPickEvery)
+    uint64_t reset_gen = 0;              // gs_cc_reset calls (a communicator's per-stream state follows it)
     unsigned long long* dstats = nullptr;    // GSGPU_FOLD_STATS=1: per-window fold counters
     uint2* hot = nullptr;                // LDS hot set master copy (kHotBuckets uint2), steady folds
     uint32_t hot_bits = 0;               // ids < 2^hot_bits
@@ -95,9 +95,11 @@ struct gs_cc {
     uint64_t warm_sample = 0;            // edges a warm count launch samples
     uint32_t warm_bcap = 0;              // keys per hash bucket
     int cus = 0;                         // compute units: k_fold_ring grid
-    uint2* rq = nullptr;                 // routed fold: part queues A -> B, then B -> C (2 x parts x rq_cap)
-    uint64_t rq_cap = 0;                 // entries per part queue
-    uint32_t* rcnt = nullptr;            // routed fold: list lengths [2][grid][parts] + the admission flag
+    // routed steady fold (route.hpp): lists, survivors, counters; sized for route_edges edges per launch
+    void* route_mem = nullptr;
+    size_t route_bytes = 0;
+    uint64_t route_edges = 0;
+    uint64_t route_launches = 0;         // parity of the overflow counters
     // GS_CC_SPARSE_IDS: id -> slot table; cap (above) = slots = 2^hbits + 1
     bool sparse = false;
     int64_t* keys = nullptr;             // 2^hbits slot keys (INT64_MIN = empty)
@@ -109,11 +111,12 @@ struct gs_cc {
     bool timing = false;
     uint32_t timing_mask = ~0u;          // kernels timed while timing (bit GS_K_*)
     int fold_timer = GS_K_FOLD;          // GS_K_MERGE while folding an exported partial summary
-    struct Pend { int k; hipEvent_t a, b; };
+    struct Pend { int k; hipEvent_t a, b; uint64_t units; };
     std::vector<Pend> pending;
     std::vector<hipEvent_t> pool;
     double total_ms[GS_K_COUNT] = {};
     uint64_t launches[GS_K_COUNT] = {};
+    uint64_t units[GS_K_COUNT] = {};     // edges (folds, merges) or vertices (closes) the timed launches took
 };
 
 namespace {
@@ -154,8 +157,8 @@ constexpr size_t kDerrBytes = 256;
 // separate hipEventRecord marker packets are barrier packets, ~10 us of idle GPU each on gfx950
 // (profiles/r01_v3).
 struct KTimer {
-    gs_cc_t* h; int k; hipEvent_t a = nullptr, b = nullptr;
-    KTimer(gs_cc_t* h_, int k_) : h(h_), k(k_) {
+    gs_cc_t* h; int k; hipEvent_t a = nullptr, b = nullptr; uint64_t units;
+    KTimer(gs_cc_t* h_, int k_, uint64_t units_ = 0) : h(h_), k(k_), units(units_) {
         if (!h->timing || !(h->timing_mask & (1u << k))) return;
         a = get_event(h);
         b = get_event(h);
@@ -163,7 +166,7 @@ struct KTimer {
     hipEvent_t start() const { return a; }
     hipEvent_t stop() const { return b; }
     ~KTimer() {
-        if (a) h->pending.push_back({k, a, b});
+        if (a) h->pending.push_back({k, a, b, units});
     }
 };
 
@@ -181,6 +184,7 @@ int resolve_timing(gs_cc_t* h) {
         GS_HIP(hipEventElapsedTime(&ms, p.a, p.b));
         h->total_ms[p.k] += ms;
         h->launches[p.k] += 1;
+        h->units[p.k] += p.units;
         h->pool.push_back(p.a);
         h->pool.push_back(p.b);
     }
@@ -242,10 +246,10 @@ constexpr uint32_t kYoungSplitDiv = 16;
 
 // ---- debug variables (read once per process; none is needed in production) ----
 //   GSGPU_FOLD_STATS=1       per-window fold counters on stderr (STATS kernel variants; same results)
-//   GSGPU_FOLD_MODE=plain|ring|auto   force the steady fold variant (parity tests of each variant)
+//   GSGPU_FOLD_MODE=plain|ring|route|auto   force the steady fold variant (parity tests of each variant)
 //   GSGPU_RING_MIN_BITS=B    ring fold + warm set from ids >= 2^B instead of 2^25 (tests at small sizes)
 //   GSGPU_YOUNG_SPLIT=S      young split after S edges instead of capacity/16 (0 = off; tests)
-enum FoldMode { kFoldPlain = 0, kFoldRing = 1, kFoldAuto = 2 };
+enum FoldMode { kFoldPlain = 0, kFoldRing = 1, kFoldAuto = 2, kFoldRoute = 3 };
 struct DebugEnv {
     bool fold_stats = false;
     int fold_mode = kFoldAuto;
@@ -257,6 +261,7 @@ struct DebugEnv {
         e = getenv("GSGPU_FOLD_MODE");
         if (e && !strcmp(e, "plain")) fold_mode = kFoldPlain;
         if (e && !strcmp(e, "ring")) fold_mode = kFoldRing;
+        if (e && !strcmp(e, "route")) fold_mode = kFoldRoute;
         e = getenv("GSGPU_RING_MIN_BITS");
         if (e && *e) ring_min_bits = (uint32_t)strtoul(e, nullptr, 0);
         e = getenv("GSGPU_YOUNG_SPLIT");
@@ -305,7 +310,7 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
     }
     const bool vec = std::is_same<IdT, uint32_t>::value && !AOS &&
                      ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
-    KTimer t(h, h->fold_timer);
+    KTimer t(h, h->fold_timer, n);
 #define GS_LAUNCH_FOLD(MARKV, VECV, EPTV, STV)                                                                       \
     klaunch((k_fold<IdT, AOS, MARKV, VECV, EPTV, STV>), dim3(grid), dim3(kFoldThreads), h->stream, t.start(), t.stop(), \
             (const IdT*)a, (const IdT*)b, f)
@@ -373,7 +378,7 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
     f.mark_len = h->mark_ctr;
     f.cbits = kUseCbits ? h->cbits : nullptr;
-    KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_RING : h->fold_timer);
+    KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_RING : h->fold_timer, n);
     const bool st = h->dstats != nullptr;
     const dim3 grid(grid_for(n / 4, kHotThreads, (unsigned)std::max(h->cus, 1)));
     hipEvent_t stop = build ? nullptr : t.stop();
@@ -388,36 +393,72 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     if (build) launch_warm_build(h, t.stop());
 }
 
-#ifdef GS_EXP_ROUTE
-// Routed steady fold (cc_kernels.hpp k_route_a / k_route_bc): the giant filter from LDS slices of
-// gbits instead of L2 lookups. Queues hold 4x a part's mean share (a tile past that is decided in
-// place from global gbits).
-static bool use_route(const gs_cc_t* h) {
-    return h->hot && !h->dstats && h->cap <= 0x80000000u && h->hot_bits <= kSliceBits + 9;
+// Routed steady fold (route.hpp): the giant filter out of LDS slices of gbits, for ids of 2^25..2^26
+// (gbits past an XCD's L2, at most kRouteMaxParts parts of 2^20 ids), on windows of at least
+// kRouteMinEdges edges (below that the per-launch slice fills and list scans cost more than the
+// ring fold's lookups). GSGPU_FOLD_MODE=route forces it wherever the ids fit (tests at small sizes).
+constexpr uint64_t kRouteMinEdges = 1ull << 22;
+static bool use_route(const gs_cc_t* h, uint64_t n) {
+    if (!h->hot || h->dstats || h->sparse || h->hot_bits > kPartBits + 6 || h->cus <= 0) return false;
+    const uint32_t parts = 1u << (h->hot_bits > kPartBits ? h->hot_bits - kPartBits : 0);
+    const uint32_t grid = (uint32_t)h->cus / parts * parts;
+    if (grid < parts) return false;
+    const int m = dbg().fold_mode;
+    if (m == kFoldRoute) return true;
+    return m == kFoldAuto && h->hot_bits >= dbg().ring_min_bits && n >= kRouteMinEdges;
 }
 
 template <typename IdT>
 int launch_fold_route(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
-    const uint32_t parts = 1u << (h->hot_bits > kSliceBits ? h->hot_bits - kSliceBits : 0);
-    const uint32_t grid = (uint32_t)std::min(std::max(h->cus, 1), (int)kMaxRouteGrid);
-    const uint64_t need = 4 * (n / ((uint64_t)grid * parts)) + 512;          // 4x a list's mean share
-    if (!h->rcnt) {
-        GS_HIP(hipMalloc(&h->rcnt, (2 * (size_t)kMaxRouteGrid * kMaxParts + 64) * sizeof(uint32_t)));
-    }
-    if (need > h->rq_cap) {
-        if (h->rq) {
+    const uint32_t parts = 1u << (h->hot_bits > kPartBits ? h->hot_bits - kPartBits : 0);
+    const uint32_t grid = (uint32_t)h->cus / parts * parts;
+    // lists: 2x a list's mean share if every edge became an entry, + a hub's worth; survivors: 2x a
+    // workgroup's share of the edges (the rest overflows into one shared list of n entries)
+    const uint64_t need_edges = std::max<uint64_t>(n, 1ull << 20);
+    const uint64_t cap = ((2 * need_edges / ((uint64_t)grid * parts) + 1024) + 3) & ~3ull;
+    const uint64_t scap = 2 * need_edges / grid + 1024;
+    const uint64_t ocap = need_edges;
+    const size_t lists = (size_t)grid * parts * cap;
+    const size_t bytes = lists * 4 + lists * 8 + lists * 4 + 3ull * grid * parts * 4 + 3ull * grid * scap * 8 +
+                         3ull * grid * 4 + ocap * 8 + 64 * 8 + 4096;
+    if (need_edges > h->route_edges) {
+        if (h->route_mem) {
             GS_HIP(hipStreamSynchronize(h->stream));
-            GS_HIP(hipFree(h->rq));
-            h->rq = nullptr;
+            GS_HIP(hipFree(h->route_mem));
+            h->route_mem = nullptr;
+            h->route_edges = 0;
         }
-        if (hipMalloc(&h->rq, 2 * (size_t)grid * parts * need * sizeof(uint2)) != hipSuccess) {
+        if (hipMalloc(&h->route_mem, bytes) != hipSuccess) {
             (void)hipGetLastError();
-            h->rq_cap = 0;
-            return fail(GS_ERR_NOMEM, "routed fold lists (%llu entries) allocation failed",
-                        (unsigned long long)(2 * (uint64_t)grid * parts * need));
+            return fail(GS_ERR_NOMEM, "routed fold lists (%zu bytes) allocation failed", bytes);
         }
-        h->rq_cap = need;
+        GS_HIP(hipMemsetAsync(h->route_mem, 0, 4096, h->stream));          // the counters (first 4 KiB)
+        h->route_edges = need_edges;
+        h->route_bytes = bytes;
     }
+    char* m = static_cast<char*>(h->route_mem);
+    auto* ctl = reinterpret_cast<unsigned long long*>(m);                   // [0..1] overflow counts, [2] admit
+    size_t off = 4096;
+    auto take = [&](size_t b) { char* p = m + off; off += (b + 255) & ~(size_t)255; return p; };
+    RouteArgs r;
+    r.qs = reinterpret_cast<uint32_t*>(take(lists * 4));
+    r.qd = reinterpret_cast<uint2*>(take(lists * 8));
+    r.qc = reinterpret_cast<uint32_t*>(take(lists * 4));
+    r.cnt = reinterpret_cast<uint32_t*>(take(3ull * grid * parts * 4));
+    r.surv = reinterpret_cast<uint2*>(take(3ull * grid * scap * 8));
+    r.scnt = reinterpret_cast<uint32_t*>(take(3ull * grid * 4));
+    r.over = reinterpret_cast<uint2*>(take(ocap * 8));
+    const int q = (int)(h->route_launches & 1);
+    ++h->route_launches;
+    r.ocount = ctl + q;
+    r.onext = ctl + (1 - q);
+    r.admit = ctl + 2;
+    r.cap = cap;
+    r.scap = scap;
+    r.ocap = ocap;
+    r.parts = parts;
+    r.gwords = (uint32_t)((h->cap + 31) / 32);
+    r.grid = grid;
     HotArgs hot{h->hot, h->hot_bits, h->hot_cand};
     hot.sample_edges = kHotSampleEdges;
     hot.budget = h->derr + 6;
@@ -425,25 +466,18 @@ int launch_fold_route(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     ++h->ring_launches;
     hot.five = (h->hot_bits <= kHotBucketBits + 12) ? 1u : 0u;
     hot.thresh = kHotThresh;
-    FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
+    FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, nullptr};
     f.mark_len = h->mark_ctr;
-    RouteArgs r{h->rq, h->rq + (size_t)grid * parts * h->rq_cap, h->rcnt,
-                reinterpret_cast<unsigned long long*>(h->rcnt + 2 * (size_t)kMaxRouteGrid * kMaxParts),
-                h->rq_cap, parts, (uint32_t)((h->cap + 31) / 32)};
-    KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_RING : h->fold_timer);
-    const dim3 g(grid), blk(kRouteThreads);
-    if (h->mark) {
-        klaunch(k_route_a<IdT, true, false>, g, blk, h->stream, t.start(), nullptr, a, b, f, hot, r);
-        klaunch(k_route_bc<true, true, false>, g, blk, h->stream, nullptr, nullptr, f, hot, r);
-        klaunch(k_route_bc<false, true, false>, g, blk, h->stream, nullptr, t.stop(), f, hot, r);
-    } else {
-        klaunch(k_route_a<IdT, false, false>, g, blk, h->stream, t.start(), nullptr, a, b, f, hot, r);
-        klaunch(k_route_bc<true, false, false>, g, blk, h->stream, nullptr, nullptr, f, hot, r);
-        klaunch(k_route_bc<false, false, false>, g, blk, h->stream, nullptr, t.stop(), f, hot, r);
-    }
+    f.cbits = kUseCbits ? h->cbits : nullptr;
+    KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_ROUTE : h->fold_timer, n);
+    const uint32_t ob = 64;                                                 // overflow-list blocks
+    klaunch(k_sift<IdT>, dim3(grid), dim3(kSiftThreads), h->stream, t.start(), nullptr, a, b, f, hot, r);
+    klaunch(k_probe<true>, dim3(grid), dim3(kProbeThreads), h->stream, nullptr, nullptr, f, hot, r);
+    klaunch(k_probe<false>, dim3(grid), dim3(kProbeThreads), h->stream, nullptr, nullptr, f, hot, r);
+    if (h->mark) klaunch(k_union_surv<true>, dim3(3 * grid + ob), dim3(256), h->stream, nullptr, t.stop(), f, r, ob);
+    else klaunch(k_union_surv<false>, dim3(3 * grid + ob), dim3(256), h->stream, nullptr, t.stop(), f, r, ob);
     return GS_OK;
 }
-#endif  // GS_EXP_ROUTE
 
 // Young-forest split points (dense ids, SoA folds): one internal close at capacity/16 edges since
 // reset where gbits outgrows L2 (ids >= 2^kRingMinBits), or at GSGPU_YOUNG_SPLIT
@@ -473,7 +507,7 @@ static void internal_close(gs_cc_t* h) {
 // SoA batches where use_ring() holds, else k_fold. Partial summaries (AOS pairs) fold a short head
 // launch first, then the rest in one launch.
 template <typename IdT, bool AOS>
-void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, size_t esz) {
+int launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, size_t esz) {
     // window 1 of the headline stays in k_fold after its young split: the ring fold there (hot set
     // empty, the giant root hooked again and again) took 2.06 ms instead of 1.19 (r02_n)
     const uint64_t young_limit = h->cap / 4;
@@ -504,14 +538,13 @@ void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, siz
             continue;
         }
         m = std::min(m, kInternalCloseEdges);
-        if (h->hot && use_ring(h) && aligned && m >= 4) {
+        if (h->hot && aligned && m >= 4 && use_route(h, m)) {
+            m &= ~(uint64_t)3;                          // the routed fold takes groups of 4 edges
+            const int rc = launch_fold_route<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
+            if (rc != GS_OK) return rc;
+        } else if (h->hot && use_ring(h) && aligned && m >= 4) {
             m &= ~(uint64_t)3;                          // the ring fold takes groups of 4 edges
-#ifdef GS_EXP_ROUTE
-            if (use_route(h))
-                (void)launch_fold_route<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
-            else
-#endif
-                launch_fold_ring<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
+            launch_fold_ring<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
         } else {
             launch_fold<IdT, AOS>(h, a + off * stride, b + off * esz, m, false);
         }
@@ -519,6 +552,7 @@ void launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, siz
         off += m;
         if (off < n && n - off >= 4) internal_close(h);   // (a tail of < 4 edges folds unclosed)
     }
+    return GS_OK;
 }
 
 SparseArgs sparse_args(gs_cc_t* h) {
@@ -554,20 +588,19 @@ void launch_fold_sparse(gs_cc_t* h, const int64_t* a, const int64_t* b, uint64_t
     }
 }
 
-void launch_fold_any(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, uint32_t id_bits) {
+int launch_fold_any(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, uint32_t id_bits) {
     if (h->sparse) {
         launch_fold_sparse(h, static_cast<const int64_t*>(a), static_cast<const int64_t*>(b), n, aos);
-        return;
+        return GS_OK;
     }
     const char* ca = static_cast<const char*>(a);
     const char* cb = static_cast<const char*>(b);
     if (id_bits == 32) {
-        if (aos) launch_fold_split<uint32_t, true>(h, ca, nullptr, n, 4);
-        else launch_fold_split<uint32_t, false>(h, ca, cb, n, 4);
-    } else {
-        if (aos) launch_fold_split<int64_t, true>(h, ca, nullptr, n, 8);
-        else launch_fold_split<int64_t, false>(h, ca, cb, n, 8);
+        if (aos) return launch_fold_split<uint32_t, true>(h, ca, nullptr, n, 4);
+        return launch_fold_split<uint32_t, false>(h, ca, cb, n, 4);
     }
+    if (aos) return launch_fold_split<int64_t, true>(h, ca, nullptr, n, 8);
+    return launch_fold_split<int64_t, false>(h, ca, cb, n, 8);
 }
 
 // host-buffer folds: edges per staging chunk (one window of the headline workload)
@@ -584,7 +617,7 @@ int fold_impl(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, ui
     h->compressed = false;
     h->minkey_valid = false;
     if (dev) {
-        launch_fold_any(h, a, b, n, aos, id_bits);
+        GS_TRY(launch_fold_any(h, a, b, n, aos, id_bits));
         GS_HIP(hipGetLastError());
         return GS_OK;
     }
@@ -617,7 +650,7 @@ int fold_impl(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, ui
         }
         GS_HIP(hipEventRecord(h->staged[k], h->copy));
         GS_HIP(hipStreamWaitEvent(h->stream, h->staged[k], 0));
-        launch_fold_any(h, s0, s1, m, aos, id_bits);
+        GS_TRY(launch_fold_any(h, s0, s1, m, aos, id_bits));
         GS_HIP(hipGetLastError());
         GS_HIP(hipEventRecord(h->freed[k], h->stream));
     }
@@ -640,7 +673,7 @@ int compress_impl(gs_cc_t* h) {
     report_fold_stats(h);
     if (h->compressed) return GS_OK;
     {
-        KTimer t(h, GS_K_COMPRESS);
+        KTimer t(h, GS_K_COMPRESS, h->cap);
         // re-sample the giant every kPickEvery closes (and, while there may be none yet, before
         // each of the first kEarlyPicks closes); otherwise k_compress follows it itself. (Early
         // picks before the first 16 closes cost 66 us per RMAT-26 step in no-op launches: r02_az.)
@@ -772,17 +805,10 @@ int find_sparse(gs_cc_t* h, const int64_t* ids, int64_t* roots, uint8_t* found, 
 }  // namespace
 
 namespace gsgpu {
-// internal accessors for comm.hip
-struct CcInfo {
-    uint32_t cap;
-    int device;
-    hipStream_t stream;
-    bool marks;
-    bool sparse;
-};
+// internal accessors for comm.hip (cc_internal.hpp)
 int cc_info(gs_cc_t* h, CcInfo* out) {
     GS_TRY(check(h));
-    *out = CcInfo{h->cap, h->device, h->stream, h->mark_buf != nullptr, h->sparse};
+    *out = CcInfo{h->cap, h->device, h->stream, h->mark_buf != nullptr, h->sparse, h->mark != nullptr, h->reset_gen};
     return GS_OK;
 }
 static int export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long* counter);
@@ -948,8 +974,7 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->hot) (void)hipFree(h->hot);
     if (h->hot_cand) (void)hipFree(h->hot_cand);
     if (h->warm) (void)hipFree(h->warm);
-    if (h->rq) (void)hipFree(h->rq);
-    if (h->rcnt) (void)hipFree(h->rcnt);
+    if (h->route_mem) (void)hipFree(h->route_mem);
     if (h->wkeys) (void)hipFree(h->wkeys);
     if (h->wpart) (void)hipFree(h->wpart);
     if (h->wctl) (void)hipFree(h->wctl);
@@ -1001,6 +1026,7 @@ int gs_cc_reset(gs_cc_t* h) {
     h->edges_since_reset = 0;
     h->closes = 0;
     h->ring_launches = 0;
+    ++h->reset_gen;
     return GS_OK;
 }
 
@@ -1313,8 +1339,8 @@ int gs_cc_timing(gs_cc_t* h, int enable) {
     GS_TRY(resolve_timing(h));
     h->timing = enable != 0;
     h->timing_mask = (enable & GS_TIMING_MASK) ? ((uint32_t)enable & 0xFFu) : ~0u;
-    if (h->timing_mask & (1u << GS_K_FOLD)) h->timing_mask |= 1u << GS_K_RING;   // "fold" = both launch kinds
-    for (int k = 0; k < GS_K_COUNT; ++k) { h->total_ms[k] = 0; h->launches[k] = 0; }
+    if (h->timing_mask & (1u << GS_K_FOLD)) h->timing_mask |= (1u << GS_K_RING) | (1u << GS_K_ROUTE);   // "fold" = every launch kind
+    for (int k = 0; k < GS_K_COUNT; ++k) { h->total_ms[k] = 0; h->launches[k] = 0; h->units[k] = 0; }
     return GS_OK;
 }
 
@@ -1325,6 +1351,16 @@ int gs_cc_kernel_time(gs_cc_t* h, int kernel, double* total_ms, uint64_t* launch
     GS_TRY(resolve_timing(h));
     if (total_ms) *total_ms = h->total_ms[kernel];
     if (launches) *launches = h->launches[kernel];
+    return GS_OK;
+}
+
+int gs_cc_kernel_units(gs_cc_t* h, int kernel, uint64_t* units) {
+    GS_TRY(check(h));
+    if (kernel < 0 || kernel >= GS_K_COUNT) return fail(GS_ERR_INVALID, "bad kernel id %d", kernel);
+    if (!units) return fail(GS_ERR_INVALID, "null out");
+    DeviceGuard g(h->device);
+    GS_TRY(resolve_timing(h));
+    *units = h->units[kernel];
     return GS_OK;
 }
 

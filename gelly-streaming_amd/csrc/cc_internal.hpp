@@ -1,0 +1,20 @@
+// cc_internal.hpp — what comm.hip needs of a summary handle (defined in cc_api.hip), declared once.
+#pragma once
+
+#include "common.hpp"
+
+namespace gsgpu {
+struct CcInfo {
+    uint32_t cap;
+    int device;
+    hipStream_t stream;
+    bool marks;              // created with GS_CC_TRACK_MARKS
+    bool sparse;
+    bool marking;            // marking currently on (gs_cc_set_marking)
+    uint64_t reset_gen;      // gs_cc_reset calls so far: a new stream starts when it changes
+};
+int cc_info(gs_cc_t* h, CcInfo* out);
+int cc_export_async(gs_cc_t* h, void* pairs, uint64_t cap, unsigned long long* dcount);
+int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int nslots, int skip, uint64_t cap);
+void cc_count_folded(gs_cc_t* h, uint64_t n);
+}  // namespace gsgpu

@@ -394,7 +394,11 @@ __device__ __forceinline__ void hot_admit(const HotArgs& hot, uint32_t v) {
 // warm: probe the warm set for LDS misses first; count: add the LDS misses found in the giant to
 // the warm build's counters.
 // Raw buffer resource over [p, p + bytes) (gfx9 dword3: 32-bit data format); a lane whose offset
-// is >= bytes (kNoLoad) makes no memory request and reads 0.
+// is >= bytes (kNoLoad) makes no memory request and reads 0. The filter's correctness depends on
+// that out-of-range behaviour, and dword3 is encoded differently on gfx10+: build for gfx9 only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "buffer_rsrc: dword3 0x00020000 is the gfx9 (CDNA) encoding; libgsgpu is built for gfx950"
+#endif
 constexpr uint32_t kNoLoad = 0xFFFFFFFFu;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* p, uint64_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)(bytes < kNoLoad ? bytes : kNoLoad), 0x00020000);
@@ -720,16 +724,16 @@ typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 constexpr uint32_t kFillThreads = 1024;
 // 16-B copy of `words` 32-bit words global -> LDS by the whole workgroup, 8 loads in flight per
 // thread before any store (a load-store loop waits one round trip per step); zero past `avail`
-template <uint32_t WORDS>
+template <uint32_t WORDS, uint32_t THREADS = kFillThreads>
 __device__ __forceinline__ void lds_fill(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, uint64_t avail) {
     constexpr uint32_t kVecs = WORDS / 4;
     const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
     u32x4* d4 = reinterpret_cast<u32x4*>(dst);
-    for (uint32_t v0 = 0; v0 < kVecs; v0 += 8 * kFillThreads) {
+    for (uint32_t v0 = 0; v0 < kVecs; v0 += 8 * THREADS) {
         u32x4 q[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const uint32_t vi = v0 + j * kFillThreads + threadIdx.x;
+            const uint32_t vi = v0 + j * THREADS + threadIdx.x;
             q[j] = (vi < kVecs && 4ull * vi + 4 <= avail) ? s4[vi] : u32x4{0u, 0u, 0u, 0u};
             if (vi < kVecs && 4ull * vi < avail && 4ull * vi + 4 > avail) {       // a partial last vector
                 const uint32_t* w = src + 4ull * vi;
@@ -738,7 +742,7 @@ __device__ __forceinline__ void lds_fill(uint32_t* __restrict__ dst, const uint3
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const uint32_t vi = v0 + j * kFillThreads + threadIdx.x;
+            const uint32_t vi = v0 + j * THREADS + threadIdx.x;
             if (vi < kVecs) d4[vi] = q[j];
         }
     }

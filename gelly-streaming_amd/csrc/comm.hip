@@ -26,21 +26,9 @@
 #include <mutex>
 #include <vector>
 
-#include "common.hpp"
+#include "cc_internal.hpp"
 
 namespace gsgpu {
-// internal accessors of a summary handle (cc_api.hip)
-struct CcInfo {
-    uint32_t cap;
-    int device;
-    hipStream_t stream;
-    bool marks;
-    bool sparse;
-};
-int cc_info(gs_cc_t* h, CcInfo* out);
-int cc_export_async(gs_cc_t* h, void* pairs, uint64_t cap, unsigned long long* dcount);
-int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int nslots, int skip, uint64_t cap);
-void cc_count_folded(gs_cc_t* h, uint64_t n);
 
 namespace {
 
@@ -76,16 +64,25 @@ struct LocalGroup {
         int state = 0;                             // 0 empty, 1 posted, 2 copied
     };
     std::vector<Box> box;
-    void barrier() {
+    bool failed = false;                           // a rank's exchange failed: every wait returns
+    // false when the group has failed (the caller returns GS_ERR_COMM instead of hanging)
+    bool barrier() {
         std::unique_lock<std::mutex> lk(mu);
+        if (failed) return false;
         const uint64_t g = gen;
         if (++arrived == world) {
             arrived = 0;
             ++gen;
             cv.notify_all();
         } else {
-            cv.wait(lk, [&] { return gen != g; });
+            cv.wait(lk, [&] { return gen != g || failed; });
         }
+        return !failed;
+    }
+    void fail_all() {
+        std::lock_guard<std::mutex> lk(mu);
+        failed = true;
+        cv.notify_all();
     }
 };
 
@@ -110,6 +107,10 @@ struct gs_comm {
     unsigned long long* hcnt = nullptr;            // pinned mirror
     bool root_marking_off = false;
     uint64_t spec_slot = 0;                        // allgather: slot size of the speculative round (0: exact)
+    gs_cc_t* bound = nullptr;                      // the one handle and mode this communicator serves
+    int mode = -1;
+    uint64_t reset_gen = 0;                        // the handle's reset generation of the current stream
+    bool broken = false;                           // an exchange failed: the communicator is unusable
     hipEvent_t ev_counts = nullptr;                // the speculative round's counts are on the host
     uint64_t bytes_sent = 0, bytes_recv = 0, exchanges = 0, overflows = 0;
 };
@@ -135,14 +136,14 @@ int allgather(gs_comm_t* c, const void* send, void* recv, size_t bytes, hipStrea
     GS_HIP(hipEventRecord(c->ev_ready, s));
     g.send[c->rank] = send;
     g.ev[c->rank] = c->ev_ready;
-    g.barrier();                                   // every rank's buffer and event published
+    if (!g.barrier()) return fail(GS_ERR_COMM, "in-process group: a peer's exchange failed");   // buffers published
     for (int q = 0; q < c->world; ++q) {
         if (q != c->rank) GS_HIP(hipStreamWaitEvent(s, g.ev[q], 0));
         GS_HIP(hipMemcpyAsync(static_cast<char*>(recv) + (size_t)q * bytes, g.send[q], bytes, hipMemcpyDeviceToDevice, s));
     }
     GS_HIP(hipEventRecord(c->ev_done, s));
     g.done[c->rank] = c->ev_done;
-    g.barrier();                                   // every rank's reads enqueued
+    if (!g.barrier()) return fail(GS_ERR_COMM, "in-process group: a peer's exchange failed");   // reads enqueued
     for (int q = 0; q < c->world; ++q)             // a send buffer is rewritten only after the
         if (q != c->rank) GS_HIP(hipStreamWaitEvent(s, g.done[q], 0));   // peers' reads of it
     return GS_OK;
@@ -162,7 +163,8 @@ int send(gs_comm_t* c, const void* p, size_t bytes, int peer, hipStream_t s) {
     b.ready = c->ev_ready;
     b.state = 1;
     g.cv.notify_all();
-    g.cv.wait(lk, [&] { return b.state == 2; });   // the receiver has enqueued its copy
+    g.cv.wait(lk, [&] { return b.state == 2 || g.failed; });   // the receiver has enqueued its copy
+    if (b.state != 2) return fail(GS_ERR_COMM, "in-process group: a peer's exchange failed");
     b.state = 0;
     const hipEvent_t taken = b.taken;
     lk.unlock();
@@ -179,7 +181,8 @@ int recv(gs_comm_t* c, void* p, size_t bytes, int peer, hipStream_t s) {
     LocalGroup& g = *c->local;
     LocalGroup::Box& b = g.box[(size_t)peer * c->world + c->rank];
     std::unique_lock<std::mutex> lk(g.mu);
-    g.cv.wait(lk, [&] { return b.state == 1; });
+    g.cv.wait(lk, [&] { return b.state == 1 || g.failed; });
+    if (b.state != 1) return fail(GS_ERR_COMM, "in-process group: a peer's exchange failed");
     if (b.bytes != bytes) {
         b.taken = nullptr;
         b.state = 2;
@@ -295,7 +298,7 @@ int exchange_exact(gs_comm_t* c, gs_cc_t* h, const CcInfo& in, uint64_t* maxc) {
         skip[c->rank] = 1;
         GS_TRY(gs_cc_set_marking(h, 0));           // the others' deltas are theirs to export
         const int rc = fold_slots(h, c->recvbuf, m, cnt, skip);
-        GS_TRY(gs_cc_set_marking(h, 1));
+        GS_TRY(gs_cc_set_marking(h, in.marking ? 1 : 0));   // the caller's marking state back
         GS_TRY(rc);
         c->bytes_sent += m * 8 * (P - 1);
         c->bytes_recv += m * 8 * (P - 1);
@@ -372,7 +375,7 @@ int merge_allgather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
         skip[c->rank] = 1;
         GS_TRY(gs_cc_set_marking(h, 0));
         const int rc = fold_slots(h, c->recvbuf, mt, tail, skip);
-        GS_TRY(gs_cc_set_marking(h, 1));
+        GS_TRY(gs_cc_set_marking(h, in.marking ? 1 : 0));
         GS_TRY(rc);
         c->bytes_sent += mt * 8 * (P - 1);
         c->bytes_recv += mt * 8 * (P - 1);
@@ -575,20 +578,58 @@ int gs_comm_info(gs_comm_t* c, int* rank, int* world, uint64_t* bytes_sent, uint
     return GS_OK;
 }
 
-int gs_cc_merge_window(gs_cc_t* h, gs_comm_t* c, int mode) {
-    if (!h || !c) return fail(GS_ERR_INVALID, "gs_cc_merge_window: null argument");
+namespace {
+// A rank that fails inside an exchange would leave its peers blocked in the next collective: tear
+// the communicator down so they fail too (RCCL: ncclCommAbort; in-process: wake every waiter).
+int abort_exchange(gs_comm_t* c, int rc) {
+    const std::string msg = last_error();
+    c->broken = true;
+    if (c->nccl) {
+        (void)ncclCommAbort(c->nccl);
+        c->nccl = nullptr;
+    }
+    if (c->local) c->local->fail_all();
+    last_error() = msg;
+    return rc;
+}
+
+int merge_window(gs_cc_t* h, gs_comm_t* c, int mode) {
     CcInfo in;
     GS_TRY(prepare(c, h, &in));
-    DeviceGuard g(in.device);
-    int rc;
-    switch (mode) {
-    case GS_MERGE_ALLGATHER: rc = merge_allgather(c, h, in); break;
-    case GS_MERGE_GATHER: rc = merge_gather(c, h, in); break;
-    case GS_MERGE_TREE: rc = merge_tree(c, h, in); break;
-    default: return fail(GS_ERR_INVALID, "gs_cc_merge_window: mode %d", mode);
+    // a communicator carries per-stream state (the speculative slot size, rank 0's paused
+    // marking): it serves one handle in one mode; a reset of that handle starts a new stream
+    if (c->bound && (c->bound != h || c->mode != mode))
+        return fail(GS_ERR_INVALID, "gs_cc_merge_window: this communicator serves another handle or mode "
+                                    "(one communicator per summary and mode)");
+    if (!c->bound) { c->bound = h; c->mode = mode; c->reset_gen = in.reset_gen; }
+    if (in.reset_gen != c->reset_gen) {              // the handle was reset: a new stream
+        c->reset_gen = in.reset_gen;
+        c->spec_slot = 0;                            // its first window runs the exact round again
     }
-    if (rc == GS_OK) ++c->exchanges;
-    return rc;
+    DeviceGuard g(in.device);
+    switch (mode) {
+    case GS_MERGE_ALLGATHER: return merge_allgather(c, h, in);
+    case GS_MERGE_GATHER: return merge_gather(c, h, in);
+    default: return merge_tree(c, h, in);
+    }
+}
+}  // namespace
+
+int gs_cc_merge_window(gs_cc_t* h, gs_comm_t* c, int mode) {
+    if (!c) return fail(GS_ERR_INVALID, "gs_cc_merge_window: null communicator");
+    if (c->broken) return fail(GS_ERR_COMM, "gs_cc_merge_window: the communicator failed in an earlier exchange");
+    int rc;
+    if (!h) rc = fail(GS_ERR_INVALID, "gs_cc_merge_window: null handle");
+    else if (mode != GS_MERGE_ALLGATHER && mode != GS_MERGE_GATHER && mode != GS_MERGE_TREE)
+        rc = fail(GS_ERR_INVALID, "gs_cc_merge_window: mode %d", mode);
+    else rc = merge_window(h, c, mode);
+    if (rc == GS_OK) {
+        ++c->exchanges;
+        return rc;
+    }
+    // any failure on one rank (a bad argument included) fails the whole group: its peers are
+    // (or will be) waiting for this rank in a collective
+    return abort_exchange(c, rc);
 }
 
 }  // extern "C"

@@ -26,7 +26,7 @@ GS_ERR_COMM = -8
 GS_CC_TRACK_MARKS = 1
 GS_CC_SPARSE_IDS = 2
 
-GS_K_FOLD, GS_K_COMPRESS, GS_K_MERGE, GS_K_EXPORT, GS_K_RING = 0, 1, 2, 3, 4
+GS_K_FOLD, GS_K_COMPRESS, GS_K_MERGE, GS_K_EXPORT, GS_K_RING, GS_K_ROUTE = 0, 1, 2, 3, 4, 5
 GS_MERGE_ALLGATHER, GS_MERGE_GATHER, GS_MERGE_TREE = 0, 1, 2
 GS_TIMING_MASK = 0x100
 
@@ -40,7 +40,7 @@ EXPORTED_SYMBOLS = (
     "gs_cc_sync", "gs_cc_fold", "gs_cc_fold_pairs", "gs_cc_merge", "gs_cc_combine",
     "gs_cc_close_window", "gs_cc_stats", "gs_cc_emit_dense", "gs_cc_emit_pairs",
     "gs_cc_checksum", "gs_cc_find", "gs_cc_find_flags", "gs_cc_labels_device", "gs_cc_export_marks",
-    "gs_cc_fold_pairs32", "gs_cc_export_marks_async", "gs_cc_set_marking", "gs_cc_timing", "gs_cc_kernel_time", "gs_gen_rmat", "gs_gen_er", "gs_parse_edges",
+    "gs_cc_fold_pairs32", "gs_cc_export_marks_async", "gs_cc_set_marking", "gs_cc_timing", "gs_cc_kernel_time", "gs_cc_kernel_units", "gs_gen_rmat", "gs_gen_er", "gs_parse_edges",
     "gs_bip_create", "gs_bip_destroy", "gs_bip_reset", "gs_bip_set_stream", "gs_bip_sync", "gs_bip_fold",
     "gs_bip_fold_pairs", "gs_bip_merge", "gs_bip_close_window", "gs_bip_status", "gs_bip_checksum",
     "gs_bip_emit_pairs",
@@ -48,6 +48,22 @@ EXPORTED_SYMBOLS = (
     "gs_cc_merge_window",
     "gs_last_error", "gs_version",
 )
+
+
+def lib_source_sha() -> str:
+    """sha256 over the library's kernel and boundary sources (csrc/*.hip, csrc/*.hpp, the header):
+    committed profiles carry it, so a number measured on other kernels is recognised as stale."""
+    import glob
+    import hashlib
+    pkg = os.path.dirname(HERE)
+    files = sorted(glob.glob(os.path.join(pkg, "csrc", "*.hip")) + glob.glob(os.path.join(pkg, "csrc", "*.hpp")))
+    files.append(os.path.join(os.path.dirname(pkg), "include", "gsgpu.h"))
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 class GsgpuUnavailable(RuntimeError):
@@ -116,6 +132,7 @@ def lib() -> ctypes.CDLL:
         "gs_cc_export_marks": [vp, vp, u64, P(u64)],
         "gs_cc_timing": [vp, i32],
         "gs_cc_kernel_time": [vp, i32, P(ctypes.c_double), P(u64)],
+        "gs_cc_kernel_units": [vp, i32, P(u64)],
         "gs_gen_rmat": [vp, vp, u32, u64, u64, i32, u64, u32, u32, u32, i32, vp],
         "gs_gen_er": [vp, vp, u32, u64, u64, u64, u64, vp],
         "gs_parse_edges": [vp, u64, u32, vp, vp, u64, P(u64), i32, vp],

@@ -122,11 +122,12 @@ class Candidates:
         return True, v, k, s
 
     def restore(self, success, vertices, keys, signs) -> None:
-        """This summary becomes the snapshotted one: reset, then one parity edge per vertex.
-        A vertex signed false (other side than its key, which is signed true) gets the edge
-        (v, key); a vertex signed true other than the key gets an edge to a false-signed vertex
-        of its component (a connected bipartite component with two true-signed vertices has
-        one); a lone key gets its self-loop (edgeToCandidate(v, v) adds it). A failed snapshot
+        """This summary becomes the snapshotted one: reset, then one parity edge per vertex,
+        relative to its component key's own sign (reversed merges can leave a key signed false,
+        Candidates.java:155-182): a vertex signed differently from its key gets the edge
+        (v, key); a vertex signed like its key (other than the key) gets an edge to a vertex of
+        its component signed the other way (a connected bipartite component of several vertices
+        has one); a lone key gets its self-loop (edgeToCandidate(v, v) adds it). A failed snapshot
         is restored as failed (Candidates.fail(): empty map) by an odd cycle on ids 0..2."""
         self.reset()
         if not success:
@@ -141,18 +142,24 @@ class Candidates:
             raise ValueError("restore: vertices, keys and signs differ in length")
         if v.size == 0:
             return
-        neg = {}                                   # component key -> one false-signed vertex
+        ksign = {}                                 # component key -> the key vertex's own sign
         for a, b, c in zip(v.tolist(), k.tolist(), s.tolist()):
-            if not c:
-                neg.setdefault(b, a)
+            if a == b:
+                ksign[b] = c
+        other = {}                                 # component key -> one vertex signed unlike the key
+        for a, b, c in zip(v.tolist(), k.tolist(), s.tolist()):
+            if b not in ksign:
+                raise ValueError("restore: component key %d is not among the vertices" % b)
+            if c != ksign[b]:
+                other.setdefault(b, a)
         src, dst = [], []
         for a, b, c in zip(v.tolist(), k.tolist(), s.tolist()):
-            if not c:
+            if c != ksign[b]:
                 src.append(a); dst.append(b)
             elif a != b:
-                if b not in neg:
-                    raise ValueError("restore: component %d has two true-signed vertices and no false one" % b)
-                src.append(a); dst.append(neg[b])
+                if b not in other:
+                    raise ValueError("restore: component %d has vertices on one side only" % b)
+                src.append(a); dst.append(other[b])
             else:
                 src.append(a); dst.append(a)
         self.fold(np.array(src, dtype=np.int64), np.array(dst, dtype=np.int64))

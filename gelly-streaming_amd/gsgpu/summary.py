@@ -286,11 +286,19 @@ class DisjointSet:
         call("gs_cc_kernel_time", self.handle, int(kernel), ctypes.byref(ms), ctypes.byref(n))
         return float(ms.value), int(n.value)
 
+    def kernel_units(self, kernel: int) -> int:
+        """Edges (folds, merges) or vertices (closes) the timed launches of that class processed."""
+        u = U64()
+        call("gs_cc_kernel_units", self.handle, int(kernel), ctypes.byref(u))
+        return int(u.value)
+
     def fold_time(self) -> Tuple[float, int]:
-        """(ms, launches) of every UpdateCC launch: k_fold (young / plain) + k_fold_ring (steady)."""
+        """(ms, launches) of every UpdateCC launch: k_fold (young / plain) + the steady folds
+        (k_fold_ring, or the routed fold's four launches timed as one)."""
         a, na = self.kernel_time(_abi.GS_K_FOLD)
         b, nb = self.kernel_time(_abi.GS_K_RING)
-        return a + b, na + nb
+        c, nc = self.kernel_time(_abi.GS_K_ROUTE)
+        return a + b + c, na + nb + nc
 
 
 def combine_cc(s1: DisjointSet, s2: DisjointSet) -> DisjointSet:

@@ -178,13 +178,17 @@ int gs_cc_merge_window(gs_cc_t* h, gs_comm_t* comm, int mode);
 
 /* ---- instrumentation ----
  * kernel ids: 0 fold (young-forest / plain k_fold launches), 1 compress (close_window), 2 merge,
- * 3 export, 4 ring (the steady k_fold_ring launches; fold time = 0 + 4). */
-enum { GS_K_FOLD = 0, GS_K_COMPRESS = 1, GS_K_MERGE = 2, GS_K_EXPORT = 3, GS_K_RING = 4, GS_K_COUNT = 5 };
+ * 3 export, 4 ring (the steady k_fold_ring launches), 5 route (the routed steady fold's four
+ * launches k_sift + k_probe x 2 + k_union_surv, timed as one); fold time = 0 + 4 + 5. */
+enum { GS_K_FOLD = 0, GS_K_COMPRESS = 1, GS_K_MERGE = 2, GS_K_EXPORT = 3, GS_K_RING = 4, GS_K_ROUTE = 5, GS_K_COUNT = 6 };
 /* enable = 0: off; 1: every kernel; GS_TIMING_MASK | (1 << GS_K_x) | ...: only those kernels
  * carry timing events (a timed launch costs ~3 us more dispatch time). Totals reset. */
 enum { GS_TIMING_MASK = 0x100 };
 int gs_cc_timing(gs_cc_t* h, int enable);
 int gs_cc_kernel_time(gs_cc_t* h, int kernel, double* total_ms, uint64_t* launches);
+/* units the timed launches of that class processed since gs_cc_timing: edges for folds and merges
+ * (what each launch actually folded, after the library's internal cuts), vertex capacity per close */
+int gs_cc_kernel_units(gs_cc_t* h, int kernel, uint64_t* units);
 
 /* ---- synthetic streams on the device (definition: oracle/gen.c header) ----
  * Write ids [first, first+n) of the stream into src/dst (device pointers, id_bits wide). */

@@ -95,6 +95,13 @@ int gso_cc_run_from(const int64_t* init_v, const int64_t* init_l, uint64_t n_ini
                     uint64_t* out_checksums, int64_t* out_labels, int64_t* final_labels,
                     gso_run_stats* stats);
 
+/* As gso_cc_run_from, also writing the per-window emission's (vertices, components) into
+ * out_counts[2w], out_counts[2w+1] (GSO_EMIT_CHECKSUM / GSO_EMIT_DENSE; optional). */
+int gso_cc_run_counts(const int64_t* init_v, const int64_t* init_l, uint64_t n_init,
+                      const int64_t* src, const int64_t* dst, uint64_t n, const gso_run_cfg* cfg,
+                      uint64_t* out_checksums, uint64_t* out_counts, int64_t* out_labels, int64_t* final_labels,
+                      gso_run_stats* stats);
+
 /* ---------------- deterministic synthetic streams (same definition as the device generators) ---------------- */
 uint64_t gso_splitmix64(uint64_t x);
 /* RMAT: vertex space 2^scale; a,b,c as 32-bit integer thresholds (probability * 2^32, cumulative

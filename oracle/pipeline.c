@@ -64,13 +64,21 @@ static uint64_t flatten_set(gso_ds* ds) {
 int gso_cc_run(const int64_t* src, const int64_t* dst, uint64_t n, const gso_run_cfg* cfg,
                uint64_t* out_checksums, int64_t* out_labels, int64_t* final_labels,
                gso_run_stats* stats) {
-    return gso_cc_run_from(NULL, NULL, 0, src, dst, n, cfg, out_checksums, out_labels, final_labels, stats);
+    return gso_cc_run_counts(NULL, NULL, 0, src, dst, n, cfg, out_checksums, NULL, out_labels, final_labels, stats);
 }
 
 int gso_cc_run_from(const int64_t* init_v, const int64_t* init_l, uint64_t n_init,
                     const int64_t* src, const int64_t* dst, uint64_t n, const gso_run_cfg* cfg,
                     uint64_t* out_checksums, int64_t* out_labels, int64_t* final_labels,
                     gso_run_stats* stats) {
+    return gso_cc_run_counts(init_v, init_l, n_init, src, dst, n, cfg, out_checksums, NULL, out_labels, final_labels,
+                             stats);
+}
+
+int gso_cc_run_counts(const int64_t* init_v, const int64_t* init_l, uint64_t n_init,
+                      const int64_t* src, const int64_t* dst, uint64_t n, const gso_run_cfg* cfg,
+                      uint64_t* out_checksums, uint64_t* out_counts, int64_t* out_labels, int64_t* final_labels,
+                      gso_run_stats* stats) {
     const int P = cfg->partitions > 0 ? cfg->partitions : 1;
     int T = cfg->threads > 0 ? cfg->threads : 1;
     if (T > P) T = P;
@@ -118,11 +126,15 @@ int gso_cc_run_from(const int64_t* init_v, const int64_t* init_l, uint64_t n_ini
         switch (cfg->emit_mode) {
         case GSO_EMIT_FLATTEN: sink += flatten_set(summary); break;
         case GSO_EMIT_CHECKSUM:
-            if (out_checksums) out_checksums[w] = gso_ds_canonical_checksum(summary, NULL, NULL);
+            if (out_checksums)
+                out_checksums[w] = gso_ds_canonical_checksum(summary, out_counts ? &out_counts[2 * w] : NULL,
+                                                             out_counts ? &out_counts[2 * w + 1] : NULL);
             break;
         case GSO_EMIT_DENSE:
             if (out_labels) gso_ds_canonical_dense(summary, out_labels + w * cfg->label_cap, cfg->label_cap);
-            if (out_checksums) out_checksums[w] = gso_ds_canonical_checksum(summary, NULL, NULL);
+            if (out_checksums)
+                out_checksums[w] = gso_ds_canonical_checksum(summary, out_counts ? &out_counts[2 * w] : NULL,
+                                                             out_counts ? &out_counts[2 * w + 1] : NULL);
             break;
         default: break;
         }

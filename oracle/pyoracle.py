@@ -232,6 +232,9 @@ class COracle:
         L.gso_cc_run_from.argtypes = [vp, vp, u64, vp, vp, u64, ctypes.POINTER(_RunCfg), vp, vp, vp,
                                       ctypes.POINTER(_RunStats)]
         L.gso_cc_run_from.restype = i32
+        L.gso_cc_run_counts.argtypes = [vp, vp, u64, vp, vp, u64, ctypes.POINTER(_RunCfg), vp, vp, vp, vp,
+                                        ctypes.POINTER(_RunStats)]
+        L.gso_cc_run_counts.restype = i32
         L.gso_gen_rmat.argtypes = [vp, vp, u64, u64, i32, u64, u32, u32, u32, i32]
         L.gso_gen_er.argtypes = [vp, vp, u64, u64, u64, u64]
         L.gso_splitmix64.argtypes = [u64]; L.gso_splitmix64.restype = u64
@@ -267,19 +270,18 @@ class COracle:
         cfg = _RunCfg(window_edges, partitions, threads, emit, label_cap)
         st = _RunStats()
         sums = np.zeros(max(nwin, 1), dtype=np.uint64)
+        counts = np.zeros((max(nwin, 1), 2), dtype=np.uint64)     # per window: (vertices, components)
         labels = np.empty((max(nwin, 1), label_cap), dtype=np.int64) if emit == EMIT_DENSE else None
         final = np.empty(label_cap, dtype=np.int64) if (want_final and label_cap) else None
+        iv = il = None
         if init is not None and len(init[0]):
             iv = np.ascontiguousarray(init[0], dtype=np.int64)
             il = np.ascontiguousarray(init[1], dtype=np.int64)
-            rc = self.L.gso_cc_run_from(_p(iv), _p(il), int(iv.size), _p(src), _p(dst), n, ctypes.byref(cfg),
-                                        _p(sums), _p(labels), _p(final), ctypes.byref(st))
-        else:
-            rc = self.L.gso_cc_run(_p(src), _p(dst), n, ctypes.byref(cfg), _p(sums), _p(labels),
-                                   _p(final), ctypes.byref(st))
+        rc = self.L.gso_cc_run_counts(_p(iv), _p(il), 0 if iv is None else int(iv.size), _p(src), _p(dst), n,
+                                      ctypes.byref(cfg), _p(sums), _p(counts), _p(labels), _p(final), ctypes.byref(st))
         if rc != 0:
             raise RuntimeError("gso_cc_run failed: %d" % rc)
-        return {"windows": int(st.windows), "checksums": sums[:nwin], "labels": labels,
+        return {"windows": int(st.windows), "checksums": sums[:nwin], "counts": counts[:nwin], "labels": labels,
                 "final": final, "final_vertices": int(st.final_vertices),
                 "final_components": int(st.final_components), "seconds": float(st.seconds)}
 
@@ -295,7 +297,7 @@ def coracle() -> COracle:
 
 
 # --------------------------------------------------------------------------------------------
-# CPU model of one rank's summary in the multi-GPU tree exchange (gsgpu/tree.py), for the
+# CPU model of one rank's summary in the multi-GPU tree exchange (tests/gloo_tree.py), for the
 # gloo tests: min-root hooking union-find over a dense parent array with per-vertex marks of
 # the roots hooked / singletons created since the last export — the same contract as
 # gs_cc_export_marks / gs_cc_fold_pairs32 (include/gsgpu.h). Pure restatement, no GPU.

@@ -12,6 +12,13 @@ import os
 import sys
 from collections import defaultdict
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gelly-streaming_amd"))
+from gsgpu._abi import lib_source_sha  # noqa: E402
+
+ROUTED = ("k_sift", "k_probe", "k_union_surv")
+ROUTE_NAME = "routed fold (k_sift + k_probe<B> + k_probe<C> + k_union_surv)"
+
 
 def load(passdir):
     files = glob.glob(os.path.join(passdir, "**", "*counter_collection.csv"), recursive=True)
@@ -33,7 +40,7 @@ def fold_sequence(passdir):
     for f in files:
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"].split("(")[0].replace("void ", "")
-            if "k_fold" not in k:
+            if "k_fold" not in k and "k_sift" not in k:
                 continue
             d = int(r.get("Dispatch_Id") or r.get("Correlation_Id"))
             per[d][r["Counter_Name"]] += float(r["Counter_Value"])
@@ -98,7 +105,7 @@ def main():
             ncalls[k] = len(c[k])
     comp = [k for k in agg if "k_compress" in k]
     windows = ncalls[comp[0]] if comp else 1
-    fold = [k for k in agg if "k_fold" in k or k.endswith("k_bin")]
+    fold = [k for k in agg if "k_fold" in k or any(r in k for r in ROUTED)]
     out = {"windows": windows, "kernels": {}}
     for k in agg:
         out["kernels"][k] = dict(agg[k], dispatches=ncalls.get(k))
@@ -112,13 +119,39 @@ def main():
         "l2_hit_rate": hit / (hit + miss) if hit + miss else None,
         "atomic_requests_per_window": sum(agg[k].get("TCC_EA0_ATOMIC_sum", 0.0) for k in fold) / windows,
     }
+    edges_per_launch = None
     try:
         b = json.load(open(os.path.join(root, "..", "bench.json")))
         out["window_edges"] = b["config"]["window_edges_per_gpu"]
         out["scale"] = b["config"]["scale"]
         out["id_bits"] = b["config"].get("id_bits", 32)
+        edges_per_launch = b["roofline"].get("edges_per_launch")
     except Exception:
         pass
+    out["lib_source_sha"] = lib_source_sha()
+    # the steady fold per launch (what bench.py's roofline.traffic / requests report): the routed
+    # fold's four kernels per k_sift dispatch, or k_fold_ring
+    routed = [k for k in agg if any(r in k for r in ROUTED)]
+    ring = [k for k in agg if "k_fold_ring" in k]
+    ks, name = (routed, ROUTE_NAME) if routed else (ring, "k_fold_ring")
+    if ks:
+        nl = max(ncalls.get([k for k in ks if "k_sift" in k or "k_fold_ring" in k][0]) or 1, 1)
+        f_ = sum(agg[k].get("FETCH_SIZE", 0.0) for k in ks) * 1024 / nl
+        w_ = sum(agg[k].get("WRITE_SIZE", 0.0) for k in ks) * 1024 / nl
+        h_ = sum(agg[k].get("TCC_HIT_sum", 0.0) for k in ks)
+        m_ = sum(agg[k].get("TCC_MISS_sum", 0.0) for k in ks)
+        e_b = 8 * (edges_per_launch or 0) * (2 if out.get("id_bits", 32) == 64 else 1)
+        out["steady"] = {
+            "kernel": name, "kernels": ks, "launches": nl, "edges_per_launch": edges_per_launch,
+            "fetch_bytes_raw_per_launch": f_, "write_bytes_per_launch": w_,
+            # gfx950: FETCH_SIZE reports half the bytes of wide (16 B/lane) streaming reads — the
+            # edge stream (MI355X_MICROARCH.md, HBM section): that half is added back; list reads and
+            # random gathers are counted raw (uncalibrated widths)
+            "hbm_bytes_per_launch": f_ + e_b / 2 + w_,
+            "l2_hit_rate": h_ / (h_ + m_) if h_ + m_ else None,
+            "tcc_requests_per_launch": (h_ + m_) / nl,
+            "memory_side_atomics_per_launch": sum(agg[k].get("TCC_EA0_ATOMIC_sum", 0.0) for k in ks) / nl,
+        }
     # the dominant kernel alone, per launch (what bench.py's roofline.traffic reports): k_fold_ring
     ring = [k for k in agg if "k_fold_ring" in k]
     if ring:

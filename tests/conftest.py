@@ -9,7 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # In-process tests run the library's production defaults. Fold variants (the ring fold and warm
 # set at small sizes, forced young splits, ...) are named subprocess cases in
 # tests/test_gpu_variants.py: the library reads its debug variables once per process.
-for p in (ROOT, os.path.join(ROOT, "gelly-streaming_amd"), os.path.join(ROOT, "oracle")):
+for p in (ROOT, os.path.join(ROOT, "gelly-streaming_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 

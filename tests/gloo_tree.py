@@ -1,4 +1,8 @@
-"""Multi-GPU CombineCC: per-window exchange of per-rank partial summaries.
+"""TEST MODEL (not the product): the multi-GPU CombineCC exchanges restated over torch.distributed,
+so the exchange logic runs multi-process under gloo on CPU (tests/test_tree_gloo.py) and bench.py's
+--dist-backend gloo test mode can put several ranks on one GPU. The product exchange is
+gelly-streaming_amd/csrc/comm.hip (gs_cc_merge_window over RCCL), the same three modes with the same
+delta contract.
 
 Three exchanges behind one contract (``merge_window()`` after each window's fold; True on the
 rank that emitted):
@@ -66,7 +70,9 @@ class TreeMerge:
         self.world = dist.get_world_size(group)
         self.device = device
         self.schedule = tree_schedule(self.rank, self.world)
-        self.cap = int(capacity_pairs)
+        # an export holds at most 2 x capacity pairs (a vertex's self-loop first touch and its hook:
+        # include/gsgpu.h gs_cc_export_marks_async)
+        self.cap = 2 * int(capacity_pairs)
         needs_buf = any(r != "idle" for r, _ in self.schedule)
         self.buf = torch.empty(2 * self.cap if needs_buf else 2, dtype=torch.int32, device=device)
         self.cnt = torch.zeros(1, dtype=torch.int64, device=device)
@@ -147,12 +153,14 @@ class GatherMerge:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.device = torch.device(device)
-        self.cap = int(capacity_pairs)
+        # an export holds at most 2 x capacity pairs; rank 0 receives up to (P - 1) exports
+        self.cap = 2 * int(capacity_pairs)
+        self.total_cap = self.cap * max(self.world - 1, 1)
         self.stage = (dist.get_backend(group) == "gloo" and self.device.type == "cuda")
         if self.rank == 0:
             self.cnts = torch.zeros(max(self.world - 1, 1), dtype=torch.int64,
                                     device="cpu" if self.stage else self.device)
-            self.buf = torch.empty(2 * max(self.cap, 1), dtype=torch.int32, device=self.device)
+            self.buf = torch.empty(2 * max(self.cap, 1), dtype=torch.int32, device=self.device)   # grows
             self.hbuf = torch.empty(0, dtype=torch.int32).pin_memory() if self.stage else None
             self.side = torch.cuda.Stream(self.device) if self.device.type == "cuda" and not self.stage else None
             self.free_ev = None            # recorded after the last fold out of self.buf
@@ -215,9 +223,13 @@ class GatherMerge:
         self._cnt_works = None
         counts = [int(x) for x in self.cnts.tolist()]
         total = sum(counts)
-        if total > self.cap:
-            raise RuntimeError("partial summaries of %d pairs exceed capacity %d" % (total, self.cap))
+        if max(counts) > self.cap:
+            raise RuntimeError("a partial summary of %d pairs exceeds capacity %d" % (max(counts), self.cap))
         if total:
+            if self.buf.numel() < 2 * total:
+                if self.free_ev is not None:
+                    self.free_ev.synchronize()
+                self.buf = torch.empty(2 * total, dtype=torch.int32, device=self.device)
             dst = self.buf
             if self.stage:
                 if self.hbuf.numel() < 2 * total:

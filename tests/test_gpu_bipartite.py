@@ -133,3 +133,16 @@ def test_checkpoint_resume(mode, odd_at):
     op2.restoreState(state)
     got = [c.toString() for c in SimpleEdgeStream(s[k * W:], d[k * W:]).aggregate(op2)]
     assert got == want[k:]
+
+
+def test_restore_with_key_signed_false():
+    """A snapshot whose component key is signed false (reversed Candidates.merge can leave it so,
+    Candidates.java:155-182): the restore reads each vertex's side relative to the key's own sign
+    (ADVICE r02). 1 and 3 share a side, 2 is on the other."""
+    c = Candidates(16, id_bits=32)
+    c.restore(True, np.array([1, 2, 3]), np.array([1, 1, 1]), np.array([False, True, False]))
+    assert c.toString() == "(true,{1={1=(1,true), 2=(2,false), 3=(3,true)}})"
+    c.fold(np.array([2]), np.array([5]))                     # 5 joins on 1's side: still bipartite
+    assert c.toString() == "(true,{1={1=(1,true), 2=(2,false), 3=(3,true), 5=(5,true)}})"
+    c.fold(np.array([1]), np.array([3]))                     # same side: an odd cycle
+    assert c.toString() == "(false,{})"

@@ -138,15 +138,99 @@ def test_local_group_speculative_slot_overflow(oracle, world):
 
 
 def test_merge_window_errors():
+    """Argument errors fail the call AND the communicator (its peers would otherwise wait forever in
+    the next collective): a later call on it returns GS_ERR_COMM."""
     comms = Comm.local_group(1, 0)
     ds = DisjointSet(64, id_bits=32)                  # no marks tracked
     with pytest.raises(gsgpu.GsError) as e:
         ds.merge_window(comms[0])
     assert e.value.code == gsgpu._abi.GS_ERR_UNSUPPORTED
     ds2 = DisjointSet(64, id_bits=32, track_marks=True)
-    with pytest.raises(gsgpu.GsError):
+    with pytest.raises(gsgpu.GsError) as e:
+        ds2.merge_window(comms[0], "tree")
+    assert e.value.code == gsgpu._abi.GS_ERR_COMM     # broken by the first failure
+    comms[0].close()
+    comms = Comm.local_group(1, 0)
+    with pytest.raises(gsgpu.GsError) as e:
         gsgpu._abi.call("gs_cc_merge_window", ds2.handle, comms[0].handle, 7)
+    assert e.value.code == gsgpu._abi.GS_ERR_INVALID
+    comms[0].close()
+    comms = Comm.local_group(1, 0)
     ds2.fold(np.array([1, 2]), np.array([2, 3]))
     ds2.merge_window(comms[0], "tree")                # world 1: a plain close
     assert ds2.getMatches() == {1: 1, 2: 1, 3: 1}
+    with pytest.raises(gsgpu.GsError) as e:           # one communicator serves one handle and mode
+        ds2.merge_window(comms[0], "gather")
+    assert e.value.code == gsgpu._abi.GS_ERR_INVALID
     comms[0].close()
+
+
+def test_failure_on_one_rank_fails_its_peers():
+    """Rank 1 fails before its first collective (its handle tracks no marks); rank 0, already in
+    the all-gather, must get an error instead of hanging."""
+    comms = Comm.local_group(2, 0)
+    errs = [None, None]
+
+    def rank(r):
+        try:
+            ds = DisjointSet(1 << 10, id_bits=32, track_marks=(r == 0))
+            ds.fold(np.array([1, 2]), np.array([2, 3]))
+            ds.merge_window(comms[r], "allgather")
+        except gsgpu.GsError as e:
+            errs[r] = e.code
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+    assert not any(t.is_alive() for t in th), "a rank hung"
+    assert errs[1] == gsgpu._abi.GS_ERR_UNSUPPORTED and errs[0] == gsgpu._abi.GS_ERR_COMM, errs
+    for c in comms:
+        c.close()
+
+
+def test_reset_restarts_the_exact_round(oracle):
+    """After gs_cc_reset the first window of the new stream runs the exact round again (ADVICE r02:
+    the speculative slot used to survive the reset, so every step's young first window overflowed):
+    two identical passes take identical decisions, so the overflow count exactly doubles."""
+    import torch
+    s, d, cap = _stream(oracle, n=200000, seed=5)
+    W = 25000
+    world = 2
+    comms = Comm.local_group(world, 0)
+    ts = torch.from_numpy(s.astype(np.int32)).cuda()
+    td = torch.from_numpy(d.astype(np.int32)).cuda()
+    torch.cuda.synchronize()
+    ov = [[None, None] for _ in range(world)]
+    sums = [[] for _ in range(world)]
+    errors = []
+
+    def rank(r):
+        try:
+            ds = DisjointSet(cap, id_bits=32, track_marks=True)
+            for step in range(2):
+                ds.reset()
+                for lo in range(0, s.size, W):
+                    ln = min(W, s.size - lo)
+                    a, b = lo + (ln * r) // world, lo + (ln * (r + 1)) // world
+                    ds.fold(ts[a:b], td[a:b])
+                    ds.merge_window(comms[r], "allgather")
+                    sums[r].append(ds.checksum()[0])
+                ov[r][step] = comms[r].info()[5]
+            ds.close()
+        except Exception as e:
+            errors.append((r, repr(e)))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th) and not errors, errors
+    for c in comms:
+        c.close()
+    want = oracle.run(s, d, W, partitions=world, emit=EMIT_CHECKSUM, label_cap=cap)
+    for r in range(world):
+        assert sums[r] == 2 * [int(x) for x in want["checksums"]]
+        assert ov[r][1] == 2 * ov[r][0], ov

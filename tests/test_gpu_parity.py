@@ -309,10 +309,10 @@ def test_device_generators_match_oracle(oracle, torch_cuda, bits):
 # ---------------- partial-summary exchange (multi-GPU tree protocol, one process) ----------------
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_tree_exchange_single_process(oracle, torch_cuda, world):
-    """Every 'rank' is a handle on this GPU; the tree rounds of gsgpu/tree.py are replayed with
+    """Every 'rank' is a handle on this GPU; the tree rounds of tests/gloo_tree.py are replayed with
     device buffers handed across directly (what RCCL send/recv does between GPUs)."""
     torch = torch_cuda
-    from gsgpu.tree import tree_schedule
+    from gloo_tree import tree_schedule
     scale, n, W = 13, 200000, 20000
     cap = 1 << scale
     s, d = oracle.gen_rmat(0, n, scale, 8)
@@ -351,7 +351,7 @@ def test_replicated_exchange_single_process(oracle, torch_cuda, world, slots):
     slice, exports its delta asynchronously (count in device memory), folds every other rank's
     delta with marking paused, closes; EVERY replica's emission must equal the oracle's."""
     torch = torch_cuda
-    from gsgpu.tree import fold_deltas, fold_slots
+    from gloo_tree import fold_deltas, fold_slots
     scale, n, W = 13, 200000, 20000
     cap = 1 << scale
     s, d = oracle.gen_rmat(0, n, scale, 9)

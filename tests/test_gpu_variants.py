@@ -1,11 +1,14 @@
 """GPU parity of the production fold selection and of each named fold variant, one subprocess per
 configuration (the library reads its debug variables once per process; csrc/cc_api.hip).
 
-* test_headline_config_production: RMAT-26 EF16, 2^24-edge windows, production defaults — windows
-  1..6 bit-exact vs the C oracle, final labels vs an independent torch CC (tests/headline_check.py).
+* test_headline_config_production: RMAT-26 EF16, 2^24-edge windows, production defaults — all 64
+  windows bit-exact vs the C oracle's fixture (tests/golden/headline_rmat26.json), two back-to-back
+  passes with reset, final labels vs an independent torch CC (tests/headline_check.py); the same
+  with the reference's Long (int64) ids.
 * test_headline_config_eight_ranks_one_gpu: the same stream as BASELINE config 3's 8-GPU strong
   layout (2^24-edge global windows, 2^21 edges per rank), 8 ranks through the C-ABI exchange on
-  one GPU (tests/headline_ranks_check.py).
+  one GPU in allgather, gather and tree modes, all 64 windows vs the fixture
+  (tests/headline_ranks_check.py).
 * test_variant_parity: every golden stream, RMAT-21, ER-21 and the giant-switch stream, per window
   vs the C oracle, under production defaults and under each forced variant (tests/variant_check.py).
 * test_fold_variants_verified: bench.py --verify (RMAT-22, 2^20-edge windows) under each variant.
@@ -33,24 +36,28 @@ def _last_json(out: bytes):
     return json.loads([l for l in out.decode().splitlines() if l.startswith("{")][-1])
 
 
-def test_headline_config_production():
-    out = subprocess.check_output([sys.executable, os.path.join(HERE, "headline_check.py")], env=_env({}), timeout=900)
+@pytest.mark.parametrize("args", [["--steps", "2"], ["--id-bits", "64", "--no-torch"]], ids=["int32_two_passes", "int64"])
+def test_headline_config_production(args):
+    out = subprocess.check_output([sys.executable, os.path.join(HERE, "headline_check.py")] + args, env=_env({}),
+                                  timeout=900)
     r = _last_json(out)
     print(r)
-    assert r["oracle_checksums_equal"], r
-    assert r["final_equals_torch_cc"] and r["labels_minimal_idempotent"], r
+    assert r["fixture_windows_equal"], r
+    assert r["final_equals_torch_cc"] is not False and r["labels_minimal_idempotent"], r
     assert r["ok"], r
 
 
-def test_headline_config_eight_ranks_one_gpu():
+@pytest.mark.parametrize("mode", ["allgather", "gather", "tree"])
+def test_headline_config_eight_ranks_one_gpu(mode):
     """BASELINE config 3's 8-rank strong layout at full scale through the C-ABI exchange
-    (in-process transport): per-window checksums vs the oracle, replicas equal, final vs torch CC."""
-    out = subprocess.check_output([sys.executable, os.path.join(HERE, "headline_ranks_check.py")], env=_env({}),
+    (in-process transport): every window's emission vs the fixture, replicas equal, final vs torch CC."""
+    args = ["--mode", mode] + ([] if mode == "allgather" else ["--no-torch"])
+    out = subprocess.check_output([sys.executable, os.path.join(HERE, "headline_ranks_check.py")] + args, env=_env({}),
                                   timeout=900)
     r = _last_json(out)
     print(r)
     assert not r["hung"] and not r["errors"], r
-    assert r["oracle_checksums_equal"] and r["replicas_equal"] and r["final_equals_torch_cc"], r
+    assert r["fixture_windows_equal"] and r["replicas_equal"] and r["final_equals_torch_cc"] is not False, r
 
 
 VARIANTS = {
@@ -60,6 +67,8 @@ VARIANTS = {
     "ring_warm_stats": {"GSGPU_RING_MIN_BITS": "20", "GSGPU_FOLD_STATS": "1"},
     "ring_forced_no_warm": {"GSGPU_FOLD_MODE": "ring"},
     "plain_forced": {"GSGPU_FOLD_MODE": "plain", "GSGPU_RING_MIN_BITS": "20"},
+    "route_forced": {"GSGPU_FOLD_MODE": "route"},
+    "route_forced_no_split": {"GSGPU_FOLD_MODE": "route", "GSGPU_YOUNG_SPLIT": "0"},
     "young_split_2^18": {"GSGPU_YOUNG_SPLIT": str(1 << 18)},
 }
 
@@ -73,7 +82,8 @@ def test_variant_parity(name):
     assert r["ok"] and not bad, bad
 
 
-@pytest.mark.parametrize("name", ["production", "ring_warm_split_from_2^20", "plain_forced", "ring_warm_stats"])
+@pytest.mark.parametrize("name", ["production", "ring_warm_split_from_2^20", "plain_forced", "ring_warm_stats",
+                                  "route_forced"])
 def test_fold_variants_verified(name):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0", "--scale", "22",
            "--edge-factor", "16", "--window-log2", "20", "--no-cpu-baseline", "--verify"]

@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from gsgpu.aggregation import SimpleEdgeStream
-from gsgpu.tree import tree_schedule
+from gloo_tree import tree_schedule
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 

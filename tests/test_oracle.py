@@ -216,3 +216,17 @@ def test_oracle_under_host_sanitizers():
                          timeout=300)
     assert out.returncode == 0, out.stdout.decode() + out.stderr.decode()
     assert b"sanitizer run OK" in out.stdout
+
+
+def test_headline_fixture_window1_live(oracle):
+    """tests/golden/headline_rmat26.json (minted by tests/golden/make_headline.py with P = 8) agrees with
+    a live oracle run of window 1 of the headline stream at another partition count (P = 3): the
+    emission is independent of P, and the fixture is what the checker computes."""
+    fx = json.load(open(os.path.join(GOLD, "headline_rmat26.json")))
+    assert fx["windows"] == 64 and len(fx["checksums"]) == 64
+    assert fx["vertices"] == sorted(fx["vertices"]) and fx["vertices"][-1] <= 1 << fx["scale"]
+    W = fx["window_edges"]
+    s, d = oracle.gen_rmat(0, W, fx["scale"], fx["seed"])
+    r = oracle.run(s, d, W, partitions=3, threads=3, emit=EMIT_CHECKSUM)
+    assert int(r["checksums"][0]) == int(fx["checksums"][0])
+    assert [int(x) for x in r["counts"][0]] == [fx["vertices"][0], fx["components"][0]]

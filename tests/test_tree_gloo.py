@@ -1,4 +1,4 @@
-"""CPU, multi-process: the multi-GPU CombineCC exchanges (gsgpu/tree.py: flat gather, pairwise
+"""CPU, multi-process: the multi-GPU CombineCC exchanges (tests/gloo_tree.py: flat gather, pairwise
 tree, replicated all-pairs delta exchange) under gloo, world 2 and 4.
 
 Each rank folds its contiguous slice of every window into a CPU summary model with the same
@@ -27,8 +27,8 @@ def _free_port():
 def _worker(rank, world, port, src, dst, W, cap, outdir, kind):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path[:0] = [os.path.join(root, "gelly-streaming_amd"), os.path.join(root, "oracle")]
-    from gsgpu.tree import AllgatherMerge, GatherMerge, TreeMerge
+    sys.path[:0] = [os.path.join(root, "gelly-streaming_amd"), os.path.join(root, "oracle"), os.path.join(root, "tests")]
+    from gloo_tree import AllgatherMerge, GatherMerge, TreeMerge
     from pyoracle import PyMarkedSummary
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -71,14 +71,34 @@ def test_tree_merge_gloo_matches_oracle(tmp_path, oracle, world, kind):
         np.testing.assert_array_equal(got, want, err_msg="rank %d" % r)
 
 
+@pytest.mark.parametrize("kind", ["tree", "gather"])
+def test_exports_of_twice_the_capacity(tmp_path, oracle, kind):
+    """A window of self-loops on every vertex that also joins them all: each vertex is exported
+    twice (its self-loop first touch, then its hook), 2 x capacity - 1 pairs per export, which the
+    tree and gather models must carry (they used to reject n > capacity)."""
+    cap = 256
+    v = np.arange(cap, dtype=np.int64)
+    s = np.concatenate([v, v[:-1]])                 # self-loops, then the chain v -- v+1
+    d = np.concatenate([v, v[1:]])
+    # every rank's slice of the one window: self-loops and chain links, so each export is big
+    order = np.argsort(np.concatenate([2 * v, 2 * v[:-1] + 1]), kind="stable")
+    s, d = s[order], d[order]
+    W = len(s)
+    mp.spawn(_worker, args=(2, _free_port(), s, d, W, cap, str(tmp_path), kind), nprocs=2, join=True)
+    from pyoracle import EMIT_DENSE
+    want = oracle.run(s, d, W, partitions=2, emit=EMIT_DENSE, label_cap=cap)["labels"]
+    got = np.load(tmp_path / "emis0.npy")
+    np.testing.assert_array_equal(got, want)
+
+
 @pytest.mark.parametrize("bulk", [False, True])
 def test_fold_slots_covers_real_pairs_only(monkeypatch, bulk):
     """AllgatherMerge's padded slots: every real pair is folded, no empty (garbage) slot is, and
     padding is only ever a copy of its own slot's first pair."""
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path[:0] = [os.path.join(root, "gelly-streaming_amd")]
-    from gsgpu import tree
+    sys.path[:0] = [os.path.join(root, "gelly-streaming_amd"), os.path.join(root, "tests")]
+    import gloo_tree as tree
     if bulk:
         monkeypatch.setattr(tree, "BULK_DELTA_PAIRS", 2)
     m, counts = 4, [3, 0, 4, 1, 0, 2]

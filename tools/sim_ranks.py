@@ -11,10 +11,10 @@ rank over its own link and every rank folds the others' deltas with marking paus
 import os, sys, time
 import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(ROOT, "gelly-streaming_amd")]
+sys.path[:0] = [os.path.join(ROOT, "gelly-streaming_amd"), os.path.join(ROOT, "tests")]
 import gsgpu
 from gsgpu import gen
-from gsgpu.tree import fold_slots, tree_schedule
+from gloo_tree import fold_slots, tree_schedule
 from gsgpu._abi import GS_K_FOLD, GS_K_COMPRESS
 
 P = int(sys.argv[1]) if len(sys.argv) > 1 else 8
