@@ -68,6 +68,10 @@ def parse():
     ap.add_argument("--id-bits", type=int, default=32, choices=[32, 64])
     ap.add_argument("--host-input", action="store_true",
                     help="edges in pinned host memory, folded through gs_cc_fold's staged H2D path")
+    ap.add_argument("--emit-host", action="store_true",
+                    help="per window, the emission's delta (gs_cc_emit_delta: pairs new or changed since the last "
+                         "window) copied to pinned host memory, inside the timed region: what a host-side Merger / "
+                         "FlattenSet consumer costs (SummaryAggregation.java:110-111)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check final labels with an independent torch CC "
                     "(multi-rank: rank 0 regenerates the whole global stream; small scales only)")
@@ -159,6 +163,10 @@ def main():
         cls = {"allgather": AllgatherMerge, "gather": GatherMerge, "tree": TreeMerge}[a.merge]
         tree = cls(ds, capacity_pairs=V, device=dev)
     gather = tree is not None and a.merge == "gather"
+    emitted = [0, 0]                                  # delta pairs copied to the host, windows
+    if a.emit_host:
+        hv = torch.empty(V, dtype=idt).pin_memory()
+        hl = torch.empty(V, dtype=idt).pin_memory()
 
     def window(w, after=None):
         lo = w * W_rank
@@ -171,6 +179,10 @@ def main():
             tree.merge_window()
         else:
             ds.close_window()
+        if a.emit_host:
+            v, _ = ds.delta(hv, hl)
+            emitted[0] += v.numel()
+            emitted[1] += 1
 
     fold_mask = GS_TIMING_MASK | (1 << GS_K_FOLD) | (1 << GS_K_RING) | (1 << GS_K_ROUTE) | \
         ((1 << GS_K_MERGE) | (1 << GS_K_EXPORT) if world > 1 else 0)
@@ -296,7 +308,8 @@ def main():
                 "workload": "%s_%s%d_ef%d_window%s%s%s" % (a.workload.split("_")[0], "er" if a.kind == "er" else "rmat",
                                                          a.scale, a.edge_factor, _pow2(W_glob),
                                                          "_int64" if a.id_bits == 64 else "",
-                                                         "_hostinput" if a.host_input else ""),
+                                                         "_hostinput" if a.host_input else "") +
+                            ("_emithost" if a.emit_host else ""),
                 "scale": a.scale, "vertices": V, "edge_factor": a.edge_factor,
                 "edges_total": E_glob, "edges_per_gpu": E_rank, "window_edges": W_glob,
                 "window_edges_per_gpu": W_rank, "windows": nwin, "id_bits": a.id_bits,
@@ -304,7 +317,9 @@ def main():
                 "parallelism": "1 subtask per GPU x %d, %s" % (
                     world, ("%s merge, %s" % (a.merge, "C ABI over RCCL" if comm is not None else "torch.distributed gloo"))
                     if world > 1 else "no merge"),
-                "emission": "per window, canonical min-id labels resident in HBM",
+                "emission": ("per window, canonical min-id labels resident in HBM, and the delta (pairs new or changed "
+                             "since the last window) copied to pinned host memory (gs_cc_emit_delta)") if a.emit_host
+                            else "per window, canonical min-id labels resident in HBM",
             },
             "roofline": {
                 "bound": "hbm",
@@ -355,6 +370,11 @@ def main():
                 "wall_ms_per_window": elapsed / a.steps / nwin * 1e3,
                 "slot_overflows": overflows,
             }
+        if a.emit_host and emitted[1]:
+            per = emitted[0] / emitted[1]
+            line["emit_host"] = {"delta_pairs_per_window": per,
+                                 "delta_bytes_per_window": per * 2 * (4 if a.id_bits == 32 else 8),
+                                 "windows": emitted[1]}
         if verify is not None:
             line["verify"] = verify
         if latency is not None:

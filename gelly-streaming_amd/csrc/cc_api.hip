@@ -68,6 +68,8 @@ struct gs_cc {
     uint32_t* gbits = nullptr;           // giant-component filter bitmap (1 bit per vertex)
     uint32_t* sbits = nullptr;           // seen bitmap (1 bit per vertex), set on first touch
     uint32_t* cbits = nullptr;           // ring folds: first touches claimed under the giant root
+    uint32_t* dbits = nullptr;           // delta emission: vertices a close may have relabelled since the last delta
+    uint32_t* elab = nullptr;            // delta emission: the labels last emitted (kInvalid: never)
     uint32_t* derr = nullptr;            // derr[0] deferred device error flags; derr[1..5] giant state
     unsigned long long* dscratch = nullptr;  // reduction outputs (8 words)
     unsigned long long* hscratch = nullptr;  // pinned mirror
@@ -255,6 +257,7 @@ struct DebugEnv {
     int fold_mode = kFoldAuto;
     uint32_t ring_min_bits = kRingMinBits;
     uint64_t young_split = ~0ull;                   // ~0: the production rule
+    uint32_t route_exp = 0;                         // GSGPU_ROUTE_EXP: routed-fold timing lab (wrong results)
     DebugEnv() {
         const char* e = getenv("GSGPU_FOLD_STATS");
         fold_stats = e && atoi(e) != 0;
@@ -266,6 +269,8 @@ struct DebugEnv {
         if (e && *e) ring_min_bits = (uint32_t)strtoul(e, nullptr, 0);
         e = getenv("GSGPU_YOUNG_SPLIT");
         if (e && *e) young_split = strtoull(e, nullptr, 0);
+        e = getenv("GSGPU_ROUTE_EXP");
+        if (e && *e) route_exp = (uint32_t)strtoul(e, nullptr, 0);
     }
 };
 static const DebugEnv& dbg() {
@@ -324,6 +329,7 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
 // Steady-state fold (mature forest, aligned device uint32 SoA): k_fold_ring (LDS hot set + warm set
 // + survivor rings, one persistent launch) once gbits outgrows an XCD's L2, else k_fold as for
 // young windows (GSGPU_FOLD_MODE forces either)
+static bool route_eligible(const gs_cc_t* h, uint64_t n);
 static bool use_ring(const gs_cc_t* h) {
     const int m = dbg().fold_mode;
     return m == kFoldRing || (m == kFoldAuto && h->hot_bits >= dbg().ring_min_bits);
@@ -368,7 +374,8 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     // kWarmAt after reset and every kWarmEvery-th after it, each time only if the set is not valid
     // for the current giant (device-gated)
     const uint64_t launch_no = h->ring_launches - 1;
-    const bool build = h->warm && launch_no >= kWarmAt && (launch_no - kWarmAt) % kWarmEvery == 0;
+    // (no warm set where the routed fold takes over: its filter never probes it)
+    const bool build = h->warm && launch_no >= kWarmAt && (launch_no - kWarmAt) % kWarmEvery == 0 && !route_eligible(h, n);
     hot.warm = h->warm;
     hot.warm_bits = h->warm_bits;
     hot.warm_valid = h->derr + 7;
@@ -393,20 +400,20 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     if (build) launch_warm_build(h, t.stop());
 }
 
-// Routed steady fold (route.hpp): the giant filter out of LDS slices of gbits, for ids of 2^25..2^26
-// (gbits past an XCD's L2, at most kRouteMaxParts parts of 2^20 ids), on windows of at least
-// kRouteMinEdges edges (below that the per-launch slice fills and list scans cost more than the
-// ring fold's lookups). GSGPU_FOLD_MODE=route forces it wherever the ids fit (tests at small sizes).
-constexpr uint64_t kRouteMinEdges = 1ull << 22;
-static bool use_route(const gs_cc_t* h, uint64_t n) {
+// Routed steady fold (route.hpp): the giant filter out of LDS slices of gbits, for ids of up to 2^26
+// (at most kRouteMaxParts parts of 2^20 ids). NOT the production fold: on RMAT-26 2^24-edge windows
+// it measured 227 us per steady window (k_sift 98 + k_probe<B> 69 + k_probe<C> 26 + k_union_surv
+// 33) against k_fold_ring's 199 us on the same box (profiles/r03_f_ab.txt); it stays as the variant
+// GSGPU_FOLD_MODE=route, parity-tested like the others (tests/test_gpu_variants.py).
+static bool route_eligible(const gs_cc_t* h, uint64_t n) {
+    (void)n;
     if (!h->hot || h->dstats || h->sparse || h->hot_bits > kPartBits + 6 || h->cus <= 0) return false;
     const uint32_t parts = 1u << (h->hot_bits > kPartBits ? h->hot_bits - kPartBits : 0);
     const uint32_t grid = (uint32_t)h->cus / parts * parts;
-    if (grid < parts) return false;
-    const int m = dbg().fold_mode;
-    if (m == kFoldRoute) return true;
-    return m == kFoldAuto && h->hot_bits >= dbg().ring_min_bits && n >= kRouteMinEdges;
+    if (grid < parts || grid / parts > kProbeMaxLists || 3 * grid + 1 > kUnionMaxRegions) return false;
+    return dbg().fold_mode == kFoldRoute;
 }
+static bool use_route(const gs_cc_t* h, uint64_t n) { return route_eligible(h, n); }
 
 template <typename IdT>
 int launch_fold_route(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
@@ -459,6 +466,7 @@ int launch_fold_route(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     r.parts = parts;
     r.gwords = (uint32_t)((h->cap + 31) / 32);
     r.grid = grid;
+    r.exp = dbg().route_exp;
     HotArgs hot{h->hot, h->hot_bits, h->hot_cand};
     hot.sample_edges = kHotSampleEdges;
     hot.budget = h->derr + 6;
@@ -471,11 +479,28 @@ int launch_fold_route(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     f.cbits = kUseCbits ? h->cbits : nullptr;
     KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_ROUTE : h->fold_timer, n);
     const uint32_t ob = 64;                                                 // overflow-list blocks
+    const unsigned ugrid = 3 * grid * kUnionSplit + ob;
     klaunch(k_sift<IdT>, dim3(grid), dim3(kSiftThreads), h->stream, t.start(), nullptr, a, b, f, hot, r);
     klaunch(k_probe<true>, dim3(grid), dim3(kProbeThreads), h->stream, nullptr, nullptr, f, hot, r);
     klaunch(k_probe<false>, dim3(grid), dim3(kProbeThreads), h->stream, nullptr, nullptr, f, hot, r);
-    if (h->mark) klaunch(k_union_surv<true>, dim3(3 * grid + ob), dim3(256), h->stream, nullptr, t.stop(), f, r, ob);
-    else klaunch(k_union_surv<false>, dim3(3 * grid + ob), dim3(256), h->stream, nullptr, t.stop(), f, r, ob);
+    if (h->mark) klaunch(k_union_surv<true>, dim3(ugrid), dim3(256), h->stream, nullptr, t.stop(), f, r, ob);
+    else klaunch(k_union_surv<false>, dim3(ugrid), dim3(256), h->stream, nullptr, t.stop(), f, r, ob);
+    if (r.exp & 8u) {                                                       // timing lab: the launch's counts
+        std::vector<uint32_t> c(3ull * grid * parts), sc(3ull * grid);
+        unsigned long long oc = 0;
+        GS_HIP(hipMemcpyAsync(c.data(), r.cnt, c.size() * 4, hipMemcpyDeviceToHost, h->stream));
+        GS_HIP(hipMemcpyAsync(sc.data(), r.scnt, sc.size() * 4, hipMemcpyDeviceToHost, h->stream));
+        GS_HIP(hipMemcpyAsync(&oc, r.ocount, 8, hipMemcpyDeviceToHost, h->stream));
+        GS_HIP(hipStreamSynchronize(h->stream));
+        uint64_t sum[3] = {0, 0, 0}, ss[3] = {0, 0, 0};
+        for (int k = 0; k < 3; ++k)
+            for (size_t i = 0; i < (size_t)grid * parts; ++i) sum[k] += c[k * (size_t)grid * parts + i];
+        for (int k = 0; k < 3; ++k)
+            for (uint32_t i = 0; i < grid; ++i) ss[k] += sc[k * grid + i];
+        fprintf(stderr, "[route] edges %llu singles %llu doubles %llu c-singles %llu survivors A %llu B %llu C %llu overflow %llu\n",
+                (unsigned long long)n, (unsigned long long)sum[0], (unsigned long long)sum[1], (unsigned long long)sum[2],
+                (unsigned long long)ss[0], (unsigned long long)ss[1], (unsigned long long)ss[2], oc);
+    }
     return GS_OK;
 }
 
@@ -686,7 +711,7 @@ int compress_impl(gs_cc_t* h) {
         ++h->closes;
         klaunch(k_compress, dim3(grid_for(h->cap, 1024, kCompressGrid)), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
                 h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot,
-                (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr);
+                (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits);
         h->sbits_stale = false;
     }
     GS_HIP(hipGetLastError());
@@ -970,6 +995,8 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->gbits) (void)hipFree(h->gbits);
     if (h->sbits) (void)hipFree(h->sbits);
     if (h->cbits) (void)hipFree(h->cbits);
+    if (h->dbits) (void)hipFree(h->dbits);
+    if (h->elab) (void)hipFree(h->elab);
     if (h->dstats) (void)hipFree(h->dstats);
     if (h->hot) (void)hipFree(h->hot);
     if (h->hot_cand) (void)hipFree(h->hot_cand);
@@ -1004,6 +1031,10 @@ int gs_cc_reset(gs_cc_t* h) {
     GS_HIP(hipMemsetAsync(h->gbits, 0, mark_bytes(h->cap), h->stream));
     GS_HIP(hipMemsetAsync(h->sbits, 0, mark_bytes(h->cap), h->stream));
     GS_HIP(hipMemsetAsync(h->cbits, 0, mark_bytes(h->cap), h->stream));
+    if (h->elab) {                       // a new stream: the next delta is the whole emission
+        GS_HIP(hipMemsetAsync(h->elab, 0xFF, (size_t)h->cap * 4, h->stream));
+        GS_HIP(hipMemsetAsync(h->dbits, 0, mark_bytes(h->cap), h->stream));
+    }
     // giant state (cc_kernels.hpp, giant_state()): both slots no giant / gbits built for none,
     // hot set owner none
     GS_HIP(hipMemsetAsync(h->derr + 1, 0xFF, 5 * sizeof(uint32_t), h->stream));
@@ -1218,6 +1249,70 @@ int gs_cc_emit_pairs(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uin
     if (total > cap) return fail(GS_ERR_CAPACITY, "gs_cc_emit_pairs: %llu pairs, capacity %llu",
                                  (unsigned long long)total, (unsigned long long)cap);
     return GS_OK;
+}
+
+int gs_cc_emit_delta(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uint64_t* n_out) {
+    GS_TRY(check(h));
+    if (!n_out) return fail(GS_ERR_INVALID, "gs_cc_emit_delta: null n_out");
+    if (cap && (!vertices || !labels)) return fail(GS_ERR_INVALID, "gs_cc_emit_delta: null output");
+    if (h->sparse) return fail(GS_ERR_UNSUPPORTED, "gs_cc_emit_delta: sparse-id summary (use gs_cc_emit_pairs)");
+    DeviceGuard g(h->device);
+    if (!h->elab) {                      // first call: every vertex dirty, nothing emitted yet
+        if (hipMalloc(&h->elab, (size_t)h->cap * 4) != hipSuccess || hipMalloc(&h->dbits, mark_bytes(h->cap)) != hipSuccess) {
+            (void)hipGetLastError();
+            if (h->elab) (void)hipFree(h->elab);
+            h->elab = nullptr;
+            return fail(GS_ERR_NOMEM, "gs_cc_emit_delta: state allocation failed");
+        }
+        GS_HIP(hipMemsetAsync(h->elab, 0xFF, (size_t)h->cap * 4, h->stream));
+        GS_HIP(hipMemsetAsync(h->dbits, 0xFF, mark_bytes(h->cap), h->stream));
+    }
+    GS_TRY(compress_impl(h));
+    const uint32_t ntiles = (uint32_t)((h->cap + kTile - 1) / kTile);
+    const size_t esz = h->cfg.id_bits / 8;
+    const size_t cnt_b = ((size_t)ntiles * 4 + 15) & ~(size_t)15;
+    const size_t off_b = ((size_t)(ntiles + 1) * 8 + 15) & ~(size_t)15;
+    GS_TRY(ensure_buf(&h->tmp, &h->tmp_bytes, cnt_b + off_b));
+    uint32_t* cnt = static_cast<uint32_t*>(h->tmp);
+    uint64_t* off = reinterpret_cast<uint64_t*>(static_cast<char*>(h->tmp) + cnt_b);
+    hipLaunchKernelGGL(k_delta_count, dim3(ntiles), dim3(kTileThreads), 0, h->stream, (const uint32_t*)h->parent, h->cap,
+                       (const uint32_t*)h->elab, (const uint32_t*)h->dbits, cnt);
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, h->stream, cnt, off, ntiles);
+    GS_HIP(hipGetLastError());
+    GS_HIP(hipMemcpyAsync(h->hscratch, off + ntiles, 8, hipMemcpyDeviceToHost, h->stream));
+    GS_TRY(sync_and_check(h));
+    const uint64_t total = h->hscratch[0];
+    *n_out = total;
+    if (total > cap) return fail(GS_ERR_CAPACITY, "gs_cc_emit_delta: %llu changed pairs, capacity %llu (nothing consumed)",
+                                 (unsigned long long)total, (unsigned long long)cap);
+    const bool dev = total == 0 || (is_device_pointer(vertices) && is_device_pointer(labels));
+    void* vo = vertices;
+    void* lo = labels;
+    if (!dev) {
+        GS_TRY(ensure_buf(&h->tmp, &h->tmp_bytes, cnt_b + off_b + 2 * total * esz));
+        cnt = static_cast<uint32_t*>(h->tmp);      // (ensure_buf may have moved tmp: recount)
+        off = reinterpret_cast<uint64_t*>(static_cast<char*>(h->tmp) + cnt_b);
+        hipLaunchKernelGGL(k_delta_count, dim3(ntiles), dim3(kTileThreads), 0, h->stream, (const uint32_t*)h->parent, h->cap,
+                           (const uint32_t*)h->elab, (const uint32_t*)h->dbits, cnt);
+        hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, h->stream, cnt, off, ntiles);
+        vo = static_cast<char*>(h->tmp) + cnt_b + off_b;
+        lo = static_cast<char*>(vo) + total * esz;
+    }
+    if (total) {
+        if (h->cfg.id_bits == 32)
+            hipLaunchKernelGGL(k_delta_scatter<uint32_t>, dim3(ntiles), dim3(kTileThreads), 0, h->stream, (const uint32_t*)h->parent,
+                               h->cap, h->elab, (const uint32_t*)h->dbits, (const uint64_t*)off, (uint32_t*)vo, (uint32_t*)lo);
+        else
+            hipLaunchKernelGGL(k_delta_scatter<int64_t>, dim3(ntiles), dim3(kTileThreads), 0, h->stream, (const uint32_t*)h->parent,
+                               h->cap, h->elab, (const uint32_t*)h->dbits, (const uint64_t*)off, (int64_t*)vo, (int64_t*)lo);
+        GS_HIP(hipGetLastError());
+        if (!dev) {
+            GS_HIP(hipMemcpyAsync(vertices, vo, total * esz, hipMemcpyDeviceToHost, h->stream));
+            GS_HIP(hipMemcpyAsync(labels, lo, total * esz, hipMemcpyDeviceToHost, h->stream));
+        }
+    }
+    GS_HIP(hipMemsetAsync(h->dbits, 0, mark_bytes(h->cap), h->stream));    // consumed
+    return sync_and_check(h);
 }
 
 int gs_cc_find(gs_cc_t* h, const void* ids, void* roots, uint64_t n) {

@@ -261,7 +261,21 @@ __device__ __forceinline__ uint32_t hot_bucket(uint32_t v, uint32_t B, uint32_t&
     r = (h & ((1u << rb) - 1)) + 1;
     return h >> rb;
 }
+// Any slot == r, by the SWAR zero-field test on x ^ (r in every field): ((z - ones) & ~z & highs)
+// is non-zero iff some field of z is zero (a borrow can only flag fields above a true zero
+// field, so "any" is exact). Empty slots (0) never equal r >= 1; r = 4096 does not fit 12 bits
+// and never matches (it never enters either).
 __device__ __forceinline__ bool hot_match(uint2 w, uint32_t r, bool five) {
+    const uint64_t x = ((uint64_t)w.y << 32) | w.x;
+    constexpr uint64_t kOnes5 = 0x001001001001001ull, kHigh5 = 0x800800800800800ull;
+    constexpr uint64_t kOnes4 = 0x0001000100010001ull, kHigh4 = 0x8000800080008000ull;
+    const uint64_t ones = five ? kOnes5 : kOnes4, high = five ? kHigh5 : kHigh4;
+    const uint64_t z = x ^ ((uint64_t)r * ones);
+    return (((z - ones) & ~z & high) != 0) & (!five | (r <= 0xFFFu));
+}
+
+// the field-by-field form (timing lab A/B of the SWAR test: GSGPU_ROUTE_EXP bit 4)
+__device__ __forceinline__ bool hot_match_fields(uint2 w, uint32_t r, bool five) {
     const uint64_t x = ((uint64_t)w.y << 32) | w.x;
     const bool m5 = ((x & 0xFFFu) == r) | (((x >> 12) & 0xFFFu) == r) | (((x >> 24) & 0xFFFu) == r) |
                     (((x >> 36) & 0xFFFu) == r) | (((x >> 48) & 0xFFFu) == r);
@@ -1178,7 +1192,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                                                   uint32_t* __restrict__ gbits, uint32_t* __restrict__ sbits,
                                                   const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                   uint32_t* __restrict__ owner, uint2* __restrict__ hot, int rebuild_seen,
-                                                  uint32_t* __restrict__ cbits) {
+                                                  uint32_t* __restrict__ cbits, uint32_t* __restrict__ dbits) {
     __shared__ uint32_t s_g, s_inc, s_clear;
     if (threadIdx.x == 0) {
         const uint32_t g0 = in[0];
@@ -1213,6 +1227,8 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
             // vertices claimed under the giant root since the last close: already labelled g
             uint32_t add = cbits ? cbits[w] : 0u;
             if (add) cbits[w] = 0u;
+            // delta emission: every vertex this close may relabel (or that is new) is dirty
+            if (dbits && (cand | add)) dbits[w] |= cand | add;
             // up to 8 stragglers at a time, their parent and grandparent reads issued back to
             // back (one at a time: a young Erdos-Renyi window's close, ~32 stragglers per word,
             // spent 121 us per 2^24 ids in dependent loads)
@@ -1287,6 +1303,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                 if ((lane & 7) == 0 && base < n) {
                     sbits[base >> 5] = sw;
                     if (cbits) cbits[base >> 5] = 0u;    // this pass labelled the claimed vertices too
+                    if (dbits) dbits[base >> 5] = sw;    // a full pass may relabel any seen vertex
                 }
             }
         }
@@ -1433,6 +1450,66 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_scatter(const uint32_t* _
     for (int k = 0; k < kTilePerThread; ++k) {
         if (p[k] == kInvalid) continue;
         if (pos < cap) { vout[pos] = static_cast<IdT>(base + k); lout[pos] = static_cast<IdT>(p[k]); }
+        ++pos;
+    }
+}
+
+// ---- delta emission (gs_cc_emit_delta): same tiles as emit_pairs; a vertex is emitted when it is
+// dirty (a close may have relabelled it since the last delta) and its label differs from the one
+// last emitted (elab). A thread's 16 vertices are half a dirty word; clean halves read nothing else.
+__device__ __forceinline__ uint32_t delta_bits(const uint32_t* __restrict__ dbits, uint64_t base) {
+    return (dbits[base >> 5] >> (base & 16)) & 0xFFFFu;
+}
+
+__global__ __launch_bounds__(kTileThreads) void k_delta_count(const uint32_t* __restrict__ parent, uint32_t n,
+                                                              const uint32_t* __restrict__ elab,
+                                                              const uint32_t* __restrict__ dbits,
+                                                              uint32_t* __restrict__ tile_count) {
+    const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kTilePerThread;
+    uint32_t c = 0;
+    if (base < n) {
+        const uint32_t d = delta_bits(dbits, base);
+#pragma unroll
+        for (int k = 0; k < kTilePerThread; ++k) {
+            const uint64_t v = base + k;
+            if (((d >> k) & 1u) && v < n) {
+                const uint32_t p = parent[v];
+                c += (p != kInvalid && p != elab[v]);
+            }
+        }
+    }
+    uint32_t tot;
+    (void)block_exclusive_scan(c, &tot);
+    if (threadIdx.x == 0) tile_count[blockIdx.x] = tot;
+}
+
+template <typename IdT>
+__global__ __launch_bounds__(kTileThreads) void k_delta_scatter(const uint32_t* __restrict__ parent, uint32_t n,
+                                                                uint32_t* __restrict__ elab,
+                                                                const uint32_t* __restrict__ dbits,
+                                                                const uint64_t* __restrict__ off, IdT* __restrict__ vout,
+                                                                IdT* __restrict__ lout) {
+    const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kTilePerThread;
+    uint32_t p[kTilePerThread];
+    uint32_t hit = 0, c = 0;
+    const uint32_t d = base < n ? delta_bits(dbits, base) : 0u;
+#pragma unroll
+    for (int k = 0; k < kTilePerThread; ++k) {
+        const uint64_t v = base + k;
+        p[k] = kInvalid;
+        if (((d >> k) & 1u) && v < n) {
+            p[k] = parent[v];
+            if (p[k] != kInvalid && p[k] != elab[v]) { hit |= 1u << k; ++c; }
+        }
+    }
+    uint32_t tot;
+    uint64_t pos = off[blockIdx.x] + block_exclusive_scan(c, &tot);
+#pragma unroll
+    for (int k = 0; k < kTilePerThread; ++k) {
+        if (!((hit >> k) & 1u)) continue;
+        vout[pos] = static_cast<IdT>(base + k);
+        lout[pos] = static_cast<IdT>(p[k]);
+        elab[base + k] = p[k];
         ++pos;
     }
 }

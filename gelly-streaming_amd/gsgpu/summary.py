@@ -230,6 +230,21 @@ class DisjointSet:
              l.ctypes.data_as(ctypes.c_void_p), nv, ctypes.byref(cnt))
         return v[:cnt.value].astype(np.int64), l[:cnt.value].astype(np.int64)
 
+    def delta(self, vertices=None, labels=None) -> Tuple[np.ndarray, np.ndarray]:
+        """gs_cc_emit_delta: the (vertex, label) pairs new or changed since the previous delta,
+        sorted by vertex (the first delta is the whole emission). Into the given buffers (host
+        numpy or device tensors, id_bits wide) if passed, else into fresh numpy arrays sized from
+        the summary. Returns views of the filled prefix."""
+        dt = np.int32 if self.id_bits == 32 else np.int64
+        if vertices is None:
+            n = max(self.stats()[0], 1)
+            vertices, labels = np.empty(n, dtype=dt), np.empty(n, dtype=dt)
+        pv, kv, cap = _buf(vertices, self.id_bits, "vertices")
+        pl, kl, cap2 = _buf(labels, self.id_bits, "labels")
+        cnt = U64()
+        call("gs_cc_emit_delta", self.handle, pv, pl, min(cap, cap2), ctypes.byref(cnt))
+        return vertices[:cnt.value], labels[:cnt.value]
+
     # ---- checkpoint / resume (Merger implements ListCheckpointed, SummaryAggregation.java:127-135) ----
     def snapshot(self) -> Tuple[np.ndarray, np.ndarray]:
         """The summary as its canonical (vertex, label) pairs, sorted by vertex: everything the

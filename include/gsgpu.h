@@ -116,6 +116,15 @@ int gs_cc_emit_dense(gs_cc_t* h, void* labels, uint64_t n);
 /* (vertex, label) pairs of every vertex in the summary, sorted by vertex.
  * Writes min(cap, |V|) pairs, *n_out = |V|; GS_ERR_CAPACITY if cap < |V|. Implies close_window. */
 int gs_cc_emit_pairs(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uint64_t* n_out);
+/* Per-window DELTA of the emission (what a host-side Merger / FlattenSet consumer needs to keep its
+ * copy of the cumulative summary, SummaryAggregation.java:110-111, ConnectedComponentsExample.java:
+ * 143-156, at O(changes) PCIe cost): the (vertex, label) pairs, sorted by vertex, of every vertex
+ * that is new or whose canonical label changed since the previous gs_cc_emit_delta call (the first
+ * call, and the first after gs_cc_reset, returns the whole emission). Writes the pairs if they fit:
+ * *n_out = their number; if cap < *n_out, GS_ERR_CAPACITY and NOTHING is consumed (call again with
+ * a bigger buffer). Applying every delta in order to a map reproduces gs_cc_emit_pairs. Output
+ * element width = id_bits; vertices/labels host or device. Dense ids only. Implies close_window. */
+int gs_cc_emit_delta(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uint64_t* n_out);
 /* Order-independent checksum of the canonical emission (definition shared with oracle/:
  * sum over seen v of splitmix64(v ^ splitmix64(label ^ 0xD1B54A32D192ED03))). Implies close_window. */
 int gs_cc_checksum(gs_cc_t* h, uint64_t* checksum, uint64_t* n_vertices, uint64_t* n_components);

@@ -234,3 +234,55 @@ def test_reset_restarts_the_exact_round(oracle):
     for r in range(world):
         assert sums[r] == 2 * [int(x) for x in want["checksums"]]
         assert ov[r][1] == 2 * ov[r][0], ov
+
+
+def test_c5_eight_ranks_small_windows_latency(oracle):
+    """BASELINE config 5's layout at 8 ranks (in-process transport, one GPU): the RMAT-24 stream
+    (seed 3) in 2^16-edge global windows, 2^13 edges per rank per window, allgather mode — every
+    window's emission vs the oracle with 8 partitions; the per-window wall latency (fold + exchange
+    + close on every rank, host-observed) is printed."""
+    import time
+    import torch
+    from gsgpu import gen
+    P, scale, W, N = 8, 24, 1 << 16, 48
+    cap = 1 << scale
+    s = torch.empty(N * W, dtype=torch.int32, device="cuda")
+    d = torch.empty(N * W, dtype=torch.int32, device="cuda")
+    gen.rmat(s, d, 0, scale, 3)
+    torch.cuda.synchronize()
+    hs, hd = s.cpu().numpy().astype(np.int64), d.cpu().numpy().astype(np.int64)
+    want = oracle.run(hs, hd, W, partitions=P, threads=P, emit=EMIT_CHECKSUM, label_cap=cap)
+    comms = Comm.local_group(P, 0)
+    sums = [[] for _ in range(P)]
+    lat = [[] for _ in range(P)]
+    errors = []
+    Wr = W // P
+
+    def rank(r):
+        try:
+            ds = DisjointSet(cap, id_bits=32, track_marks=True)
+            for w in range(N):
+                t0 = time.perf_counter()
+                lo = w * W + r * Wr
+                ds.fold(s[lo:lo + Wr], d[lo:lo + Wr])
+                ds.merge_window(comms[r], "allgather")
+                ds.sync()
+                lat[r].append((time.perf_counter() - t0) * 1e6)
+                sums[r].append(ds.checksum()[0])
+            ds.close()
+        except Exception as e:
+            errors.append((r, repr(e)))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th) and not errors, errors
+    for c in comms:
+        c.close()
+    for r in range(P):
+        assert sums[r] == [int(x) for x in want["checksums"]], "rank %d" % r
+    steady = sorted(max(lat[r][w] for r in range(P)) for w in range(8, N))
+    print("C5 8 ranks (in-process, one GPU): per-window latency p50 %.0f us, p99 %.0f us (max over ranks)"
+          % (steady[len(steady) // 2], steady[min(len(steady) - 1, int(len(steady) * 0.99))]))

@@ -273,6 +273,41 @@ def test_emit_pairs_sorted_and_capacity_error(torch_cuda):
     assert rc == _abi.GS_ERR_CAPACITY and n.value == v.size
 
 
+@pytest.mark.parametrize("bits", [32, 64])
+def test_emit_delta_rebuilds_every_emission(oracle, torch_cuda, bits):
+    """gs_cc_emit_delta: applying each window's delta to a host map reproduces that window's whole
+    emission (gs_cc_emit_pairs, and the oracle's checksum), a too-small buffer consumes nothing,
+    and after reset the first delta is the whole emission again (SummaryAggregation.java:110-111)."""
+    from pyoracle import dense_checksum
+    s, d = oracle.gen_rmat(0, 1 << 18, 15, 4)
+    cap, W = 1 << 15, 1 << 15
+    want = oracle.run(s, d, W, partitions=2, emit=EMIT_CHECKSUM, label_cap=cap)
+    ds = DisjointSet(cap, id_bits=bits)
+    for step in range(2):
+        ds.reset()
+        mirror = np.full(cap, -1, dtype=np.int64)
+        sizes = []
+        for w, lo in enumerate(range(0, s.size, W)):
+            ds.fold(s[lo:lo + W], d[lo:lo + W])
+            if w == 2:                                   # too small: error, nothing consumed
+                small = np.empty(1, dtype=np.int32 if bits == 32 else np.int64)
+                with pytest.raises(GsError) as e:
+                    ds.delta(small, small.copy())
+                assert e.value.code == _abi.GS_ERR_CAPACITY
+            v, l = ds.delta()
+            assert (np.diff(v) > 0).all()
+            sizes.append(v.size)
+            mirror[v.astype(np.int64)] = l
+            pv, pl = ds.pairs()
+            np.testing.assert_array_equal(np.nonzero(mirror >= 0)[0], pv)
+            np.testing.assert_array_equal(mirror[pv], pl)
+            assert dense_checksum(mirror)[0] == int(want["checksums"][w])
+        assert sizes[0] == ds.stats()[0] or len(sizes) > 1
+        assert sum(sizes[1:]) < 2 * ds.stats()[0]        # deltas, not whole emissions
+        v, l = ds.delta()                                # nothing changed since
+        assert v.size == 0
+
+
 def test_reset_and_transient_state():
     ds = DisjointSet(64, id_bits=32)
     ds.union(1, 2)
@@ -519,7 +554,8 @@ def test_bench_two_ranks_one_gpu_verified(merge, scaling):
 
 
 @pytest.mark.parametrize("extra", [["--id-bits", "64"], ["--host-input"], ["--host-input", "--id-bits", "64"],
-                                   ["--workload", "c3_single"]], ids=["int64", "host", "host_int64", "single_window"])
+                                   ["--workload", "c3_single"], ["--emit-host"]],
+                         ids=["int64", "host", "host_int64", "single_window", "emit_host"])
 def test_bench_lines_verified(extra):
     """The extra bench lines (int64 ids, pinned-host input through the double-buffered staging,
     one window), end to end against the independent torch CC, at RMAT-22 / 2^20-edge windows."""
