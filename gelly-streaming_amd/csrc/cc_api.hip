@@ -13,6 +13,7 @@
 #include "cc_internal.hpp"
 #include "cc_kernels.hpp"
 #include "route.hpp"
+#include "xtail.hpp"
 #include "sparse_ids.hpp"
 
 #include <hipcub/hipcub.hpp>
@@ -102,6 +103,9 @@ struct gs_cc {
     size_t route_bytes = 0;
     uint64_t route_edges = 0;
     uint64_t route_launches = 0;         // parity of the overflow counters
+    // XCD-sliced filter tail (xtail.hpp): lists and counts, sized for xr_edges edges per launch
+    void* xr_mem = nullptr;
+    uint64_t xr_edges = 0;
     // GS_CC_SPARSE_IDS: id -> slot table; cap (above) = slots = 2^hbits + 1
     bool sparse = false;
     int64_t* keys = nullptr;             // 2^hbits slot keys (INT64_MIN = empty)
@@ -248,10 +252,10 @@ constexpr uint32_t kYoungSplitDiv = 16;
 
 // ---- debug variables (read once per process; none is needed in production) ----
 //   GSGPU_FOLD_STATS=1       per-window fold counters on stderr (STATS kernel variants; same results)
-//   GSGPU_FOLD_MODE=plain|ring|route|auto   force the steady fold variant (parity tests of each variant)
+//   GSGPU_FOLD_MODE=plain|ring|route|xr|auto   force the steady fold variant (parity tests of each variant)
 //   GSGPU_RING_MIN_BITS=B    ring fold + warm set from ids >= 2^B instead of 2^25 (tests at small sizes)
 //   GSGPU_YOUNG_SPLIT=S      young split after S edges instead of capacity/16 (0 = off; tests)
-enum FoldMode { kFoldPlain = 0, kFoldRing = 1, kFoldAuto = 2, kFoldRoute = 3 };
+enum FoldMode { kFoldPlain = 0, kFoldRing = 1, kFoldAuto = 2, kFoldRoute = 3, kFoldXr = 4 };
 struct DebugEnv {
     bool fold_stats = false;
     int fold_mode = kFoldAuto;
@@ -265,6 +269,7 @@ struct DebugEnv {
         if (e && !strcmp(e, "plain")) fold_mode = kFoldPlain;
         if (e && !strcmp(e, "ring")) fold_mode = kFoldRing;
         if (e && !strcmp(e, "route")) fold_mode = kFoldRoute;
+        if (e && !strcmp(e, "xr")) fold_mode = kFoldXr;
         e = getenv("GSGPU_RING_MIN_BITS");
         if (e && *e) ring_min_bits = (uint32_t)strtoul(e, nullptr, 0);
         e = getenv("GSGPU_YOUNG_SPLIT");
@@ -332,7 +337,7 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
 static bool route_eligible(const gs_cc_t* h, uint64_t n);
 static bool use_ring(const gs_cc_t* h) {
     const int m = dbg().fold_mode;
-    return m == kFoldRing || (m == kFoldAuto && h->hot_bits >= dbg().ring_min_bits);
+    return m == kFoldRing || m == kFoldXr || (m == kFoldAuto && h->hot_bits >= dbg().ring_min_bits);
 }
 
 static void launch_warm_build(gs_cc_t* h, hipEvent_t stop) {
@@ -357,6 +362,79 @@ static WarmBuild warm_build_args(gs_cc_t* h) {
     w.wb = h->warm_bits;
     w.valid = h->derr + 7;
     return w;
+}
+
+// The XCD-sliced tail replaces the ring fold's gbits lookups (xtail.hpp) in steady launches: not in
+// the first kXrFirst ring launches after reset (the hot set's admission budget, the warm count at
+// launch kWarmAt), nor in a warm-count or periodic-admission launch, which stay k_fold_ring.
+constexpr uint64_t kXrFirst = 6;
+constexpr bool kXrDefault = false;
+static bool xr_launch(const gs_cc_t* h) {
+    const int m = dbg().fold_mode;
+    if (!(m == kFoldXr || (m == kFoldAuto && kXrDefault))) return false;
+    // slices of 2^(B-3) ids; ring entries carry flags in bit 31 (B <= 30); auto mode only where
+    // gbits outgrows an XCD's L2 (at smaller B the forced mode is a parity test)
+    if (!h->hot || h->dstats || h->sparse || h->cus < (int)kXSlices || h->hot_bits < 8 || h->hot_bits > 30) return false;
+    if (m == kFoldAuto && h->hot_bits < kRingMinBits) return false;
+    const uint64_t no = h->ring_launches;
+    const bool build = h->warm && no >= kWarmAt && (no - kWarmAt) % kWarmEvery == 0;
+    const bool periodic = no % kHotAdmitEvery == kHotAdmitEvery - 1;
+    return no >= kXrFirst && !build && !periodic;
+}
+
+template <typename IdT>
+int launch_fold_xr(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
+    const uint32_t grid = (uint32_t)h->cus / kXSlices * kXSlices;
+    const uint64_t need = std::max<uint64_t>(n, 1ull << 20);
+    const uint64_t cap = ((2 * need / ((uint64_t)grid * kXSlices) + 4096) + 3) & ~3ull;
+    const size_t regions = (size_t)kXSlices * grid;
+    const size_t bytes = regions * cap * 16 + 3 * regions * 4 + 1024;
+    if (need > h->xr_edges) {
+        if (h->xr_mem) {
+            GS_HIP(hipStreamSynchronize(h->stream));
+            GS_HIP(hipFree(h->xr_mem));
+            h->xr_mem = nullptr;
+            h->xr_edges = 0;
+        }
+        if (hipMalloc(&h->xr_mem, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(GS_ERR_NOMEM, "XCD-sliced fold lists (%zu bytes) allocation failed", bytes);
+        }
+        h->xr_edges = need;
+    }
+    char* m = static_cast<char*>(h->xr_mem);
+    XrArgs x;
+    x.cap = cap;
+    x.grid = grid;
+    x.shift = h->hot_bits - 3;
+    x.qs = reinterpret_cast<uint32_t*>(m);
+    x.qd = reinterpret_cast<uint2*>(m + regions * cap * 4);
+    x.qc = reinterpret_cast<uint32_t*>(m + regions * cap * 12);
+    x.cnt = reinterpret_cast<uint32_t*>(m + regions * cap * 16);
+    HotArgs hot{h->hot, h->hot_bits, h->hot_cand};
+    hot.sample_edges = kHotSampleEdges;
+    hot.budget = h->derr + 6;
+    hot.periodic = 0u;
+    ++h->ring_launches;
+    hot.five = (h->hot_bits <= kHotBucketBits + 12) ? 1u : 0u;
+    hot.thresh = kHotThresh;
+    hot.warm = h->warm;
+    hot.warm_bits = h->warm_bits;
+    hot.warm_valid = h->derr + 7;
+    FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, nullptr};
+    f.mark_len = h->mark_ctr;
+    f.cbits = kUseCbits ? h->cbits : nullptr;
+    KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_ROUTE : h->fold_timer, n);
+    if (h->mark) {
+        klaunch(k_fold_xr<IdT, true>, dim3(grid), dim3(kXThreads), h->stream, t.start(), nullptr, a, b, f, hot, x);
+        klaunch(k_xr_tail<true, true>, dim3(grid), dim3(kXThreads), h->stream, nullptr, nullptr, f, x);
+        klaunch(k_xr_tail<true, false>, dim3(grid), dim3(kXThreads), h->stream, nullptr, t.stop(), f, x);
+    } else {
+        klaunch(k_fold_xr<IdT, false>, dim3(grid), dim3(kXThreads), h->stream, t.start(), nullptr, a, b, f, hot, x);
+        klaunch(k_xr_tail<false, true>, dim3(grid), dim3(kXThreads), h->stream, nullptr, nullptr, f, x);
+        klaunch(k_xr_tail<false, false>, dim3(grid), dim3(kXThreads), h->stream, nullptr, t.stop(), f, x);
+    }
+    return GS_OK;
 }
 
 template <typename IdT>
@@ -569,7 +647,12 @@ int launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, size
             if (rc != GS_OK) return rc;
         } else if (h->hot && use_ring(h) && aligned && m >= 4) {
             m &= ~(uint64_t)3;                          // the ring fold takes groups of 4 edges
-            launch_fold_ring<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
+            if (xr_launch(h)) {
+                const int rc = launch_fold_xr<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
+                if (rc != GS_OK) return rc;
+            } else {
+                launch_fold_ring<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
+            }
         } else {
             launch_fold<IdT, AOS>(h, a + off * stride, b + off * esz, m, false);
         }
@@ -1002,6 +1085,7 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->hot_cand) (void)hipFree(h->hot_cand);
     if (h->warm) (void)hipFree(h->warm);
     if (h->route_mem) (void)hipFree(h->route_mem);
+    if (h->xr_mem) (void)hipFree(h->xr_mem);
     if (h->wkeys) (void)hipFree(h->wkeys);
     if (h->wpart) (void)hipFree(h->wpart);
     if (h->wctl) (void)hipFree(h->wctl);

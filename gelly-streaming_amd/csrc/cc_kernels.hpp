@@ -470,6 +470,16 @@ __device__ __forceinline__ void filter_group(const FoldArgs& f, const uint32_t (
     }
     if (HOT) {                                       // branch-free, as the warm probes
         const __amdgpu_buffer_rsrc_t gr = buffer_rsrc(f.gbits, (((uint64_t)f.rc.cap + 31) >> 5) << 2);
+#ifdef GS_EXP_NOGBITS
+        // timing lab (wrong results on purpose): warm misses are taken as giant members, no gbits
+        // load (the warm loads are kept alive: their results feed an empty asm statement)
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            asm volatile("" ::"v"((uint32_t)mu[k]), "v"((uint32_t)mv[k]));
+            mu[k] = true;
+            mv[k] = true;
+        }
+#endif
 #pragma unroll
         for (int k = 0; k < EPT; ++k) {
             const uint32_t xu = __builtin_amdgcn_raw_buffer_load_b32(gr, mu[k] ? kNoLoad : (u[k] >> 5) << 2, 0, 0);

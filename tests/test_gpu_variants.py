@@ -70,6 +70,8 @@ VARIANTS = {
     "route_forced": {"GSGPU_FOLD_MODE": "route"},
     "route_forced_no_split": {"GSGPU_FOLD_MODE": "route", "GSGPU_YOUNG_SPLIT": "0"},
     "young_split_2^18": {"GSGPU_YOUNG_SPLIT": str(1 << 18)},
+    "xr_forced": {"GSGPU_FOLD_MODE": "xr"},
+    "xr_forced_no_split": {"GSGPU_FOLD_MODE": "xr", "GSGPU_YOUNG_SPLIT": "0"},
 }
 
 
@@ -83,7 +85,7 @@ def test_variant_parity(name):
 
 
 @pytest.mark.parametrize("name", ["production", "ring_warm_split_from_2^20", "plain_forced", "ring_warm_stats",
-                                  "route_forced"])
+                                  "route_forced", "xr_forced"])
 def test_fold_variants_verified(name):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0", "--scale", "22",
            "--edge-factor", "16", "--window-log2", "20", "--no-cpu-baseline", "--verify"]

@@ -33,6 +33,29 @@ __global__ __launch_bounds__(256) void k_rand(const uint32_t* __restrict__ mem, 
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// As k_rand over an 8 MiB table, but every workgroup only reads the 1 MiB slice numbered by its
+// XCD (HW_REG_XCC_ID): each XCD's L2 then holds one slice instead of sharing the whole table —
+// the access shape of an XCD-routed giant filter
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & 7u;
+}
+__global__ __launch_bounds__(256) void k_rand_xcd(const uint32_t* __restrict__ mem, uint64_t n, uint32_t seed,
+                                                  uint32_t* __restrict__ out) {
+    uint32_t acc = 0;
+    const uint32_t* slice = mem + (uint64_t)xcc_id() * (1u << 18);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 8;
+    for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < n; i += stride) {
+        uint32_t x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = slice[mix((uint32_t)(i + k) * 0x9E3779B1u + seed) & ((1u << 18) - 1)];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc += x[k];
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void k_stream(const u32x4* __restrict__ mem, uint64_t n16, uint32_t* __restrict__ out) {
     uint32_t acc = 0;
@@ -63,6 +86,10 @@ static void run_rand(void* p) {
     RandArg* r = static_cast<RandArg*>(p);
     hipLaunchKernelGGL(k_rand, dim3(r->blocks), dim3(256), 0, 0, r->mem, r->mask, r->n, 0x1234u, r->out);
 }
+static void run_rand_xcd(void* p) {
+    RandArg* r = static_cast<RandArg*>(p);
+    hipLaunchKernelGGL(k_rand_xcd, dim3(r->blocks), dim3(256), 0, 0, r->mem, r->n, 0x1234u, r->out);
+}
 struct StreamArg { const u32x4* mem; uint64_t n16; uint32_t* out; };
 static void run_stream(void* p) {
     StreamArg* s = static_cast<StreamArg*>(p);
@@ -86,6 +113,11 @@ int main() {
             const float ms = time_ms(run_rand, &r);
             printf(", \"rand4B_%s_%dw_Gps\": %.1f", names[s], wpc, n / (ms * 1e6));
         }
+    }
+    for (int wpc = 16; wpc <= 32; wpc *= 2) {
+        RandArg r{mem, 0, n, (unsigned)(cus * wpc / 4), out};
+        const float ms = time_ms(run_rand_xcd, &r);
+        printf(", \"rand4B_8MiB_xcdslice_%dw_Gps\": %.1f", wpc, n / (ms * 1e6));
     }
     StreamArg st{reinterpret_cast<const u32x4*>(mem), big / 16, out};
     const float ms = time_ms(run_stream, &st);

@@ -8,7 +8,8 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 first = int(sys.argv[2]) if len(sys.argv) > 2 else 13
 ks = sorted(((r["Kernel_Name"].split("(")[0].replace("void ", "").split("::")[-1], int(r["Start_Timestamp"]),
              int(r["End_Timestamp"])) for r in rows), key=lambda x: x[1])
-heads = [i for i, k in enumerate(ks) if k[0].startswith("k_sift") or k[0].startswith("k_fold_ring")]
+HEADS = ("k_sift", "k_fold_ring", "k_fold_xr")
+heads = [i for i, k in enumerate(ks) if k[0].startswith(HEADS)]
 last = heads[-63:]                                  # windows 2..64 of the last step
 tot = defaultdict(float)
 n = 0
@@ -19,7 +20,7 @@ for w, i in enumerate(last, 2):
     n += 1
     j = i
     t0 = ks[i][1]
-    while j < len(ks) and (j == i or not (ks[j][0].startswith("k_sift") or ks[j][0].startswith("k_fold_ring"))):
+    while j < len(ks) and (j == i or not ks[j][0].startswith(HEADS)):
         if ks[j][0].startswith(("k_compress", "k_pick")):
             break
         tot[ks[j][0]] += (ks[j][2] - ks[j][1]) / 1000
