@@ -38,7 +38,7 @@ import torch.distributed as dist  # noqa: E402
 
 import gsgpu  # noqa: E402
 from gsgpu import gen  # noqa: E402
-from gsgpu._abi import (GS_K_COMPRESS, GS_K_EXPORT, GS_K_FOLD, GS_K_MERGE, GS_K_RING, GS_K_ROUTE,  # noqa: E402
+from gsgpu._abi import (GS_K_COMPRESS, GS_K_EXPORT, GS_K_FOLD, GS_K_MERGE, GS_K_RING,  # noqa: E402
                         GS_TIMING_MASK, lib_source_sha)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
@@ -184,13 +184,21 @@ def main():
             emitted[0] += v.numel()
             emitted[1] += 1
 
-    fold_mask = GS_TIMING_MASK | (1 << GS_K_FOLD) | (1 << GS_K_RING) | (1 << GS_K_ROUTE) | \
+    fold_mask = GS_TIMING_MASK | (1 << GS_K_FOLD) | (1 << GS_K_RING) | \
         ((1 << GS_K_MERGE) | (1 << GS_K_EXPORT) if world > 1 else 0)
+
+    # the plain per-window loop runs inside the library (gs_cc_fold_windows: one ABI call per step
+    # instead of two per window); per-window host work (delta copies, the gloo model) keeps the loop
+    batched = not a.emit_host and tree is None
 
     def step():
         ds.reset()
-        for w in range(nwin):
-            window(w)
+        if batched:
+            n_all = nwin * W_rank
+            ds.fold_windows(fsrc[:n_all], fdst[:n_all], W_rank, comm=comm, mode=a.merge)
+        else:
+            for w in range(nwin):
+                window(w)
 
     log = lambda m: print("[bench rank %d] %s" % (rank, m), file=sys.stderr, flush=True)
     log("inputs ready: %d edges/rank, %d windows of %d (global %d), %s scaling" % (E_rank, nwin, W_rank, W_glob, a.scaling))
@@ -217,8 +225,7 @@ def main():
     elapsed = time.perf_counter() - t0
     young_ms, young_n = ds.kernel_time(GS_K_FOLD)
     ring_ms, ring_n = ds.kernel_time(GS_K_RING)
-    route_ms, route_n = ds.kernel_time(GS_K_ROUTE)
-    young_e, ring_e, route_e = (ds.kernel_units(k) for k in (GS_K_FOLD, GS_K_RING, GS_K_ROUTE))
+    young_e, ring_e = (ds.kernel_units(k) for k in (GS_K_FOLD, GS_K_RING))
     merge_ms, _ = ds.kernel_time(GS_K_MERGE)
     export_ms, _ = ds.kernel_time(GS_K_EXPORT)
     ds.timing(False)
@@ -272,13 +279,11 @@ def main():
         label_b = 4 if a.id_bits == 32 else 8
         total_edges = a.steps * E_rank * world
         folds = nwin                                  # the timed launches: the last step's
-        fold_win_ms = (young_ms + ring_ms + route_ms) / max(folds, 1) or float("nan")
-        # the dominant kernel: the steady fold (the routed fold's four launches, or k_fold_ring),
+        fold_win_ms = (young_ms + ring_ms) / max(folds, 1) or float("nan")
+        # the dominant kernel: the steady fold k_fold_ring,
         # bytes per launch from the edges each timed launch actually folded (the library cuts a
         # long fold call into launches of at most 2^24 edges)
-        if route_n and route_ms >= ring_ms:
-            kernel, avg_ms, n_l, e_l = ROUTE_NAME, route_ms / route_n, route_n, route_e / route_n
-        elif ring_n:
+        if ring_n:
             kernel, avg_ms, n_l, e_l = "k_fold_ring", ring_ms / ring_n, ring_n, ring_e / ring_n
         else:                                        # no steady launches (small ids: plain k_fold)
             kernel, avg_ms, n_l, e_l = "k_fold (every window)", fold_win_ms, folds, W_rank
@@ -348,7 +353,7 @@ def main():
                                        "(P x 8 TB/s)" % (per_edge, label_b)},
             },
             "kernels": {
-                "fold_share": (young_ms + ring_ms + route_ms) / (elapsed / a.steps * 1e3),   # timed: the last step's folds
+                "fold_share": (young_ms + ring_ms) / (elapsed / a.steps * 1e3),   # timed: the last step's folds
                 "compress_ms_per_window": comp_ms / max(comp_n, 1),
                 "compress_share": comp_ms / (elapsed / a.steps * 1e3),
             },
@@ -397,9 +402,6 @@ def _pow2(x: int) -> str:
         if x >= (1 << sh) and x % (1 << sh) == 0:
             return "%d%s" % (x >> sh, suf)
     return str(x)
-
-
-ROUTE_NAME = "routed fold (k_sift + k_probe<B> + k_probe<C> + k_union_surv)"
 
 
 def steady_profile(a, kernel, edges_per_launch):

@@ -12,8 +12,6 @@
 
 #include "cc_internal.hpp"
 #include "cc_kernels.hpp"
-#include "route.hpp"
-#include "xtail.hpp"
 #include "sparse_ids.hpp"
 
 #include <hipcub/hipcub.hpp>
@@ -72,6 +70,7 @@ struct gs_cc {
     uint32_t* dbits = nullptr;           // delta emission: vertices a close may have relabelled since the last delta
     uint32_t* elab = nullptr;            // delta emission: the labels last emitted (kInvalid: never)
     uint32_t* derr = nullptr;            // derr[0] deferred device error flags; derr[1..5] giant state
+    uint32_t* psamp = nullptr;           // 2 x kPickSamples labels a full-pass close recorded (k_compress)
     unsigned long long* dscratch = nullptr;  // reduction outputs (8 words)
     unsigned long long* hscratch = nullptr;  // pinned mirror
     void* stage = nullptr;               // host->device staging: 2 slots x (src, dst) x staging_edges ids
@@ -98,14 +97,6 @@ struct gs_cc {
     uint64_t warm_sample = 0;            // edges a warm count launch samples
     uint32_t warm_bcap = 0;              // keys per hash bucket
     int cus = 0;                         // compute units: k_fold_ring grid
-    // routed steady fold (route.hpp): lists, survivors, counters; sized for route_edges edges per launch
-    void* route_mem = nullptr;
-    size_t route_bytes = 0;
-    uint64_t route_edges = 0;
-    uint64_t route_launches = 0;         // parity of the overflow counters
-    // XCD-sliced filter tail (xtail.hpp): lists and counts, sized for xr_edges edges per launch
-    void* xr_mem = nullptr;
-    uint64_t xr_edges = 0;
     // GS_CC_SPARSE_IDS: id -> slot table; cap (above) = slots = 2^hbits + 1
     bool sparse = false;
     int64_t* keys = nullptr;             // 2^hbits slot keys (INT64_MIN = empty)
@@ -252,30 +243,25 @@ constexpr uint32_t kYoungSplitDiv = 16;
 
 // ---- debug variables (read once per process; none is needed in production) ----
 //   GSGPU_FOLD_STATS=1       per-window fold counters on stderr (STATS kernel variants; same results)
-//   GSGPU_FOLD_MODE=plain|ring|route|xr|auto   force the steady fold variant (parity tests of each variant)
+//   GSGPU_FOLD_MODE=plain|ring|auto   force the steady fold variant (parity tests of each variant)
 //   GSGPU_RING_MIN_BITS=B    ring fold + warm set from ids >= 2^B instead of 2^25 (tests at small sizes)
 //   GSGPU_YOUNG_SPLIT=S      young split after S edges instead of capacity/16 (0 = off; tests)
-enum FoldMode { kFoldPlain = 0, kFoldRing = 1, kFoldAuto = 2, kFoldRoute = 3, kFoldXr = 4 };
+enum FoldMode { kFoldPlain = 0, kFoldRing = 1, kFoldAuto = 2 };
 struct DebugEnv {
     bool fold_stats = false;
     int fold_mode = kFoldAuto;
     uint32_t ring_min_bits = kRingMinBits;
     uint64_t young_split = ~0ull;                   // ~0: the production rule
-    uint32_t route_exp = 0;                         // GSGPU_ROUTE_EXP: routed-fold timing lab (wrong results)
     DebugEnv() {
         const char* e = getenv("GSGPU_FOLD_STATS");
         fold_stats = e && atoi(e) != 0;
         e = getenv("GSGPU_FOLD_MODE");
         if (e && !strcmp(e, "plain")) fold_mode = kFoldPlain;
         if (e && !strcmp(e, "ring")) fold_mode = kFoldRing;
-        if (e && !strcmp(e, "route")) fold_mode = kFoldRoute;
-        if (e && !strcmp(e, "xr")) fold_mode = kFoldXr;
         e = getenv("GSGPU_RING_MIN_BITS");
         if (e && *e) ring_min_bits = (uint32_t)strtoul(e, nullptr, 0);
         e = getenv("GSGPU_YOUNG_SPLIT");
         if (e && *e) young_split = strtoull(e, nullptr, 0);
-        e = getenv("GSGPU_ROUTE_EXP");
-        if (e && *e) route_exp = (uint32_t)strtoul(e, nullptr, 0);
     }
 };
 static const DebugEnv& dbg() {
@@ -334,10 +320,9 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
 // Steady-state fold (mature forest, aligned device uint32 SoA): k_fold_ring (LDS hot set + warm set
 // + survivor rings, one persistent launch) once gbits outgrows an XCD's L2, else k_fold as for
 // young windows (GSGPU_FOLD_MODE forces either)
-static bool route_eligible(const gs_cc_t* h, uint64_t n);
 static bool use_ring(const gs_cc_t* h) {
     const int m = dbg().fold_mode;
-    return m == kFoldRing || m == kFoldXr || (m == kFoldAuto && h->hot_bits >= dbg().ring_min_bits);
+    return m == kFoldRing || (m == kFoldAuto && h->hot_bits >= dbg().ring_min_bits);
 }
 
 static void launch_warm_build(gs_cc_t* h, hipEvent_t stop) {
@@ -364,79 +349,6 @@ static WarmBuild warm_build_args(gs_cc_t* h) {
     return w;
 }
 
-// The XCD-sliced tail replaces the ring fold's gbits lookups (xtail.hpp) in steady launches: not in
-// the first kXrFirst ring launches after reset (the hot set's admission budget, the warm count at
-// launch kWarmAt), nor in a warm-count or periodic-admission launch, which stay k_fold_ring.
-constexpr uint64_t kXrFirst = 6;
-constexpr bool kXrDefault = false;
-static bool xr_launch(const gs_cc_t* h) {
-    const int m = dbg().fold_mode;
-    if (!(m == kFoldXr || (m == kFoldAuto && kXrDefault))) return false;
-    // slices of 2^(B-3) ids; ring entries carry flags in bit 31 (B <= 30); auto mode only where
-    // gbits outgrows an XCD's L2 (at smaller B the forced mode is a parity test)
-    if (!h->hot || h->dstats || h->sparse || h->cus < (int)kXSlices || h->hot_bits < 8 || h->hot_bits > 30) return false;
-    if (m == kFoldAuto && h->hot_bits < kRingMinBits) return false;
-    const uint64_t no = h->ring_launches;
-    const bool build = h->warm && no >= kWarmAt && (no - kWarmAt) % kWarmEvery == 0;
-    const bool periodic = no % kHotAdmitEvery == kHotAdmitEvery - 1;
-    return no >= kXrFirst && !build && !periodic;
-}
-
-template <typename IdT>
-int launch_fold_xr(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
-    const uint32_t grid = (uint32_t)h->cus / kXSlices * kXSlices;
-    const uint64_t need = std::max<uint64_t>(n, 1ull << 20);
-    const uint64_t cap = ((2 * need / ((uint64_t)grid * kXSlices) + 4096) + 3) & ~3ull;
-    const size_t regions = (size_t)kXSlices * grid;
-    const size_t bytes = regions * cap * 16 + 3 * regions * 4 + 1024;
-    if (need > h->xr_edges) {
-        if (h->xr_mem) {
-            GS_HIP(hipStreamSynchronize(h->stream));
-            GS_HIP(hipFree(h->xr_mem));
-            h->xr_mem = nullptr;
-            h->xr_edges = 0;
-        }
-        if (hipMalloc(&h->xr_mem, bytes) != hipSuccess) {
-            (void)hipGetLastError();
-            return fail(GS_ERR_NOMEM, "XCD-sliced fold lists (%zu bytes) allocation failed", bytes);
-        }
-        h->xr_edges = need;
-    }
-    char* m = static_cast<char*>(h->xr_mem);
-    XrArgs x;
-    x.cap = cap;
-    x.grid = grid;
-    x.shift = h->hot_bits - 3;
-    x.qs = reinterpret_cast<uint32_t*>(m);
-    x.qd = reinterpret_cast<uint2*>(m + regions * cap * 4);
-    x.qc = reinterpret_cast<uint32_t*>(m + regions * cap * 12);
-    x.cnt = reinterpret_cast<uint32_t*>(m + regions * cap * 16);
-    HotArgs hot{h->hot, h->hot_bits, h->hot_cand};
-    hot.sample_edges = kHotSampleEdges;
-    hot.budget = h->derr + 6;
-    hot.periodic = 0u;
-    ++h->ring_launches;
-    hot.five = (h->hot_bits <= kHotBucketBits + 12) ? 1u : 0u;
-    hot.thresh = kHotThresh;
-    hot.warm = h->warm;
-    hot.warm_bits = h->warm_bits;
-    hot.warm_valid = h->derr + 7;
-    FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, nullptr};
-    f.mark_len = h->mark_ctr;
-    f.cbits = kUseCbits ? h->cbits : nullptr;
-    KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_ROUTE : h->fold_timer, n);
-    if (h->mark) {
-        klaunch(k_fold_xr<IdT, true>, dim3(grid), dim3(kXThreads), h->stream, t.start(), nullptr, a, b, f, hot, x);
-        klaunch(k_xr_tail<true, true>, dim3(grid), dim3(kXThreads), h->stream, nullptr, nullptr, f, x);
-        klaunch(k_xr_tail<true, false>, dim3(grid), dim3(kXThreads), h->stream, nullptr, t.stop(), f, x);
-    } else {
-        klaunch(k_fold_xr<IdT, false>, dim3(grid), dim3(kXThreads), h->stream, t.start(), nullptr, a, b, f, hot, x);
-        klaunch(k_xr_tail<false, true>, dim3(grid), dim3(kXThreads), h->stream, nullptr, nullptr, f, x);
-        klaunch(k_xr_tail<false, false>, dim3(grid), dim3(kXThreads), h->stream, nullptr, t.stop(), f, x);
-    }
-    return GS_OK;
-}
-
 template <typename IdT>
 void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     ensure_stats(h);
@@ -452,8 +364,7 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     // kWarmAt after reset and every kWarmEvery-th after it, each time only if the set is not valid
     // for the current giant (device-gated)
     const uint64_t launch_no = h->ring_launches - 1;
-    // (no warm set where the routed fold takes over: its filter never probes it)
-    const bool build = h->warm && launch_no >= kWarmAt && (launch_no - kWarmAt) % kWarmEvery == 0 && !route_eligible(h, n);
+    const bool build = h->warm && launch_no >= kWarmAt && (launch_no - kWarmAt) % kWarmEvery == 0;
     hot.warm = h->warm;
     hot.warm_bits = h->warm_bits;
     hot.warm_valid = h->derr + 7;
@@ -476,110 +387,6 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
         else klaunch(k_fold_ring<IdT, false, false>, grid, dim3(kHotThreads), h->stream, start, stop, a, b, f, hot);
     }
     if (build) launch_warm_build(h, t.stop());
-}
-
-// Routed steady fold (route.hpp): the giant filter out of LDS slices of gbits, for ids of up to 2^26
-// (at most kRouteMaxParts parts of 2^20 ids). NOT the production fold: on RMAT-26 2^24-edge windows
-// it measured 227 us per steady window (k_sift 98 + k_probe<B> 69 + k_probe<C> 26 + k_union_surv
-// 33) against k_fold_ring's 199 us on the same box (profiles/r03_f_ab.txt); it stays as the variant
-// GSGPU_FOLD_MODE=route, parity-tested like the others (tests/test_gpu_variants.py).
-static bool route_eligible(const gs_cc_t* h, uint64_t n) {
-    (void)n;
-    if (!h->hot || h->dstats || h->sparse || h->hot_bits > kPartBits + 6 || h->cus <= 0) return false;
-    const uint32_t parts = 1u << (h->hot_bits > kPartBits ? h->hot_bits - kPartBits : 0);
-    const uint32_t grid = (uint32_t)h->cus / parts * parts;
-    if (grid < parts || grid / parts > kProbeMaxLists || 3 * grid + 1 > kUnionMaxRegions) return false;
-    return dbg().fold_mode == kFoldRoute;
-}
-static bool use_route(const gs_cc_t* h, uint64_t n) { return route_eligible(h, n); }
-
-template <typename IdT>
-int launch_fold_route(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
-    const uint32_t parts = 1u << (h->hot_bits > kPartBits ? h->hot_bits - kPartBits : 0);
-    const uint32_t grid = (uint32_t)h->cus / parts * parts;
-    // lists: 2x a list's mean share if every edge became an entry, + a hub's worth; survivors: 2x a
-    // workgroup's share of the edges (the rest overflows into one shared list of n entries)
-    const uint64_t need_edges = std::max<uint64_t>(n, 1ull << 20);
-    const uint64_t cap = ((2 * need_edges / ((uint64_t)grid * parts) + 1024) + 3) & ~3ull;
-    const uint64_t scap = 2 * need_edges / grid + 1024;
-    const uint64_t ocap = need_edges;
-    const size_t lists = (size_t)grid * parts * cap;
-    const size_t bytes = lists * 4 + lists * 8 + lists * 4 + 3ull * grid * parts * 4 + 3ull * grid * scap * 8 +
-                         3ull * grid * 4 + ocap * 8 + 64 * 8 + 4096;
-    if (need_edges > h->route_edges) {
-        if (h->route_mem) {
-            GS_HIP(hipStreamSynchronize(h->stream));
-            GS_HIP(hipFree(h->route_mem));
-            h->route_mem = nullptr;
-            h->route_edges = 0;
-        }
-        if (hipMalloc(&h->route_mem, bytes) != hipSuccess) {
-            (void)hipGetLastError();
-            return fail(GS_ERR_NOMEM, "routed fold lists (%zu bytes) allocation failed", bytes);
-        }
-        GS_HIP(hipMemsetAsync(h->route_mem, 0, 4096, h->stream));          // the counters (first 4 KiB)
-        h->route_edges = need_edges;
-        h->route_bytes = bytes;
-    }
-    char* m = static_cast<char*>(h->route_mem);
-    auto* ctl = reinterpret_cast<unsigned long long*>(m);                   // [0..1] overflow counts, [2] admit
-    size_t off = 4096;
-    auto take = [&](size_t b) { char* p = m + off; off += (b + 255) & ~(size_t)255; return p; };
-    RouteArgs r;
-    r.qs = reinterpret_cast<uint32_t*>(take(lists * 4));
-    r.qd = reinterpret_cast<uint2*>(take(lists * 8));
-    r.qc = reinterpret_cast<uint32_t*>(take(lists * 4));
-    r.cnt = reinterpret_cast<uint32_t*>(take(3ull * grid * parts * 4));
-    r.surv = reinterpret_cast<uint2*>(take(3ull * grid * scap * 8));
-    r.scnt = reinterpret_cast<uint32_t*>(take(3ull * grid * 4));
-    r.over = reinterpret_cast<uint2*>(take(ocap * 8));
-    const int q = (int)(h->route_launches & 1);
-    ++h->route_launches;
-    r.ocount = ctl + q;
-    r.onext = ctl + (1 - q);
-    r.admit = ctl + 2;
-    r.cap = cap;
-    r.scap = scap;
-    r.ocap = ocap;
-    r.parts = parts;
-    r.gwords = (uint32_t)((h->cap + 31) / 32);
-    r.grid = grid;
-    r.exp = dbg().route_exp;
-    HotArgs hot{h->hot, h->hot_bits, h->hot_cand};
-    hot.sample_edges = kHotSampleEdges;
-    hot.budget = h->derr + 6;
-    hot.periodic = (h->ring_launches % kHotAdmitEvery == kHotAdmitEvery - 1) ? 1u : 0u;
-    ++h->ring_launches;
-    hot.five = (h->hot_bits <= kHotBucketBits + 12) ? 1u : 0u;
-    hot.thresh = kHotThresh;
-    FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, nullptr};
-    f.mark_len = h->mark_ctr;
-    f.cbits = kUseCbits ? h->cbits : nullptr;
-    KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_ROUTE : h->fold_timer, n);
-    const uint32_t ob = 64;                                                 // overflow-list blocks
-    const unsigned ugrid = 3 * grid * kUnionSplit + ob;
-    klaunch(k_sift<IdT>, dim3(grid), dim3(kSiftThreads), h->stream, t.start(), nullptr, a, b, f, hot, r);
-    klaunch(k_probe<true>, dim3(grid), dim3(kProbeThreads), h->stream, nullptr, nullptr, f, hot, r);
-    klaunch(k_probe<false>, dim3(grid), dim3(kProbeThreads), h->stream, nullptr, nullptr, f, hot, r);
-    if (h->mark) klaunch(k_union_surv<true>, dim3(ugrid), dim3(256), h->stream, nullptr, t.stop(), f, r, ob);
-    else klaunch(k_union_surv<false>, dim3(ugrid), dim3(256), h->stream, nullptr, t.stop(), f, r, ob);
-    if (r.exp & 8u) {                                                       // timing lab: the launch's counts
-        std::vector<uint32_t> c(3ull * grid * parts), sc(3ull * grid);
-        unsigned long long oc = 0;
-        GS_HIP(hipMemcpyAsync(c.data(), r.cnt, c.size() * 4, hipMemcpyDeviceToHost, h->stream));
-        GS_HIP(hipMemcpyAsync(sc.data(), r.scnt, sc.size() * 4, hipMemcpyDeviceToHost, h->stream));
-        GS_HIP(hipMemcpyAsync(&oc, r.ocount, 8, hipMemcpyDeviceToHost, h->stream));
-        GS_HIP(hipStreamSynchronize(h->stream));
-        uint64_t sum[3] = {0, 0, 0}, ss[3] = {0, 0, 0};
-        for (int k = 0; k < 3; ++k)
-            for (size_t i = 0; i < (size_t)grid * parts; ++i) sum[k] += c[k * (size_t)grid * parts + i];
-        for (int k = 0; k < 3; ++k)
-            for (uint32_t i = 0; i < grid; ++i) ss[k] += sc[k * grid + i];
-        fprintf(stderr, "[route] edges %llu singles %llu doubles %llu c-singles %llu survivors A %llu B %llu C %llu overflow %llu\n",
-                (unsigned long long)n, (unsigned long long)sum[0], (unsigned long long)sum[1], (unsigned long long)sum[2],
-                (unsigned long long)ss[0], (unsigned long long)ss[1], (unsigned long long)ss[2], oc);
-    }
-    return GS_OK;
 }
 
 // Young-forest split points (dense ids, SoA folds): one internal close at capacity/16 edges since
@@ -641,18 +448,9 @@ int launch_fold_split(gs_cc_t* h, const char* a, const char* b, uint64_t n, size
             continue;
         }
         m = std::min(m, kInternalCloseEdges);
-        if (h->hot && aligned && m >= 4 && use_route(h, m)) {
-            m &= ~(uint64_t)3;                          // the routed fold takes groups of 4 edges
-            const int rc = launch_fold_route<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
-            if (rc != GS_OK) return rc;
-        } else if (h->hot && use_ring(h) && aligned && m >= 4) {
+        if (h->hot && use_ring(h) && aligned && m >= 4) {
             m &= ~(uint64_t)3;                          // the ring fold takes groups of 4 edges
-            if (xr_launch(h)) {
-                const int rc = launch_fold_xr<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
-                if (rc != GS_OK) return rc;
-            } else {
-                launch_fold_ring<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
-            }
+            launch_fold_ring<IdT>(h, reinterpret_cast<const IdT*>(a + off * esz), reinterpret_cast<const IdT*>(b + off * esz), m);
         } else {
             launch_fold<IdT, AOS>(h, a + off * stride, b + off * esz, m, false);
         }
@@ -788,13 +586,15 @@ int compress_impl(gs_cc_t* h) {
         const bool force = h->closes % kPickEvery == 0;
         const bool pick = force || h->closes < kEarlyPicks;
         uint32_t* in = giant_state(h);
+        const uint32_t* samp_in = h->psamp + (h->closes & 1) * kPickSamples;
+        uint32_t* samp_out = h->psamp + ((h->closes + 1) & 1) * kPickSamples;
         if (pick)
             klaunch(k_pick_giant, dim3(1), dim3(1024), h->stream, t.start(), nullptr, (const uint32_t*)h->parent, h->cap,
                     in, (int)force);
         ++h->closes;
         klaunch(k_compress, dim3(grid_for(h->cap, 1024, kCompressGrid)), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
                 h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot,
-                (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits);
+                (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits, samp_in, samp_out);
         h->sbits_stale = false;
     }
     GS_HIP(hipGetLastError());
@@ -1002,7 +802,7 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
     }
     if (hipMalloc(&h->gbits, mark_bytes(h->cap)) != hipSuccess || hipMalloc(&h->sbits, mark_bytes(h->cap)) != hipSuccess ||
         hipMalloc(&h->cbits, mark_bytes(h->cap)) != hipSuccess ||
-        hipMalloc(&h->derr, kDerrBytes) != hipSuccess || hipMalloc(&h->dscratch, 8 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&h->derr, kDerrBytes) != hipSuccess || hipMalloc(&h->psamp, 2 * kPickSamples * sizeof(uint32_t)) != hipSuccess || hipMalloc(&h->dscratch, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&h->hscratch, 8 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         return bail(fail(GS_ERR_NOMEM, "scratch allocation failed"));
@@ -1075,6 +875,7 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->mark_buf) (void)hipFree(h->mark_buf);
     if (h->mark_ctr) (void)hipFree(h->mark_ctr);
     if (h->derr) (void)hipFree(h->derr);
+    if (h->psamp) (void)hipFree(h->psamp);
     if (h->gbits) (void)hipFree(h->gbits);
     if (h->sbits) (void)hipFree(h->sbits);
     if (h->cbits) (void)hipFree(h->cbits);
@@ -1084,8 +885,6 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->hot) (void)hipFree(h->hot);
     if (h->hot_cand) (void)hipFree(h->hot_cand);
     if (h->warm) (void)hipFree(h->warm);
-    if (h->route_mem) (void)hipFree(h->route_mem);
-    if (h->xr_mem) (void)hipFree(h->xr_mem);
     if (h->wkeys) (void)hipFree(h->wkeys);
     if (h->wpart) (void)hipFree(h->wpart);
     if (h->wctl) (void)hipFree(h->wctl);
@@ -1127,6 +926,7 @@ int gs_cc_reset(gs_cc_t* h) {
         GS_HIP(hipMemcpyAsync(h->derr + 6, &budget, sizeof(uint32_t), hipMemcpyHostToDevice, h->stream));
     }
     GS_HIP(hipMemsetAsync(h->derr + 7, 0, sizeof(uint32_t), h->stream));      // warm set: not built
+    GS_HIP(hipMemsetAsync(h->psamp, 0xFF, 2 * kPickSamples * sizeof(uint32_t), h->stream));   // no samples yet
     if (h->hot) GS_HIP(hipMemsetAsync(h->hot, 0, kHotBuckets * sizeof(uint2), h->stream));
     if (h->hot_cand) GS_HIP(hipMemsetAsync(h->hot_cand, 0xFF, sizeof(uint32_t) << kHotCandBits, h->stream));
     if (h->sparse) {
@@ -1238,6 +1038,25 @@ int gs_cc_close_window(gs_cc_t* h) {
     GS_TRY(check(h));
     DeviceGuard g(h->device);
     return compress_impl(h);
+}
+
+int gs_cc_fold_windows(gs_cc_t* h, gs_comm_t* comm, int mode, const void* src, const void* dst, uint64_t n,
+                       uint64_t window_edges, uint64_t* windows_out) {
+    GS_TRY(check(h));
+    if (windows_out) *windows_out = 0;
+    if (window_edges == 0) return fail(GS_ERR_INVALID, "gs_cc_fold_windows: window_edges must be > 0");
+    if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "gs_cc_fold_windows: null edge buffer");
+    const size_t esz = h->cfg.id_bits / 8;
+    const char* a = static_cast<const char*>(src);
+    const char* b = static_cast<const char*>(dst);
+    uint64_t w = 0;
+    for (uint64_t off = 0; off < n; off += window_edges, ++w) {
+        const uint64_t m = std::min(window_edges, n - off);
+        GS_TRY(gs_cc_fold(h, a + off * esz, b + off * esz, m));
+        GS_TRY(comm ? gs_cc_merge_window(h, comm, mode) : gs_cc_close_window(h));
+        if (windows_out) *windows_out = w + 1;
+    }
+    return GS_OK;
 }
 
 int gs_cc_stats(gs_cc_t* h, uint64_t* nv, uint64_t* nc) {
@@ -1518,7 +1337,7 @@ int gs_cc_timing(gs_cc_t* h, int enable) {
     GS_TRY(resolve_timing(h));
     h->timing = enable != 0;
     h->timing_mask = (enable & GS_TIMING_MASK) ? ((uint32_t)enable & 0xFFu) : ~0u;
-    if (h->timing_mask & (1u << GS_K_FOLD)) h->timing_mask |= (1u << GS_K_RING) | (1u << GS_K_ROUTE);   // "fold" = every launch kind
+    if (h->timing_mask & (1u << GS_K_FOLD)) h->timing_mask |= (1u << GS_K_RING);   // "fold" = every launch kind
     for (int k = 0; k < GS_K_COUNT; ++k) { h->total_ms[k] = 0; h->launches[k] = 0; h->units[k] = 0; }
     return GS_OK;
 }

@@ -274,15 +274,6 @@ __device__ __forceinline__ bool hot_match(uint2 w, uint32_t r, bool five) {
     return (((z - ones) & ~z & high) != 0) & (!five | (r <= 0xFFFu));
 }
 
-// the field-by-field form (timing lab A/B of the SWAR test: GSGPU_ROUTE_EXP bit 4)
-__device__ __forceinline__ bool hot_match_fields(uint2 w, uint32_t r, bool five) {
-    const uint64_t x = ((uint64_t)w.y << 32) | w.x;
-    const bool m5 = ((x & 0xFFFu) == r) | (((x >> 12) & 0xFFFu) == r) | (((x >> 24) & 0xFFFu) == r) |
-                    (((x >> 36) & 0xFFFu) == r) | (((x >> 48) & 0xFFFu) == r);
-    const bool m4 = ((w.x & 0xFFFFu) == r) | ((w.x >> 16) == r) | ((w.y & 0xFFFFu) == r) | ((w.y >> 16) == r);
-    return five ? m5 : m4;
-}
-
 // add v to the global table if a slot of its bucket is free (a full bucket drops it)
 __device__ inline void hot_insert(uint2* gtab, uint32_t v, uint32_t B, bool five) {
     const uint32_t h = hot_hash(v, B);
@@ -470,16 +461,6 @@ __device__ __forceinline__ void filter_group(const FoldArgs& f, const uint32_t (
     }
     if (HOT) {                                       // branch-free, as the warm probes
         const __amdgpu_buffer_rsrc_t gr = buffer_rsrc(f.gbits, (((uint64_t)f.rc.cap + 31) >> 5) << 2);
-#ifdef GS_EXP_NOGBITS
-        // timing lab (wrong results on purpose): warm misses are taken as giant members, no gbits
-        // load (the warm loads are kept alive: their results feed an empty asm statement)
-#pragma unroll
-        for (int k = 0; k < EPT; ++k) {
-            asm volatile("" ::"v"((uint32_t)mu[k]), "v"((uint32_t)mv[k]));
-            mu[k] = true;
-            mv[k] = true;
-        }
-#endif
 #pragma unroll
         for (int k = 0; k < EPT; ++k) {
             const uint32_t xu = __builtin_amdgcn_raw_buffer_load_b32(gr, mu[k] ? kNoLoad : (u[k] >> 5) << 2, 0, 0);
@@ -1171,6 +1152,57 @@ __device__ uint32_t sample_giant(const uint32_t* __restrict__ parent, uint32_t n
     return g;
 }
 
+// As sample_giant, over labels a previous full-pass close recorded (samp[i] = the label of sample
+// position i, kInvalid where unseen): no parent[] walks. Every workgroup of a launch reads the same
+// samp and gets the same pick (the count order breaks ties by key).
+__device__ uint32_t mode_of_samples(const uint32_t* __restrict__ samp, PickLds& L) {
+    for (int i = threadIdx.x; i < kPickSlots; i += blockDim.x) { L.keys[i] = kInvalid; L.cnt[i] = 0; }
+    if (threadIdx.x == 0) L.seen_total = 0;
+    __syncthreads();
+    uint32_t seen = 0;
+    for (int i = threadIdx.x; i < kPickSamples; i += blockDim.x) {
+        const uint32_t lab = samp[i];
+        if (lab == kInvalid) continue;
+        ++seen;
+        uint32_t h = (lab * 2654435761u) & (kPickSlots - 1);
+        for (;;) {
+            const uint32_t old = atomicCAS(&L.keys[h], kInvalid, lab);
+            if (old == kInvalid || old == lab) { atomicAdd(&L.cnt[h], 1u); break; }
+            h = (h + 1) & (kPickSlots - 1);
+        }
+    }
+    atomicAdd(&L.seen_total, seen);
+    __syncthreads();
+    unsigned long long mine = 0;
+    for (int i = threadIdx.x; i < kPickSlots; i += blockDim.x)
+        if (L.cnt[i]) {
+            const unsigned long long c = ((unsigned long long)L.cnt[i] << 32) | L.keys[i];
+            mine = c > mine ? c : mine;
+        }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_down(mine, off, 64);
+        mine = o > mine ? o : mine;
+    }
+    if ((threadIdx.x & 63) == 0) L.best[threadIdx.x >> 6] = mine;
+    __syncthreads();
+    unsigned long long b = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) b = L.best[w] > b ? L.best[w] : b;
+    const uint32_t c = (uint32_t)(b >> 32);
+    return (c >= 16 && 4 * c >= L.seen_total) ? (uint32_t)b : kInvalid;
+}
+
+// Sample positions a full-pass close records labels of: position i (< kPickSamples) sits at a hashed
+// offset inside the i-th stride of 2^sb ids, sb = max(0, floor(log2 n) - 10).
+__device__ __forceinline__ uint32_t samp_shift(uint32_t n) {
+    const uint32_t lg = 31u - (uint32_t)__clz(n | 1u);
+    return lg > 10u ? lg - 10u : 0u;
+}
+__device__ __forceinline__ bool is_sample(uint32_t v, uint32_t sb) {
+    const uint32_t i = v >> sb;
+    return i < (uint32_t)kPickSamples && (v & ((1u << sb) - 1u)) == ((uint32_t)splitmix64(0x5A3Dull + i) & ((1u << sb) - 1u));
+}
+
 // Sample the giant before a close into the slot that close reads (force: even if one is known).
 // One workgroup.
 __global__ __launch_bounds__(1024) void k_pick_giant(const uint32_t* __restrict__ parent, uint32_t n,
@@ -1202,10 +1234,18 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                                                   uint32_t* __restrict__ gbits, uint32_t* __restrict__ sbits,
                                                   const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                   uint32_t* __restrict__ owner, uint2* __restrict__ hot, int rebuild_seen,
-                                                  uint32_t* __restrict__ cbits, uint32_t* __restrict__ dbits) {
+                                                  uint32_t* __restrict__ cbits, uint32_t* __restrict__ dbits,
+                                                  const uint32_t* __restrict__ samp_in, uint32_t* __restrict__ samp_out) {
     __shared__ uint32_t s_g, s_inc, s_clear;
+    __shared__ PickLds L;
+    // no giant known (none picked yet, or a re-pick found none): the mode of the labels the last
+    // full pass recorded at the sample positions, the same in every workgroup (a giant that forms
+    // mid-stream, e.g. an Erdos-Renyi stream past average degree 1, gets its filter at the next
+    // close instead of at the next host-side pick)
+    uint32_t g_samp = kInvalid;
+    if (samp_in && in[0] == kInvalid) g_samp = mode_of_samples(samp_in, L);      // uniform
     if (threadIdx.x == 0) {
-        const uint32_t g0 = in[0];
+        const uint32_t g0 = in[0] != kInvalid ? in[0] : g_samp;
         const uint32_t g = (g0 == kInvalid) ? kInvalid : find_root_ro(parent, g0);
         s_g = g;
         s_inc = (g != kInvalid && g == in[1] && !rebuild_seen) ? 1u : 0u;
@@ -1272,6 +1312,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
             if (add) gbits[w] |= add;
         }
     } else {
+        const uint32_t sb = samp_shift(n);
         for (uint64_t blk = (uint64_t)blockIdx.x * 1024; blk < n; blk += (uint64_t)gridDim.x * 1024) {
             const uint32_t base = (uint32_t)blk + threadIdx.x * 4;
             uint32_t p[4];
@@ -1299,6 +1340,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                 }
                 nib |= (lab == g && lab != kInvalid) ? (1u << k) : 0u;
                 seen |= (p[k] != kInvalid) ? (1u << k) : 0u;
+                if (samp_out && v < n && is_sample(v, sb)) samp_out[v >> sb] = lab;   // kInvalid: unseen
             }
             uint32_t word = nib << (4 * (lane & 7));
             word |= __shfl_xor(word, 1, 64);

@@ -26,7 +26,7 @@ GS_ERR_COMM = -8
 GS_CC_TRACK_MARKS = 1
 GS_CC_SPARSE_IDS = 2
 
-GS_K_FOLD, GS_K_COMPRESS, GS_K_MERGE, GS_K_EXPORT, GS_K_RING, GS_K_ROUTE = 0, 1, 2, 3, 4, 5
+GS_K_FOLD, GS_K_COMPRESS, GS_K_MERGE, GS_K_EXPORT, GS_K_RING = 0, 1, 2, 3, 4
 GS_MERGE_ALLGATHER, GS_MERGE_GATHER, GS_MERGE_TREE = 0, 1, 2
 GS_TIMING_MASK = 0x100
 
@@ -45,7 +45,7 @@ EXPORTED_SYMBOLS = (
     "gs_bip_fold_pairs", "gs_bip_merge", "gs_bip_close_window", "gs_bip_status", "gs_bip_checksum",
     "gs_bip_emit_pairs",
     "gs_comm_unique_id", "gs_comm_create", "gs_comm_create_local", "gs_comm_destroy", "gs_comm_info",
-    "gs_cc_merge_window",
+    "gs_cc_merge_window", "gs_cc_fold_windows",
     "gs_last_error", "gs_version",
 )
 
@@ -155,6 +155,7 @@ def lib() -> ctypes.CDLL:
         "gs_comm_destroy": [vp],
         "gs_comm_info": [vp, P(i32), P(i32), P(u64), P(u64), P(u64), P(u64)],
         "gs_cc_merge_window": [vp, vp, i32],
+        "gs_cc_fold_windows": [vp, vp, i32, vp, vp, u64, u64, P(u64)],
     }
     for name, args in sig.items():
         f = getattr(L, name)

@@ -197,6 +197,19 @@ class DisjointSet:
         from .comm import MODES
         call("gs_cc_merge_window", self.handle, comm.handle, MODES[mode])
 
+    def fold_windows(self, src, dst, window_edges: int, comm=None, mode: str = "allgather") -> int:
+        """A batch of count windows in one call (gs_cc_fold_windows): fold each window of
+        ``window_edges`` edges, then close it (or merge it over ``comm``). Returns the windows."""
+        from .comm import MODES
+        ps, ks, n = _buf(src, self.id_bits, "src")
+        pd, kd, m = _buf(dst, self.id_bits, "dst")
+        if n != m:
+            raise ValueError("src and dst lengths differ (%d, %d)" % (n, m))
+        w = U64()
+        call("gs_cc_fold_windows", self.handle, comm.handle if comm is not None else None,
+             MODES[mode], ps, pd, n, int(window_edges), ctypes.byref(w))
+        return int(w.value)
+
     def stats(self) -> Tuple[int, int]:
         nv, nc = U64(), U64()
         call("gs_cc_stats", self.handle, ctypes.byref(nv), ctypes.byref(nc))
@@ -308,12 +321,10 @@ class DisjointSet:
         return int(u.value)
 
     def fold_time(self) -> Tuple[float, int]:
-        """(ms, launches) of every UpdateCC launch: k_fold (young / plain) + the steady folds
-        (k_fold_ring, or the routed fold's four launches timed as one)."""
+        """(ms, launches) of every UpdateCC launch: k_fold (young / plain) + the steady k_fold_ring."""
         a, na = self.kernel_time(_abi.GS_K_FOLD)
         b, nb = self.kernel_time(_abi.GS_K_RING)
-        c, nc = self.kernel_time(_abi.GS_K_ROUTE)
-        return a + b + c, na + nb + nc
+        return a + b, na + nb
 
 
 def combine_cc(s1: DisjointSet, s2: DisjointSet) -> DisjointSet:

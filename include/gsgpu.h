@@ -185,10 +185,20 @@ int gs_comm_info(gs_comm_t* comm, int* rank, int* world, uint64_t* bytes_sent, u
                  uint64_t* overflows);
 int gs_cc_merge_window(gs_cc_t* h, gs_comm_t* comm, int mode);
 
+/* ---- a batch of count windows in one call ----
+ * SummaryBulkAggregation.run over a bounded stream (SummaryBulkAggregation.java:68-90, the Merger
+ * SummaryAggregation.java:106-119): for each window of window_edges edges of src/dst (the last
+ * window may be shorter) gs_cc_fold, then gs_cc_merge_window(h, comm, mode) when comm is not NULL,
+ * else gs_cc_close_window — the per-window host loop run inside the library (one ABI call per batch
+ * instead of two per window). After it returns, the labels are those of the last window's
+ * emission; *windows_out (may be NULL) = windows folded. Stops at the first failure. */
+int gs_cc_fold_windows(gs_cc_t* h, gs_comm_t* comm, int mode, const void* src, const void* dst, uint64_t n,
+                       uint64_t window_edges, uint64_t* windows_out);
+
 /* ---- instrumentation ----
  * kernel ids: 0 fold (young-forest / plain k_fold launches), 1 compress (close_window), 2 merge,
- * 3 export, 4 ring (the steady k_fold_ring launches), 5 route (the routed steady fold's four
- * launches k_sift + k_probe x 2 + k_union_surv, timed as one); fold time = 0 + 4 + 5. */
+ * 3 export, 4 ring (the steady k_fold_ring launches), 5 reserved (a retired steady-fold variant;
+ * always 0); fold time = 0 + 4. */
 enum { GS_K_FOLD = 0, GS_K_COMPRESS = 1, GS_K_MERGE = 2, GS_K_EXPORT = 3, GS_K_RING = 4, GS_K_ROUTE = 5, GS_K_COUNT = 6 };
 /* enable = 0: off; 1: every kernel; GS_TIMING_MASK | (1 << GS_K_x) | ...: only those kernels
  * carry timing events (a timed launch costs ~3 us more dispatch time). Totals reset. */

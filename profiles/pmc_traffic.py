@@ -16,8 +16,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gelly-streaming_amd"))
 from gsgpu._abi import lib_source_sha  # noqa: E402
 
-ROUTED = ("k_sift", "k_probe", "k_union_surv")
-ROUTE_NAME = "routed fold (k_sift + k_probe<B> + k_probe<C> + k_union_surv)"
 
 
 def load(passdir):
@@ -105,7 +103,7 @@ def main():
             ncalls[k] = len(c[k])
     comp = [k for k in agg if "k_compress" in k]
     windows = ncalls[comp[0]] if comp else 1
-    fold = [k for k in agg if "k_fold" in k or any(r in k for r in ROUTED)]
+    fold = [k for k in agg if "k_fold" in k]
     out = {"windows": windows, "kernels": {}}
     for k in agg:
         out["kernels"][k] = dict(agg[k], dispatches=ncalls.get(k))
@@ -129,13 +127,10 @@ def main():
     except Exception:
         pass
     out["lib_source_sha"] = lib_source_sha()
-    # the steady fold per launch (what bench.py's roofline.traffic / requests report): the routed
-    # fold's four kernels per k_sift dispatch, or k_fold_ring
-    routed = [k for k in agg if any(r in k for r in ROUTED)]
-    ring = [k for k in agg if "k_fold_ring" in k]
-    ks, name = (routed, ROUTE_NAME) if routed else (ring, "k_fold_ring")
+    # the steady fold per launch (what bench.py's roofline.traffic / requests report): k_fold_ring
+    ks, name = [k for k in agg if "k_fold_ring" in k], "k_fold_ring"
     if ks:
-        nl = max(ncalls.get([k for k in ks if "k_sift" in k or "k_fold_ring" in k][0]) or 1, 1)
+        nl = max(sum(ncalls.get(k) or 0 for k in ks), 1)
         f_ = sum(agg[k].get("FETCH_SIZE", 0.0) for k in ks) * 1024 / nl
         w_ = sum(agg[k].get("WRITE_SIZE", 0.0) for k in ks) * 1024 / nl
         h_ = sum(agg[k].get("TCC_HIT_sum", 0.0) for k in ks)

@@ -47,20 +47,20 @@ def test_stale_profile_is_dropped(tmp_path):
     from gsgpu._abi import lib_source_sha
     bench, a = _bench()
     prof = {"lib_source_sha": "0" * 16, "scale": a.scale, "id_bits": 32,
-            "steady": {"kernel": bench.ROUTE_NAME, "edges_per_launch": 1 << 24, "hbm_bytes_per_launch": 1e8,
+            "steady": {"kernel": "k_fold_ring", "edges_per_launch": 1 << 24, "hbm_bytes_per_launch": 1e8,
                        "tcc_requests_per_launch": 1e7}}
     p = tmp_path / "t.json"
     p.write_text(json.dumps(prof))
     a.traffic_json = str(p)
-    st, note = bench.steady_profile(a, bench.ROUTE_NAME, 1 << 24)
+    st, note = bench.steady_profile(a, "k_fold_ring", 1 << 24)
     assert st is None and note.startswith("stale")
     prof["lib_source_sha"] = lib_source_sha()
     p.write_text(json.dumps(prof))
-    st, note = bench.steady_profile(a, bench.ROUTE_NAME, 1 << 24)
+    st, note = bench.steady_profile(a, "k_fold_ring", 1 << 24)
     assert st is not None and st["hbm_bytes_per_launch"] == 1e8
-    st, note = bench.steady_profile(a, "k_fold_ring", 1 << 24)          # another kernel: not used
+    st, note = bench.steady_profile(a, "k_fold", 1 << 24)               # another kernel: not used
     assert st is None
-    st, note = bench.steady_profile(a, bench.ROUTE_NAME, 1 << 21)       # another launch size: not used
+    st, note = bench.steady_profile(a, "k_fold_ring", 1 << 21)       # another launch size: not used
     assert st is None
 
 

@@ -286,3 +286,66 @@ def test_c5_eight_ranks_small_windows_latency(oracle):
     steady = sorted(max(lat[r][w] for r in range(P)) for w in range(8, N))
     print("C5 8 ranks (in-process, one GPU): per-window latency p50 %.0f us, p99 %.0f us (max over ranks)"
           % (steady[len(steady) // 2], steady[min(len(steady) - 1, int(len(steady) * 0.99))]))
+
+
+@pytest.mark.parametrize("world,mode", [(1, None), (1, "allgather"), (3, "allgather"), (4, "tree")])
+def test_fold_windows_batch(oracle, world, mode):
+    """gs_cc_fold_windows (the per-window fold + close / merge loop inside the library) ends in the
+    same emission as the oracle's last window; every window is folded, and merged over the comm
+    (RCCL at world 1, the in-process group beyond) — exchanges counted per window."""
+    import torch
+    s, d, cap = _stream(oracle, n=200000, seed=13)
+    W = 25000
+    want = oracle.run(s, d, W, partitions=world, emit=EMIT_CHECKSUM, label_cap=cap, want_final=True)
+    nwin = (s.size + W - 1) // W
+    if mode is None:
+        ds = DisjointSet(cap, id_bits=32, stream=torch.cuda.current_stream())
+        ts = torch.from_numpy(s.astype(np.int32)).cuda()
+        td = torch.from_numpy(d.astype(np.int32)).cuda()
+        assert ds.fold_windows(ts, td, W) == nwin
+        assert ds.checksum()[0] == int(want["checksums"][-1])
+        np.testing.assert_array_equal(ds.dense().astype(np.int64), want["final"])
+        ds.close()
+        return
+    # rank r's slice of window w = the partition _run_local folds; laid out contiguously per rank
+    # so one fold_windows call per rank takes every window
+    per = []
+    for r in range(world):
+        ss, dd, lens = [], [], []
+        for lo in range(0, s.size, W):
+            ln = min(W, s.size - lo)
+            a, b = lo + (ln * r) // world, lo + (ln * (r + 1)) // world
+            ss.append(s[a:b]); dd.append(d[a:b]); lens.append(b - a)
+        per.append((np.concatenate(ss), np.concatenate(dd), lens))
+    if any(len(set(p[2][:-1])) > 1 or p[2][-1] > p[2][0] for p in per):
+        pytest.skip("uneven rank slices: fold_windows takes one window size")
+    comms = [Comm.create(unique_id(), 0, 1, 0)] if world == 1 else Comm.local_group(world, 0)
+    finals, errors, wins = [None] * world, [], [0] * world
+
+    def rank(r):
+        try:
+            ss, dd, lens = per[r]
+            ts = torch.from_numpy(ss.astype(np.int32)).cuda()
+            td = torch.from_numpy(dd.astype(np.int32)).cuda()
+            ds = DisjointSet(cap, id_bits=32, track_marks=True)
+            wins[r] = ds.fold_windows(ts, td, lens[0], comm=comms[r], mode=mode)
+            finals[r] = (ds.checksum()[0], ds.dense().astype(np.int64))
+            ds.close()
+        except Exception as e:
+            errors.append((r, repr(e)))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th), "a rank hung"
+    info = [c.info() for c in comms]
+    for c in comms:
+        c.close()
+    assert not errors, errors
+    assert wins == [nwin] * world
+    assert all(i[4] == nwin for i in info), info            # one exchange per window
+    for r in ([0] if mode == "tree" else range(world)):     # tree: rank 0 is the Merger
+        assert finals[r][0] == int(want["checksums"][-1])
+        np.testing.assert_array_equal(finals[r][1], want["final"])

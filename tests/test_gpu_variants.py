@@ -67,11 +67,7 @@ VARIANTS = {
     "ring_warm_stats": {"GSGPU_RING_MIN_BITS": "20", "GSGPU_FOLD_STATS": "1"},
     "ring_forced_no_warm": {"GSGPU_FOLD_MODE": "ring"},
     "plain_forced": {"GSGPU_FOLD_MODE": "plain", "GSGPU_RING_MIN_BITS": "20"},
-    "route_forced": {"GSGPU_FOLD_MODE": "route"},
-    "route_forced_no_split": {"GSGPU_FOLD_MODE": "route", "GSGPU_YOUNG_SPLIT": "0"},
     "young_split_2^18": {"GSGPU_YOUNG_SPLIT": str(1 << 18)},
-    "xr_forced": {"GSGPU_FOLD_MODE": "xr"},
-    "xr_forced_no_split": {"GSGPU_FOLD_MODE": "xr", "GSGPU_YOUNG_SPLIT": "0"},
 }
 
 
@@ -84,8 +80,7 @@ def test_variant_parity(name):
     assert r["ok"] and not bad, bad
 
 
-@pytest.mark.parametrize("name", ["production", "ring_warm_split_from_2^20", "plain_forced", "ring_warm_stats",
-                                  "route_forced", "xr_forced"])
+@pytest.mark.parametrize("name", ["production", "ring_warm_split_from_2^20", "plain_forced", "ring_warm_stats"])
 def test_fold_variants_verified(name):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0", "--scale", "22",
            "--edge-factor", "16", "--window-log2", "20", "--no-cpu-baseline", "--verify"]

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B of fold variants (GPU box, repo root): one bench step under rocprofv3 --kernel-trace
-# per environment, then the steady windows' per-kernel means (tools/route_windows.py).
+# per environment, then the steady windows' per-kernel means (tools/steady_windows.py).
 # usage: bash tools/r03_ab.sh <tag> "ENV=1 ENV2=x" "..."   ("-" = production)
 set -u
 TAG=${1:-r03_ab}; shift
@@ -19,6 +19,6 @@ for ENVS in "$@"; do
   if [ $rc -ne 0 ]; then tail -5 "$OUT/v$i.log"; exit 3; fi
   grep -o '"ms_per_step": [0-9.]*' "$OUT/v$i.log" | head -1
   f=$(find "$OUT/v$i" -name "*kernel_trace.csv" | head -1)
-  python3 tools/route_windows.py "$f" 13
+  python3 tools/steady_windows.py "$f" 13
 done
 exit 0

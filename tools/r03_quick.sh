@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-3 quick look (GPU box, repo root): headline parity vs the 64-window fixture, forced-route
-# variant parity, a short bench and a kernel trace. Every GPU step has its own limit; a fault,
+# Round-3 quick look (GPU box, repo root): headline parity vs the 64-window fixture, variant
+# parity (production), a short bench and a kernel trace. Every GPU step has its own limit; a fault,
 # abort or timeout stops the script. usage: bash tools/r03_quick.sh <tag>
 set -u
 TAG=${1:-r03}
@@ -11,8 +11,8 @@ stop() { case "$1" in 0) return 1;; *) return 0;; esac; }
 timeout -k 10 300 python -u tests/headline_check.py --steps 2 > "$OUT/headline.json" 2> "$OUT/headline.err"
 rc=$?; echo "headline rc=$rc"; cat "$OUT/headline.json"; tail -4 "$OUT/headline.err"
 if stop $rc; then exit 3; fi
-GSGPU_FOLD_MODE=route timeout -k 10 300 python -u tests/variant_check.py > "$OUT/variant_route.json" 2> "$OUT/variant_route.err"
-rc=$?; echo "variant route rc=$rc"; cut -c1-400 "$OUT/variant_route.json"; tail -3 "$OUT/variant_route.err"
+timeout -k 10 300 python -u tests/variant_check.py > "$OUT/variant.json" 2> "$OUT/variant.err"
+rc=$?; echo "variant rc=$rc"; cut -c1-400 "$OUT/variant.json"; tail -3 "$OUT/variant.err"
 if stop $rc; then exit 3; fi
 timeout -k 10 300 python -u bench.py --steps 3 --no-cpu-baseline > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; echo "bench rc=$rc"; cut -c1-600 "$OUT/bench.json"; tail -3 "$OUT/bench.err"

@@ -1,5 +1,5 @@
 """Per-window durations of the steady fold's kernels from a rocprofv3 kernel trace (last step):
-usage: python tools/route_windows.py <kernel_trace.csv> [first_window]"""
+usage: python tools/steady_windows.py <kernel_trace.csv> [first_window]"""
 import csv
 import sys
 from collections import defaultdict
@@ -8,7 +8,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 first = int(sys.argv[2]) if len(sys.argv) > 2 else 13
 ks = sorted(((r["Kernel_Name"].split("(")[0].replace("void ", "").split("::")[-1], int(r["Start_Timestamp"]),
              int(r["End_Timestamp"])) for r in rows), key=lambda x: x[1])
-HEADS = ("k_sift", "k_fold_ring", "k_fold_xr")
+HEADS = ("k_fold_ring",)
 heads = [i for i, k in enumerate(ks) if k[0].startswith(HEADS)]
 last = heads[-63:]                                  # windows 2..64 of the last step
 tot = defaultdict(float)
