@@ -78,6 +78,9 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = the C-ABI exchange over RCCL/xGMI (production); gloo = the Python exchange "
                          "over host staging (several ranks on one GPU, tests)")
+    ap.add_argument("--exchange-world1", action="store_true",
+                    help="one GPU through the C-ABI exchange (RCCL with one rank): the per-window cost of "
+                         "export + collective + delta fold + close that a multi-GPU window adds (a measurement line)")
     ap.add_argument("--merge", default="allgather", choices=["allgather", "gather", "tree"],
                     help="multi-rank CombineCC: allgather = replicated global summary (every rank folds every "
                          "delta); gather = windowAll gather to rank 0 (SummaryBulkAggregation.java:81); tree = "
@@ -152,11 +155,14 @@ def main():
         fsrc, fdst = src, dst
 
     stream = torch.cuda.current_stream()
-    marks = world > 1 and (a.merge == "allgather" or a.dist_backend == "nccl" or rank != 0)
+    marks = (world > 1 and (a.merge == "allgather" or a.dist_backend == "nccl" or rank != 0)) or a.exchange_world1
     ds = gsgpu.DisjointSet(V, id_bits=a.id_bits, device=local, track_marks=marks, stream=stream)
     comm = tree = None
     if world > 1 and a.dist_backend == "nccl":
         comm = gsgpu.Comm.from_process_group(local)                  # C ABI: gs_comm_create (RCCL)
+    elif a.exchange_world1:
+        from gsgpu.comm import unique_id
+        comm = gsgpu.Comm.create(unique_id(), 0, 1, local)
     elif world > 1:
         sys.path.insert(0, os.path.join(ROOT, "tests"))          # test mode: the Python exchange model
         from gloo_tree import AllgatherMerge, GatherMerge, TreeMerge
@@ -312,7 +318,8 @@ def main():
             "config": {
                 "workload": "%s_%s%d_ef%d_window%s%s%s" % (a.workload.split("_")[0], "er" if a.kind == "er" else "rmat",
                                                          a.scale, a.edge_factor, _pow2(W_glob),
-                                                         "_int64" if a.id_bits == 64 else "",
+                                                         ("_int64" if a.id_bits == 64 else "") +
+                                                         ("_xchg1" if a.exchange_world1 else ""),
                                                          "_hostinput" if a.host_input else "") +
                             ("_emithost" if a.emit_host else ""),
                 "scale": a.scale, "vertices": V, "edge_factor": a.edge_factor,
@@ -321,7 +328,8 @@ def main():
                 "input": "pinned host memory (PCIe-inclusive)" if a.host_input else "HBM",
                 "parallelism": "1 subtask per GPU x %d, %s" % (
                     world, ("%s merge, %s" % (a.merge, "C ABI over RCCL" if comm is not None else "torch.distributed gloo"))
-                    if world > 1 else "no merge"),
+                    if world > 1 else ("%s merge through the C-ABI exchange at world 1 (RCCL, one rank)" % a.merge
+                                       if a.exchange_world1 else "no merge")),
                 "emission": ("per window, canonical min-id labels resident in HBM, and the delta (pairs new or changed "
                              "since the last window) copied to pinned host memory (gs_cc_emit_delta)") if a.emit_host
                             else "per window, canonical min-id labels resident in HBM",

@@ -71,6 +71,11 @@ struct gs_cc {
     uint32_t* elab = nullptr;            // delta emission: the labels last emitted (kInvalid: never)
     uint32_t* derr = nullptr;            // derr[0] deferred device error flags; derr[1..5] giant state
     uint32_t* psamp = nullptr;           // 2 x kPickSamples labels a full-pass close recorded (k_compress)
+    // a multi-GPU window whose exchange is still to be verified (comm.hip: the speculative
+    // all-gather's delta sizes are checked lazily, so the host never waits for them per window):
+    // every call that consumes the emission runs it first (cc_settle)
+    int (*settle_fn)(void*) = nullptr;
+    void* settle_ctx = nullptr;
     unsigned long long* dscratch = nullptr;  // reduction outputs (8 words)
     unsigned long long* hscratch = nullptr;  // pinned mirror
     void* stage = nullptr;               // host->device staging: 2 slots x (src, dst) x staging_edges ids
@@ -719,7 +724,7 @@ int cc_info(gs_cc_t* h, CcInfo* out) {
     *out = CcInfo{h->cap, h->device, h->stream, h->mark_buf != nullptr, h->sparse, h->mark != nullptr, h->reset_gen};
     return GS_OK;
 }
-static int export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long* counter);
+static int export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long* counter, uint64_t expect = ~0ull);
 // Fold the slots of a speculative all-gather (comm.hip): every slot but `skip`, pairs up to
 // min(count, cap) read on the device; marking is off for these folds (the others' deltas are theirs
 // to export). Big slots (young windows: components not yet joined) fold a short head of every
@@ -744,13 +749,27 @@ int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int ns
 }
 void cc_count_folded(gs_cc_t* h, uint64_t n) { h->edges_since_reset += n; }
 
-int cc_export_async(gs_cc_t* h, void* pairs, uint64_t cap, unsigned long long* dcount) {
+void cc_set_settle(gs_cc_t* h, int (*fn)(void*), void* ctx) {
+    h->settle_fn = fn;
+    h->settle_ctx = ctx;
+}
+
+int cc_settle(gs_cc_t* h) {
+    if (!h || !h->settle_fn) return GS_OK;
+    int (*fn)(void*) = h->settle_fn;
+    void* ctx = h->settle_ctx;
+    h->settle_fn = nullptr;                          // the settle itself folds and closes
+    h->settle_ctx = nullptr;
+    return fn(ctx);
+}
+
+int cc_export_async(gs_cc_t* h, void* pairs, uint64_t cap, unsigned long long* dcount, uint64_t expect) {
     GS_TRY(check(h));
     if (!h->mark_buf || h->sparse) return fail(GS_ERR_UNSUPPORTED, "export: no marks on this handle");
     // (cap may be smaller than the log: the pending tail stays for the next export; the count word
     // receives the whole pending number, so the caller can tell)
     DeviceGuard g(h->device);
-    return export_launch(h, pairs, cap, dcount);
+    return export_launch(h, pairs, cap, dcount, expect);
 }
 }  // namespace gsgpu
 
@@ -866,6 +885,7 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
 
 int gs_cc_destroy(gs_cc_t* h) {
     if (!h) return GS_OK;
+    (void)cc_settle(h);                          // peers may wait for this rank in a tail round
     DeviceGuard g(h->device);
     if (h->own) (void)hipStreamSynchronize(h->own);
     if (h->stream && h->stream != h->own) (void)hipStreamSynchronize(h->stream);
@@ -908,9 +928,10 @@ int gs_cc_destroy(gs_cc_t* h) {
 
 int gs_cc_reset(gs_cc_t* h) {
     GS_TRY(check(h));
+    GS_TRY(cc_settle(h));                      // a pending multi-GPU window first (comm.hip)
     DeviceGuard g(h->device);
     GS_HIP(hipMemsetAsync(h->parent, 0xFF, (size_t)h->cap * sizeof(uint32_t), h->stream));
-    if (h->mark_ctr) GS_HIP(hipMemsetAsync(h->mark_ctr, 0, 2 * sizeof(unsigned long long), h->stream));
+    if (h->mark_ctr) GS_HIP(hipMemsetAsync(h->mark_ctr, 0, 3 * sizeof(unsigned long long), h->stream));
     GS_HIP(hipMemsetAsync(h->gbits, 0, mark_bytes(h->cap), h->stream));
     GS_HIP(hipMemsetAsync(h->sbits, 0, mark_bytes(h->cap), h->stream));
     GS_HIP(hipMemsetAsync(h->cbits, 0, mark_bytes(h->cap), h->stream));
@@ -960,22 +981,30 @@ int gs_cc_get_stream(gs_cc_t* h, void** s) {
 
 int gs_cc_sync(gs_cc_t* h) {
     GS_TRY(check(h));
+    GS_TRY(cc_settle(h));                      // a pending multi-GPU window first (comm.hip)
     DeviceGuard g(h->device);
     return sync_and_check(h);
 }
 
+// A fold settles a pending multi-GPU window first: its tail pairs (foreign unions folded with marking
+// paused) must land before this fold's hooks are exported, or not under their roots at all
+// (comm.hip merge_allgather). gs_cc_fold_windows folds without it: its merge_window exports the new
+// window's hooks BEFORE settling the previous window, so its host never waits per window.
 int gs_cc_fold(gs_cc_t* h, const void* src, const void* dst, uint64_t n) {
     GS_TRY(check(h));
+    GS_TRY(cc_settle(h));
     return fold_impl(h, src, dst, n, false, h->cfg.id_bits);
 }
 
 int gs_cc_fold_pairs(gs_cc_t* h, const void* pairs, uint64_t n) {
     GS_TRY(check(h));
+    GS_TRY(cc_settle(h));
     return fold_impl(h, pairs, nullptr, n, true, h->cfg.id_bits);
 }
 
 int gs_cc_fold_pairs32(gs_cc_t* h, const void* pairs, uint64_t n) {
     GS_TRY(check(h));
+    GS_TRY(cc_settle(h));
     h->fold_timer = GS_K_MERGE;          // a partial summary: timed as CombineCC, not UpdateCC
     const int rc = fold_impl(h, pairs, nullptr, n, true, 32);
     h->fold_timer = GS_K_FOLD;
@@ -985,6 +1014,8 @@ int gs_cc_fold_pairs32(gs_cc_t* h, const void* pairs, uint64_t n) {
 int gs_cc_merge(gs_cc_t* into, gs_cc_t* from) {
     GS_TRY(check(into));
     GS_TRY(check(from));
+    GS_TRY(cc_settle(into));
+    GS_TRY(cc_settle(from));
     if (into == from) return GS_OK;
     if (into->device != from->device) return fail(GS_ERR_UNSUPPORTED, "gs_cc_merge: summaries on different devices");
     if (into->sparse != from->sparse) return fail(GS_ERR_UNSUPPORTED, "gs_cc_merge: sparse-id and dense-id summaries do not mix");
@@ -1025,6 +1056,8 @@ int gs_cc_merge(gs_cc_t* into, gs_cc_t* from) {
 int gs_cc_combine(gs_cc_t* s1, gs_cc_t* s2, gs_cc_t** result) {
     GS_TRY(check(s1));
     GS_TRY(check(s2));
+    GS_TRY(cc_settle(s1));
+    GS_TRY(cc_settle(s2));
     if (!result) return fail(GS_ERR_INVALID, "gs_cc_combine: null result");
     uint64_t c1 = 0, c2 = 0;
     GS_TRY(gs_cc_stats(s1, &c1, nullptr));
@@ -1036,6 +1069,7 @@ int gs_cc_combine(gs_cc_t* s1, gs_cc_t* s2, gs_cc_t** result) {
 
 int gs_cc_close_window(gs_cc_t* h) {
     GS_TRY(check(h));
+    GS_TRY(cc_settle(h));                      // a pending multi-GPU window first (comm.hip)
     DeviceGuard g(h->device);
     return compress_impl(h);
 }
@@ -1052,21 +1086,23 @@ int gs_cc_fold_windows(gs_cc_t* h, gs_comm_t* comm, int mode, const void* src, c
     uint64_t w = 0;
     for (uint64_t off = 0; off < n; off += window_edges, ++w) {
         const uint64_t m = std::min(window_edges, n - off);
-        GS_TRY(gs_cc_fold(h, a + off * esz, b + off * esz, m));
+        GS_TRY(fold_impl(h, a + off * esz, b + off * esz, m, false, h->cfg.id_bits));   // (no settle: above)
         GS_TRY(comm ? gs_cc_merge_window(h, comm, mode) : gs_cc_close_window(h));
         if (windows_out) *windows_out = w + 1;
     }
-    return GS_OK;
+    return cc_settle(h);                             // the last window's exchange verified
 }
 
 int gs_cc_stats(gs_cc_t* h, uint64_t* nv, uint64_t* nc) {
     GS_TRY(check(h));
+    GS_TRY(cc_settle(h));                      // a pending multi-GPU window first (comm.hip)
     DeviceGuard g(h->device);
     return stats_impl(h, false, nv, nc, nullptr);
 }
 
 int gs_cc_checksum(gs_cc_t* h, uint64_t* sum, uint64_t* nv, uint64_t* nc) {
     GS_TRY(check(h));
+    GS_TRY(cc_settle(h));                      // a pending multi-GPU window first (comm.hip)
     DeviceGuard g(h->device);
     GS_TRY(compress_impl(h));
     return stats_impl(h, true, nv, nc, sum);
@@ -1074,6 +1110,7 @@ int gs_cc_checksum(gs_cc_t* h, uint64_t* sum, uint64_t* nv, uint64_t* nc) {
 
 int gs_cc_emit_dense(gs_cc_t* h, void* labels, uint64_t n) {
     GS_TRY(check(h));
+    GS_TRY(cc_settle(h));                      // a pending multi-GPU window first (comm.hip)
     if (n && !labels) return fail(GS_ERR_INVALID, "gs_cc_emit_dense: null output");
     if (h->sparse) return fail(GS_ERR_UNSUPPORTED, "gs_cc_emit_dense: sparse-id summary (use gs_cc_emit_pairs)");
     DeviceGuard g(h->device);
@@ -1101,6 +1138,7 @@ int gs_cc_emit_dense(gs_cc_t* h, void* labels, uint64_t n) {
 
 int gs_cc_emit_pairs(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uint64_t* n_out) {
     GS_TRY(check(h));
+    GS_TRY(cc_settle(h));                      // a pending multi-GPU window first (comm.hip)
     if (!n_out) return fail(GS_ERR_INVALID, "gs_cc_emit_pairs: null n_out");
     if (cap && (!vertices || !labels)) return fail(GS_ERR_INVALID, "gs_cc_emit_pairs: null output");
     DeviceGuard g(h->device);
@@ -1156,6 +1194,7 @@ int gs_cc_emit_pairs(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uin
 
 int gs_cc_emit_delta(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uint64_t* n_out) {
     GS_TRY(check(h));
+    GS_TRY(cc_settle(h));                      // a pending multi-GPU window first (comm.hip)
     if (!n_out) return fail(GS_ERR_INVALID, "gs_cc_emit_delta: null n_out");
     if (cap && (!vertices || !labels)) return fail(GS_ERR_INVALID, "gs_cc_emit_delta: null output");
     if (h->sparse) return fail(GS_ERR_UNSUPPORTED, "gs_cc_emit_delta: sparse-id summary (use gs_cc_emit_pairs)");
@@ -1224,6 +1263,7 @@ int gs_cc_find(gs_cc_t* h, const void* ids, void* roots, uint64_t n) {
 
 int gs_cc_find_flags(gs_cc_t* h, const void* ids, void* roots, uint8_t* found, uint64_t n) {
     GS_TRY(check(h));
+    GS_TRY(cc_settle(h));                      // a pending multi-GPU window first (comm.hip)
     if (n == 0) return GS_OK;
     if (!ids || !roots) return fail(GS_ERR_INVALID, "gs_cc_find: null buffer");
     DeviceGuard g(h->device);
@@ -1261,21 +1301,24 @@ int gs_cc_find_flags(gs_cc_t* h, const void* ids, void* roots, uint8_t* found, u
 
 int gs_cc_labels_device(gs_cc_t* h, const void** p) {
     GS_TRY(check(h));
+    GS_TRY(cc_settle(h));                      // a pending multi-GPU window first (comm.hip)
     if (!p) return fail(GS_ERR_INVALID, "null out");
     if (h->sparse) return fail(GS_ERR_UNSUPPORTED, "gs_cc_labels_device: sparse-id summary (labels are per slot)");
     *p = h->parent;
     return GS_OK;
 }
 
-int gsgpu::export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long* counter) {
-    // the pending hook-log entries -> (v, root(v)) pairs; the grid is fixed (the count is on the
-    // device): a steady window's few thousand hooks need a few workgroups, a young one's millions
-    // are strided over 1024
+int gsgpu::export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long* counter, uint64_t expect) {
+    // the pending hook-log entries -> (v, root(v)) pairs; the count is on the device, so the grid
+    // follows the caller's expectation (the exchange: twice its last delta), strided past it: a
+    // steady window's few thousand hooks need a few workgroups, a young one's millions up to 1024.
+    // (Every workgroup counts itself once on one word to let the last one advance the cursor:
+    // 1024 of them cost ~11 us per export, r03_xchg2.)
     {
+        const unsigned grid = expect == ~0ull ? 1024u : (unsigned)std::min<uint64_t>(std::max<uint64_t>((expect + 255) / 256, 8), 1024);
         KTimer t(h, GS_K_EXPORT);
-        klaunch(k_export_log, dim3(1024), dim3(256), h->stream, t.start(), nullptr, (const uint32_t*)h->mark_buf,
-                (const unsigned long long*)h->mark_ctr, (const uint32_t*)h->parent, (uint32_t*)out, cap, counter);
-        klaunch(k_log_advance, dim3(1), dim3(1), h->stream, nullptr, t.stop(), h->mark_ctr, cap);
+        klaunch(k_export_log, dim3(grid), dim3(256), h->stream, t.start(), t.stop(), (const uint32_t*)h->mark_buf,
+                h->mark_ctr, (const uint32_t*)h->parent, (uint32_t*)out, cap, counter);
     }
     GS_HIP(hipGetLastError());
     return GS_OK;
@@ -1289,6 +1332,7 @@ static int export_check(gs_cc_t* h, const char* fn) {
 
 int gs_cc_export_marks(gs_cc_t* h, void* pairs, uint64_t cap, uint64_t* n_out) {
     GS_TRY(check(h));
+    GS_TRY(cc_settle(h));                      // a pending multi-GPU window first (comm.hip)
     if (!n_out) return fail(GS_ERR_INVALID, "gs_cc_export_marks: null n_out");
     GS_TRY(export_check(h, "gs_cc_export_marks"));
     if (cap && !pairs) return fail(GS_ERR_INVALID, "gs_cc_export_marks: null output");
@@ -1315,6 +1359,7 @@ int gs_cc_export_marks(gs_cc_t* h, void* pairs, uint64_t cap, uint64_t* n_out) {
 
 int gs_cc_export_marks_async(gs_cc_t* h, void* pairs, uint64_t cap, void* dev_count) {
     GS_TRY(check(h));
+    GS_TRY(cc_settle(h));                      // a pending multi-GPU window first (comm.hip)
     GS_TRY(export_check(h, "gs_cc_export_marks_async"));
     if (!dev_count || !is_device_pointer(dev_count) || (cap && (!pairs || !is_device_pointer(pairs))))
         return fail(GS_ERR_INVALID, "gs_cc_export_marks_async: pairs and dev_count must be device pointers");

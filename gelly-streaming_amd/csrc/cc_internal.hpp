@@ -14,7 +14,10 @@ struct CcInfo {
     uint64_t reset_gen;      // gs_cc_reset calls so far: a new stream starts when it changes
 };
 int cc_info(gs_cc_t* h, CcInfo* out);
-int cc_export_async(gs_cc_t* h, void* pairs, uint64_t cap, unsigned long long* dcount);
+int cc_export_async(gs_cc_t* h, void* pairs, uint64_t cap, unsigned long long* dcount, uint64_t expect = ~0ull);
 int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int nslots, int skip, uint64_t cap);
 void cc_count_folded(gs_cc_t* h, uint64_t n);
+// a pending exchange verification of the handle's last window (comm.hip): cc_settle runs it once
+void cc_set_settle(gs_cc_t* h, int (*fn)(void*), void* ctx);
+int cc_settle(gs_cc_t* h);
 }  // namespace gsgpu

@@ -547,7 +547,7 @@ __device__ __forceinline__ void union_group(const FoldArgs& f, const uint32_t (&
 template <bool MARK, bool STATS, int EPT>
 __device__ __forceinline__ void union_group_g(const FoldArgs& f, const uint32_t (&u)[EPT], const uint32_t (&v)[EPT],
                                               const bool (&ok)[EPT], const uint32_t (&gflag)[EPT], uint32_t gR,
-                                              FoldStats& st) {
+                                              FoldStats& st, uint32_t* marks_out = nullptr) {
     uint32_t pu[EPT], pv[EPT];
     // one endpoint in the giant, the other x > gR: claim x straight under gR with a CAS from
     // kInvalid instead of gathering parent[x] first. Success = x was never touched, and hanging a
@@ -578,7 +578,12 @@ __device__ __forceinline__ void union_group_g(const FoldArgs& f, const uint32_t 
             m[k] = ok[k] ? union_edge<MARK, STATS>(f.parent, f.sbits, u[k], v[k], pu[k], pv[k], &st, f.halve != 0) : kInvalid;
         }
     }
-    if (MARK) log_append<EPT>(f.mark, f.mark_len, m);
+    if (MARK && marks_out) {                         // the caller appends them (ring_flush_final)
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) marks_out[k] = m[k];
+    } else if (MARK) {
+        log_append<EPT>(f.mark, f.mark_len, m);
+    }
 }
 
 // Filter, parent gathers and unions of one thread's EPT edges (ids already range-checked;
@@ -719,6 +724,50 @@ __device__ __forceinline__ void ring_flush(const FoldArgs& f, uint2* ring, uint3
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+}
+
+// The last flush of every wave's ring at the end of k_fold_ring. With the hook log on (MARK), the
+// marks of the whole workgroup go into the log with ONE global atomic: at a launch's end every wave
+// of the chip flushes at once, and a log append per wave (4096 returning atomics on one word)
+// serialised there (~46 us per launch). All threads of the workgroup must call it.
+template <bool MARK, bool STATS>
+__device__ __forceinline__ void ring_flush_final(const FoldArgs& f, uint2* ring, uint32_t cnt, FoldStats& st, uint32_t gR,
+                                                 uint32_t* s_cnt, unsigned long long* s_base) {
+    if (!MARK) {
+        ring_flush<MARK, STATS>(f, ring, cnt, 0, st, gR);
+        return;
+    }
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x == 0) *s_cnt = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    uint32_t mk[2] = {kInvalid, kInvalid};           // the ring holds at most 2 x 64 entries here
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        if (cnt == 0) break;                         // uniform
+        const uint32_t take = min(cnt, 64u);
+        const uint32_t at = cnt - take;
+        const bool ok1 = (uint32_t)lane < take;
+        const uint2 e = ok1 ? ring[at + lane] : make_uint2(0u, 0u);
+        const uint32_t u[1] = {e.x & 0x7FFFFFFFu}, v[1] = {e.y & 0x7FFFFFFFu};
+        const uint32_t gf[1] = {(e.x >> 31) | ((e.y >> 31) << 1)};
+        const bool ok[1] = {ok1};
+        union_group_g<MARK, STATS, 1>(f, u, v, ok, gf, gR, st, &mk[it]);
+        cnt = at;
+    }
+    __syncthreads();                                 // s_cnt is zeroed
+    const uint64_t lt = (1ull << lane) - 1;
+    const uint64_t b0 = __ballot(mk[0] != kInvalid), b1 = __ballot(mk[1] != kInvalid);
+    const uint32_t c = (uint32_t)__popcll(b0) + (uint32_t)__popcll(b1);
+    uint32_t off = 0;
+    if (lane == 0 && c) off = atomicAdd(s_cnt, c);   // LDS: the wave's place in the workgroup's batch
+    off = __shfl(off, 0, 64);
+    __syncthreads();
+    if (threadIdx.x == 0) *s_base = *s_cnt ? atomicAdd(f.mark_len, (unsigned long long)*s_cnt) : 0ull;
+    __syncthreads();
+    const unsigned long long base = *s_base + off;
+    if (mk[0] != kInvalid) f.mark[base + __popcll(b0 & lt)] = mk[0];
+    if (mk[1] != kInvalid) f.mark[base + __popcll(b0) + __popcll(b1 & lt)] = mk[1];
 }
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
@@ -869,7 +918,9 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
         cnt += wtot;
         if (cnt >= 64) ring_flush<MARK, STATS>(f, ring, cnt, cnt - 64, st, gR);
     }
-    ring_flush<MARK, STATS>(f, ring, cnt, 0, st, gR);
+    __shared__ uint32_t s_mcnt;
+    __shared__ unsigned long long s_mbase;
+    ring_flush_final<MARK, STATS>(f, ring, cnt, st, gR, &s_mcnt, &s_mbase);
     if (STATS) {
         atomicAdd(&f.stats[0], nvalid);
         atomicAdd(&f.stats[1], nvalid - nkept);
@@ -1571,9 +1622,9 @@ __global__ __launch_bounds__(kTileThreads) void k_delta_scatter(const uint32_t* 
 // the parent words at hook time: the receiver's unions then all point at the few component minima
 // its own forest already holds (short walks, no hook chains to contend on). ctr = [length, read
 // cursor]; the pending entries are [cursor, length); *count receives their number; at most cap
-// pairs are written, the rest stay pending (k_log_advance). One thread per entry: the export
+// pairs are written, the rest stay pending (the last workgroup advances the cursor). One thread per entry: the export
 // costs O(hooks) instead of a scan of a V-bit mark bitmap (23 us per RMAT-26 window).
-__global__ __launch_bounds__(256) void k_export_log(const uint32_t* __restrict__ log, const unsigned long long* __restrict__ ctr,
+__global__ __launch_bounds__(256) void k_export_log(const uint32_t* __restrict__ log, unsigned long long* __restrict__ ctr,
                                                     const uint32_t* __restrict__ parent, uint32_t* __restrict__ pairs,
                                                     uint64_t cap, unsigned long long* __restrict__ count) {
     const unsigned long long len = ctr[0], rd = ctr[1];
@@ -1586,13 +1637,18 @@ __global__ __launch_bounds__(256) void k_export_log(const uint32_t* __restrict__
         pairs[2 * i] = v;
         pairs[2 * i + 1] = find_root_ro(parent, v);
     }
-}
-// after k_export_log (stream order): consume what it wrote; an emptied log restarts at 0
-__global__ void k_log_advance(unsigned long long* __restrict__ ctr, uint64_t cap) {
-    const unsigned long long len = ctr[0], rd = ctr[1];
-    const unsigned long long take = (len - rd) < cap ? (len - rd) : cap;
-    if (rd + take == len) { ctr[0] = 0; ctr[1] = 0; }
-    else ctr[1] = rd + take;
+    // consume what was written, by the last workgroup to finish (ctr[2] counts finished workgroups;
+    // each has read ctr before it counts itself): an emptied log restarts at 0. (Was a second
+    // one-thread launch, ~5 us per exchanged window.)
+    __syncthreads();
+    if (threadIdx.x == 0 && len >= rd) {             // (the condition orders the ctr reads first)
+        const unsigned long long done = atomicAdd(&ctr[2], 1ull);
+        if (done == gridDim.x - 1) {
+            if (rd + take == len) { ctr[0] = 0; ctr[1] = 0; }
+            else ctr[1] = rd + take;
+            ctr[2] = 0;
+        }
+    }
 }
 
 }  // namespace gsgpu

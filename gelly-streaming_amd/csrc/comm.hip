@@ -40,13 +40,6 @@ __global__ void k_pad_pairs(uint2* __restrict__ buf, uint64_t n, uint64_t m) {
         buf[i] = p;
 }
 
-// the count words of P exchange slots -> out[0..P) (one small D2H copy for the host's check)
-__global__ void k_slot_counts(const uint32_t* __restrict__ slots, uint64_t slot_words, int P,
-                              unsigned long long* __restrict__ out) {
-    for (int q = threadIdx.x; q < P; q += blockDim.x)
-        out[q] = *reinterpret_cast<const unsigned long long*>(slots + (uint64_t)q * slot_words);
-}
-
 // ---- in-process group (tests): threads on one device ----
 struct LocalGroup {
     explicit LocalGroup(int w) : world(w), send(w, nullptr), ev(w, nullptr), done(w, nullptr), box((size_t)w * w) {}
@@ -99,6 +92,8 @@ struct gs_comm {
     // exchange buffers (device), sized at the first merge for the handle's capacity
     uint64_t cap_pairs = 0;
     uint32_t* sendbuf = nullptr;                   // cap_pairs pairs (2 x the handle's capacity)
+    uint32_t* sendbuf2 = nullptr;                  // allgather: exports alternate between the two, so a
+                                                   // pending window's tail survives the next export
     uint32_t* recvbuf = nullptr;                   // exact rounds: grows to world * m pairs
     size_t recv_bytes = 0;
     uint32_t* slotbuf = nullptr;                   // speculative rounds: world count-headed slots
@@ -112,6 +107,12 @@ struct gs_comm {
     uint64_t reset_gen = 0;                        // the handle's reset generation of the current stream
     bool broken = false;                           // an exchange failed: the communicator is unusable
     hipEvent_t ev_counts = nullptr;                // the speculative round's counts are on the host
+    hipEvent_t ev_slots = nullptr;                 // the speculative round's slots have arrived
+    hipStream_t side = nullptr;                    // copies the slots' count words to the host
+    bool pending = false;                          // a speculative window not yet verified (settle_allgather)
+    uint64_t pend_slot = 0;                        // its slot size S
+    uint32_t* pend_buf = nullptr;                  // its export (the tail pairs [S, n) are sent from it)
+    uint64_t last_delta = 0;                       // the largest delta of the last verified window
     uint64_t bytes_sent = 0, bytes_recv = 0, exchanges = 0, overflows = 0;
 };
 
@@ -234,11 +235,13 @@ int prepare(gs_comm_t* c, gs_cc_t* h, CcInfo* info) {
     const uint64_t need = 2ull * info->cap;        // an export never exceeds 2 x capacity pairs
     if (c->cap_pairs < need) {
         if (c->sendbuf) (void)hipFree(c->sendbuf);
-        c->sendbuf = nullptr;
-        if (hipMalloc(&c->sendbuf, (size_t)(need + 1) * 8) != hipSuccess) {     // + a count word
+        if (c->sendbuf2) (void)hipFree(c->sendbuf2);
+        c->sendbuf = c->sendbuf2 = nullptr;
+        if (hipMalloc(&c->sendbuf, (size_t)(need + 1) * 8) != hipSuccess ||                  // + a count word
+            hipMalloc(&c->sendbuf2, (size_t)(need + 1) * 8) != hipSuccess) {
             (void)hipGetLastError();
             c->cap_pairs = 0;
-            return fail(GS_ERR_NOMEM, "exchange buffer of %llu pairs", (unsigned long long)need);
+            return fail(GS_ERR_NOMEM, "exchange buffers of %llu pairs", (unsigned long long)need);
         }
         c->cap_pairs = need;
     }
@@ -319,36 +322,32 @@ uint64_t next_slot(const gs_comm_t* c, uint64_t maxc) {
 // Speculative single-collective round (once a slot size S is known): every rank exports its WHOLE
 // delta behind a count word, right after its own fold, and the first S pairs of every rank are
 // all-gathered in ONE RCCL call; the others' slots are folded and the window is closed with the
-// counts read on the device while the host checks the counts it copied back. A delta larger than
-// S (every rank sees every count, so all agree) has its tail sent in one more all-gather, from the
-// same export: the pairs must be the exporter's state right after its own fold — re-exported
-// after folding the others' slots (marking paused), a root of its own that a foreign pair hooked
-// would vanish from its pairs. The first window of a stream runs the exact round and sizes S.
-int merge_allgather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
+// counts read on the device. The host does NOT wait for the counts here: the window is left
+// pending (settle_allgather) and verified at the start of the next merge_window, or by any call
+// that consumes the emission first (cc_settle: stats, checksum, emit_*, find, sync, ...), by
+// which time the counts are long on the host — so the host can enqueue the next window's fold
+// while this window's exchange and close still run. A delta larger than S (every rank sees every
+// count, so all agree) has its tail sent in one more all-gather, from the same export: the pairs
+// must be the exporter's state right after its own fold — re-exported after folding the others'
+// slots (marking paused), a root of its own that a foreign pair hooked would vanish from its
+// pairs. A tail folded after the next window's local fold is still exact for every emission a
+// caller can observe: the next emission closes after it, and the pending window's own emission is
+// only readable through a call that settles first. The first window of a stream runs the exact
+// round and sizes S.
+int settle_allgather(gs_comm_t* c, bool close) {
+    if (!c->pending) return GS_OK;
+    c->pending = false;
+    gs_cc_t* h = c->bound;
+    CcInfo in;
+    GS_TRY(cc_info(h, &in));
+    DeviceGuard g(in.device);
     const int P = c->world;
     hipStream_t s = in.stream;
-    uint64_t maxc = 0;
-    const uint64_t S = c->spec_slot;
-    if (S == 0) {
-        GS_TRY(exchange_exact(c, h, in, &maxc));
-        GS_TRY(gs_cc_close_window(h));
-        c->spec_slot = next_slot(c, maxc);
-        return GS_OK;
-    }
-    const uint64_t slot_words = 2 + 2 * S;                       // [u64 count][S pairs]
-    uint32_t* send = c->sendbuf;
-    GS_TRY(cc_export_async(h, send + 2, c->cap_pairs - 1, reinterpret_cast<unsigned long long*>(send)));
-    GS_TRY(ensure(reinterpret_cast<void**>(&c->slotbuf), &c->slot_bytes, (size_t)P * slot_words * 4, s));
-    GS_TRY(allgather(c, send, c->slotbuf, slot_words * 4, s));
-    hipLaunchKernelGGL(k_slot_counts, dim3(1), dim3(64), 0, s, (const uint32_t*)c->slotbuf, slot_words, P, c->dcnt);
-    GS_HIP(hipGetLastError());
-    GS_HIP(hipMemcpyAsync(c->hcnt, c->dcnt, P * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    GS_HIP(hipEventRecord(c->ev_counts, s));
-    GS_TRY(cc_fold_slots(h, c->slotbuf, slot_words, P, c->rank, S));
-    GS_TRY(gs_cc_close_window(h));                              // optimistic: no delta exceeded S
-    GS_HIP(hipEventSynchronize(c->ev_counts));                  // the GPU folds and closes meanwhile
+    const uint64_t S = c->pend_slot;
+    uint32_t* send = c->pend_buf;
+    GS_HIP(hipEventSynchronize(c->ev_counts));      // normally complete long ago
     std::vector<uint64_t> tail(P, 0);
-    uint64_t folded = 0, mt = 0;
+    uint64_t folded = 0, mt = 0, maxc = 0;
     for (int q = 0; q < P; ++q) {
         const uint64_t n = c->hcnt[q];
         if (n > c->cap_pairs - 1) return fail(GS_ERR_CAPACITY, "rank %d delta of %llu pairs past the export buffer", q,
@@ -359,8 +358,6 @@ int merge_allgather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
         if (q != c->rank) folded += n;
     }
     cc_count_folded(h, folded);
-    c->bytes_sent += slot_words * 4 * (P - 1);
-    c->bytes_recv += slot_words * 4 * (P - 1);
     if (mt) {                                                   // tails past S: one more all-gather
         ++c->overflows;
         uint32_t* t = send + 2 + 2 * S;                         // this rank's pairs [S, n)
@@ -379,9 +376,65 @@ int merge_allgather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
         GS_TRY(rc);
         c->bytes_sent += mt * 8 * (P - 1);
         c->bytes_recv += mt * 8 * (P - 1);
-        GS_TRY(gs_cc_close_window(h));
+        if (close) GS_TRY(gs_cc_close_window(h));              // (from merge_window: its close follows)
     }
     c->spec_slot = next_slot(c, maxc);
+    c->last_delta = maxc;
+    return GS_OK;
+}
+
+int abort_exchange(gs_comm_t* c, int rc);
+
+// cc_settle's callback: a failed verification fails the group (peers may be in the tail round)
+int settle_cb(void* ctx) {
+    gs_comm_t* c = static_cast<gs_comm_t*>(ctx);
+    const int rc = settle_allgather(c, true);
+    return rc == GS_OK ? rc : abort_exchange(c, rc);
+}
+
+int merge_allgather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
+    const int P = c->world;
+    hipStream_t s = in.stream;
+    uint64_t maxc = 0;
+    if (c->spec_slot == 0 && !c->pending) {
+        GS_TRY(exchange_exact(c, h, in, &maxc));
+        GS_TRY(gs_cc_close_window(h));
+        c->spec_slot = next_slot(c, maxc);
+        c->last_delta = maxc;
+        return GS_OK;
+    }
+    // 1. this window's export, into the buffer the pending window does not use: its roots are
+    //    this rank's forest right after its own fold (the pending window's tails, foreign pairs
+    //    folded with marking paused, must not be under them: a root of its own they hooked would
+    //    vanish from its pairs)
+    uint32_t* send = (c->pending && c->pend_buf == c->sendbuf) ? c->sendbuf2 : c->sendbuf;
+    GS_TRY(cc_export_async(h, send + 2, c->cap_pairs - 1, reinterpret_cast<unsigned long long*>(send), 2 * c->last_delta));
+    // 2. the previous window's verification (its tail round, if any, is the next collective on
+    //    every rank); it sizes this window's slot
+    if (c->pending) {
+        cc_set_settle(h, nullptr, nullptr);
+        GS_TRY(settle_allgather(c, false));
+    }
+    const uint64_t S = c->spec_slot;
+    const uint64_t slot_words = 2 + 2 * S;                       // [u64 count][S pairs]
+    GS_TRY(ensure(reinterpret_cast<void**>(&c->slotbuf), &c->slot_bytes, (size_t)P * slot_words * 4, s));
+    GS_TRY(allgather(c, send, c->slotbuf, slot_words * 4, s));
+    // the count words (one per slot, strided) go to the host on a side stream, so the slots' fold
+    // and the close start right after the collective; settle_allgather reads them (the next
+    // window's collective is enqueued only after that, so the slots are not overwritten under it)
+    GS_HIP(hipEventRecord(c->ev_slots, s));
+    GS_HIP(hipStreamWaitEvent(c->side, c->ev_slots, 0));
+    GS_HIP(hipMemcpy2DAsync(c->hcnt, sizeof(unsigned long long), c->slotbuf, slot_words * 4, sizeof(unsigned long long), P,
+                            hipMemcpyDeviceToHost, c->side));
+    GS_HIP(hipEventRecord(c->ev_counts, c->side));
+    GS_TRY(cc_fold_slots(h, c->slotbuf, slot_words, P, c->rank, S));
+    GS_TRY(gs_cc_close_window(h));                              // optimistic: no delta exceeded S
+    c->bytes_sent += slot_words * 4 * (P - 1);
+    c->bytes_recv += slot_words * 4 * (P - 1);
+    c->pending = true;                                          // verified by settle_allgather
+    c->pend_slot = S;
+    c->pend_buf = send;
+    cc_set_settle(h, settle_cb, c);
     return GS_OK;
 }
 
@@ -482,6 +535,8 @@ int alloc_common(gs_comm_t* c) {
     if (hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_counts, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_slots, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->dcnt, (c->world + 1) * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&c->hcnt, (c->world + 1) * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
@@ -552,12 +607,19 @@ int gs_comm_create_local(gs_comm_t** comms, int world, int device) {
 int gs_comm_destroy(gs_comm_t* c) {
     if (!c) return GS_OK;
     DeviceGuard g(c->device);
+    if (c->pending && c->bound) {                   // verify the last window (peers may be in its tail
+        cc_set_settle(c->bound, nullptr, nullptr);  // round), then the handle forgets this communicator
+        if (!c->broken) (void)settle_cb(c);
+    }
     (void)hipDeviceSynchronize();
     if (c->nccl) (void)ncclCommDestroy(c->nccl);
     if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->ev_counts) (void)hipEventDestroy(c->ev_counts);
+    if (c->ev_slots) (void)hipEventDestroy(c->ev_slots);
+    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->sendbuf) (void)hipFree(c->sendbuf);
+    if (c->sendbuf2) (void)hipFree(c->sendbuf2);
     if (c->recvbuf) (void)hipFree(c->recvbuf);
     if (c->slotbuf) (void)hipFree(c->slotbuf);
     if (c->dcnt) (void)hipFree(c->dcnt);
@@ -569,6 +631,8 @@ int gs_comm_destroy(gs_comm_t* c) {
 int gs_comm_info(gs_comm_t* c, int* rank, int* world, uint64_t* bytes_sent, uint64_t* bytes_recv, uint64_t* exchanges,
                  uint64_t* overflows) {
     if (!c) return fail(GS_ERR_INVALID, "null communicator");
+    // (a pending window's overflow round is counted when it is verified: the next merge_window or
+    // any call that consumes the emission)
     if (overflows) *overflows = c->overflows;
     if (rank) *rank = c->rank;
     if (world) *world = c->world;
@@ -602,6 +666,7 @@ int merge_window(gs_cc_t* h, gs_comm_t* c, int mode) {
         return fail(GS_ERR_INVALID, "gs_cc_merge_window: this communicator serves another handle or mode "
                                     "(one communicator per summary and mode)");
     if (!c->bound) { c->bound = h; c->mode = mode; c->reset_gen = in.reset_gen; }
+    if (mode != GS_MERGE_ALLGATHER) GS_TRY(cc_settle(h));   // (allgather settles after its export)
     if (in.reset_gen != c->reset_gen) {              // the handle was reset: a new stream
         c->reset_gen = in.reset_gen;
         c->spec_slot = 0;                            // its first window runs the exact round again

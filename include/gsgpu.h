@@ -171,8 +171,12 @@ int gs_cc_set_marking(gs_cc_t* h, int on);
  *                         more exact round, decided alike on every rank)
  *     GS_MERGE_GATHER     windowAll: deltas to rank 0, which folds them and emits
  *     GS_MERGE_TREE       log2(P) pairwise rounds to rank 0 (SummaryTreeReduce.enhance)
- *   Every rank must call it once per window with the same mode. It waits once per window for the
- *   delta sizes. In GATHER / TREE only rank 0's emission is the job's. */
+ *   Every rank must call it once per window with the same mode. In GATHER / TREE only rank 0's
+ *   emission is the job's, and the call waits for the delta sizes. In ALLGATHER it does not wait:
+ *   the sizes are checked lazily (an outgrown slot's tail round) by the next merge_window, or first
+ *   thing in any call that consumes the emission or folds (stats, checksum, emit_*, find,
+ *   labels_device, sync, fold*, merge, combine, reset, destroy) — gs_cc_fold_windows alone folds
+ *   the next window without that wait (its merge exports before settling). */
 typedef struct gs_comm gs_comm_t;
 enum { GS_MERGE_ALLGATHER = 0, GS_MERGE_GATHER = 1, GS_MERGE_TREE = 2 };
 int gs_comm_unique_id(void* id, uint64_t id_bytes);

@@ -137,6 +137,54 @@ def test_local_group_speculative_slot_overflow(oracle, world):
     assert all(i[5] >= 1 for i in info) and len({i[5] for i in info}) == 1, info
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_lazy_verification_overflow_in_a_batch(oracle, world):
+    """The speculative all-gather is verified lazily (comm.hip settle_allgather): with
+    gs_cc_fold_windows nothing consumes an emission between windows, so an outgrown slot's tail
+    round runs only after the NEXT window's local fold. The final emission must still be exact and
+    the overflow counted alike on every rank (the same stream as the per-window overflow test)."""
+    import torch
+    cap = 1 << 16
+    W = 1 << 17
+    s1 = np.zeros(W, dtype=np.int64)
+    s2, d2 = oracle.gen_er(0, 3 * W, cap, 4)
+    s = np.concatenate([s1, s2]); d = np.concatenate([s1, d2])
+    want = oracle.run(s, d, W, partitions=world, emit=EMIT_CHECKSUM, label_cap=cap, want_final=True)
+    assert W % world == 0
+    per = []
+    for r in range(world):
+        idx = np.concatenate([np.arange(lo + (W * r) // world, lo + (W * (r + 1)) // world) for lo in range(0, s.size, W)])
+        per.append((s[idx], d[idx]))
+    comms = Comm.local_group(world, 0)
+    finals, errors, ov = [None] * world, [], [None] * world
+
+    def rank(r):
+        try:
+            ts = torch.from_numpy(per[r][0].astype(np.int32)).cuda()
+            td = torch.from_numpy(per[r][1].astype(np.int32)).cuda()
+            ds = DisjointSet(cap, id_bits=32, track_marks=True)
+            assert ds.fold_windows(ts, td, W // world, comm=comms[r], mode="allgather") == s.size // W
+            finals[r] = (ds.checksum()[0], ds.dense().astype(np.int64))
+            ov[r] = comms[r].info()[5]
+            ds.close()
+        except Exception as e:
+            errors.append((r, repr(e)))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th), "a rank hung"
+    for c in comms:
+        c.close()
+    assert not errors, errors
+    for r in range(world):
+        assert finals[r][0] == int(want["checksums"][-1]), "rank %d" % r
+        np.testing.assert_array_equal(finals[r][1], want["final"])
+    assert all(o >= 1 for o in ov) and len(set(ov)) == 1, ov
+
+
 def test_merge_window_errors():
     """Argument errors fail the call AND the communicator (its peers would otherwise wait forever in
     the next collective): a later call on it returns GS_ERR_COMM."""
