@@ -293,7 +293,13 @@ template <typename IdT, bool AOS>
 void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool young = false) {
     const int ept = young ? kYoungEpt : kEdgesPerThread;
     const bool persist = young && h->cus > 0;
-    const unsigned grid = persist ? (unsigned)std::min<uint64_t>((uint64_t)h->cus * kYoungBlocksPerCu, grid_for((n + ept - 1) / ept, kFoldThreads, 1u << 20))
+    // The first young launch after reset folds into an EMPTY forest: every hub's first hooks and
+    // the giant root's repeated re-hooks collide there, so it keeps at most ~1/16 of its edges in
+    // flight (>= 32 workgroups). BASELINE config 2 (RMAT-20, the whole 2^18-edge launch in flight
+    // at 2/CU): 0.97 -> 0.64 ms per step; configs 3-5 unchanged (profiles/r03_ygrid2).
+    const uint64_t ycap = h->edges_since_reset ? ~0ull : std::max<uint64_t>(32, n / (16ull * kFoldThreads * kYoungEpt));
+    const unsigned grid = persist ? (unsigned)std::min<uint64_t>(std::min<uint64_t>((uint64_t)h->cus * kYoungBlocksPerCu, ycap),
+                                                                  grid_for((n + ept - 1) / ept, kFoldThreads, 1u << 20))
                                   : grid_for((n + ept - 1) / ept, kFoldThreads, 16384);
     ensure_stats(h);
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
