@@ -217,6 +217,10 @@ int sync_and_check(gs_cc_t* h) {
 // edges 1746 us, one launch 2/CU 1403 us, 4/CU 2265 us; EPT 4 -> 2: 1873 -> 1715 us.
 constexpr int kYoungEpt = 2;
 constexpr unsigned kYoungBlocksPerCu = 2;
+// the first young launch after reset: at most 1/kYoungFirstDiv of its edges in flight (headline
+// RMAT-26 sweep of the divisor 16 / 32 / 64 / 128 / 256: 16.29 / 16.25 / 16.47 / 17.03 / 18.19 ms
+// per step, profiles/r03_yfirst_sweep.txt; at 2^22 edges 16 keeps the 2-per-CU grid)
+constexpr uint64_t kYoungFirstDiv = 16;
 // Folding a partial summary (AOS pairs: fold_pairs / the multi-GPU merge): the pairs (v, R) of one
 // component all name its root R; while R's component is not yet joined to the receiver's, every
 // pair in flight CASes the same word (RMAT-26 window-1 deltas: 5-14 ms for 6M pairs). A head
@@ -267,6 +271,7 @@ struct DebugEnv {
         if (e && *e) ring_min_bits = (uint32_t)strtoul(e, nullptr, 0);
         e = getenv("GSGPU_YOUNG_SPLIT");
         if (e && *e) young_split = strtoull(e, nullptr, 0);
+
     }
 };
 static const DebugEnv& dbg() {
@@ -297,7 +302,7 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
     // the giant root's repeated re-hooks collide there, so it keeps at most ~1/16 of its edges in
     // flight (>= 32 workgroups). BASELINE config 2 (RMAT-20, the whole 2^18-edge launch in flight
     // at 2/CU): 0.97 -> 0.64 ms per step; configs 3-5 unchanged (profiles/r03_ygrid2).
-    const uint64_t ycap = h->edges_since_reset ? ~0ull : std::max<uint64_t>(32, n / (16ull * kFoldThreads * kYoungEpt));
+    const uint64_t ycap = h->edges_since_reset ? ~0ull : std::max<uint64_t>(32, n / (kYoungFirstDiv * kFoldThreads * kYoungEpt));
     const unsigned grid = persist ? (unsigned)std::min<uint64_t>(std::min<uint64_t>((uint64_t)h->cus * kYoungBlocksPerCu, ycap),
                                                                   grid_for((n + ept - 1) / ept, kFoldThreads, 1u << 20))
                                   : grid_for((n + ept - 1) / ept, kFoldThreads, 16384);
