@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--exchange-world1", action="store_true",
                     help="one GPU through the C-ABI exchange (RCCL with one rank): the per-window cost of "
                          "export + collective + delta fold + close that a multi-GPU window adds (a measurement line)")
+    ap.add_argument("--host-loop", action="store_true",
+                    help="drive the windows from Python (fold + close / merge per window) instead of one "
+                         "gs_cc_fold_windows call per step (an A/B of the host loop)")
     ap.add_argument("--merge", default="allgather", choices=["allgather", "gather", "tree"],
                     help="multi-rank CombineCC: allgather = replicated global summary (every rank folds every "
                          "delta); gather = windowAll gather to rank 0 (SummaryBulkAggregation.java:81); tree = "
@@ -195,7 +198,7 @@ def main():
 
     # the plain per-window loop runs inside the library (gs_cc_fold_windows: one ABI call per step
     # instead of two per window); per-window host work (delta copies, the gloo model) keeps the loop
-    batched = not a.emit_host and tree is None
+    batched = not a.emit_host and tree is None and not a.host_loop
 
     def step():
         ds.reset()
