@@ -441,7 +441,7 @@ def request_roofline(prof, avg_ms):
     random 4-B loads over an L2-resident table (the request rate of L2 channels) and a streaming
     read. Bound = max(requests / L2 request rate, HBM bytes / stream rate): the two are served by
     different units and overlap."""
-    lab_path = os.path.join(ROOT, "profiles", "r02_request_lab.json")
+    lab_path = os.path.join(ROOT, "profiles", "r03_request_lab.json")
     if not os.path.exists(lab_path):
         return None
     try:
@@ -457,7 +457,7 @@ def request_roofline(prof, avg_ms):
                 "frac": bound_us / (avg_ms * 1e3),
                 "definition": "max(TCC requests / L2 random-request rate, PMC HBM bytes / streaming-read rate) per "
                               "launch (counts: profiles/fold_traffic.json; rates: tools/request_lab.hip, "
-                              "profiles/r02_request_lab.json) / the launch's average duration"}
+                              "profiles/r03_request_lab.json) / the launch's average duration"}
     except Exception:
         return None
 

@@ -119,7 +119,12 @@ def main():
     }
     edges_per_launch = None
     try:
-        b = json.load(open(os.path.join(root, "..", "bench.json")))
+        bj = os.path.join(root, "..", "bench.json")
+        if os.path.exists(bj):
+            b = json.load(open(bj))
+        else:                                          # the bench line in the first pass's log
+            lines = [l for l in open(os.path.join(root, "p1.log")) if l.startswith("{")]
+            b = json.loads(lines[-1])
         out["window_edges"] = b["config"]["window_edges_per_gpu"]
         out["scale"] = b["config"]["scale"]
         out["id_bits"] = b["config"].get("id_bits", 32)

@@ -66,7 +66,7 @@ def test_stale_profile_is_dropped(tmp_path):
 
 def test_request_roofline_definition():
     bench, a = _bench()
-    lab = json.load(open(os.path.join(ROOT, "profiles", "r02_request_lab.json")))
+    lab = json.load(open(os.path.join(ROOT, "profiles", "r03_request_lab.json")))
     prof = {"tcc_requests_per_launch": 13.0e6, "hbm_bytes_per_launch": 400e6}
     r = bench.request_roofline(prof, 0.1)
     t_req = 13.0e6 / (lab["rand4B_1MiB_32w_Gps"] * 1e3)
