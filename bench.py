@@ -71,7 +71,10 @@ def parse():
     ap.add_argument("--emit-host", action="store_true",
                     help="per window, the emission's delta (gs_cc_emit_delta: pairs new or changed since the last "
                          "window) copied to pinned host memory, inside the timed region: what a host-side Merger / "
-                         "FlattenSet consumer costs (SummaryAggregation.java:110-111)")
+                         "FlattenSet consumer costs (SummaryAggregation.java:110-111); async by default "
+                         "(gs_cc_emit_delta_async: the copy of window w overlaps the fold of window w+1)")
+    ap.add_argument("--emit-sync", action="store_true",
+                    help="with --emit-host: the blocking gs_cc_emit_delta per window instead")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check final labels with an independent torch CC "
                     "(multi-rank: rank 0 regenerates the whole global stream; small scales only)")
@@ -173,9 +176,14 @@ def main():
         tree = cls(ds, capacity_pairs=V, device=dev)
     gather = tree is not None and a.merge == "gather"
     emitted = [0, 0]                                  # delta pairs copied to the host, windows
-    if a.emit_host:
-        hv = torch.empty(V, dtype=idt).pin_memory()
-        hl = torch.empty(V, dtype=idt).pin_memory()
+    if a.emit_host:                                   # two pinned slots: window w's delta lands in w & 1
+        hv = [torch.empty(V, dtype=idt).pin_memory() for _ in range(2)]
+        hl = [torch.empty(V, dtype=idt).pin_memory() for _ in range(2)]
+
+    def consume(done):
+        for v, _ in done:
+            emitted[0] += v.numel()
+            emitted[1] += 1
 
     def window(w, after=None):
         lo = w * W_rank
@@ -188,10 +196,11 @@ def main():
             tree.merge_window()
         else:
             ds.close_window()
-        if a.emit_host:
-            v, _ = ds.delta(hv, hl)
-            emitted[0] += v.numel()
-            emitted[1] += 1
+        if a.emit_host and a.emit_sync:
+            consume([ds.delta(hv[0], hl[0])])
+        elif a.emit_host:                             # enqueue w's delta, take w-1's
+            ds.delta_async(hv[w & 1], hl[w & 1])
+            consume(ds.emit_wait(1))
 
     fold_mask = GS_TIMING_MASK | (1 << GS_K_FOLD) | (1 << GS_K_RING) | \
         ((1 << GS_K_MERGE) | (1 << GS_K_EXPORT) if world > 1 else 0)
@@ -208,6 +217,8 @@ def main():
         else:
             for w in range(nwin):
                 window(w)
+            if a.emit_host:
+                consume(ds.emit_wait(0))
 
     log = lambda m: print("[bench rank %d] %s" % (rank, m), file=sys.stderr, flush=True)
     log("inputs ready: %d edges/rank, %d windows of %d (global %d), %s scaling" % (E_rank, nwin, W_rank, W_glob, a.scaling))
@@ -324,7 +335,7 @@ def main():
                                                          ("_int64" if a.id_bits == 64 else "") +
                                                          ("_xchg1" if a.exchange_world1 else ""),
                                                          "_hostinput" if a.host_input else "") +
-                            ("_emithost" if a.emit_host else ""),
+                            ("_emithost" + ("sync" if a.emit_sync else "") if a.emit_host else ""),
                 "scale": a.scale, "vertices": V, "edge_factor": a.edge_factor,
                 "edges_total": E_glob, "edges_per_gpu": E_rank, "window_edges": W_glob,
                 "window_edges_per_gpu": W_rank, "windows": nwin, "id_bits": a.id_bits,
@@ -334,7 +345,8 @@ def main():
                     if world > 1 else ("%s merge through the C-ABI exchange at world 1 (RCCL, one rank)" % a.merge
                                        if a.exchange_world1 else "no merge")),
                 "emission": ("per window, canonical min-id labels resident in HBM, and the delta (pairs new or changed "
-                             "since the last window) copied to pinned host memory (gs_cc_emit_delta)") if a.emit_host
+                             "since the last window) copied to pinned host memory (%s)" % ("gs_cc_emit_delta" if a.emit_sync else
+                             "gs_cc_emit_delta_async, waited one window later")) if a.emit_host
                             else "per window, canonical min-id labels resident in HBM",
             },
             "roofline": {

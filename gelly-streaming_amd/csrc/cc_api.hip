@@ -84,6 +84,16 @@ struct gs_cc {
     hipEvent_t staged[2] = {nullptr, nullptr}, freed[2] = {nullptr, nullptr};
     void* tmp = nullptr;                 // emission temporaries
     size_t tmp_bytes = 0;
+    // delta emission (gs_cc_emit_delta[_async]): two slots of packed pairs; an async emission's
+    // slot is copied out on estream (k_delta_copy: device / pinned buffers) or at gs_cc_emit_wait
+    struct EmitSlot { void* mem = nullptr; size_t bytes = 0; hipEvent_t staged = nullptr, done = nullptr; };
+    EmitSlot eslot[2];
+    unsigned long long* ecount = nullptr;    // pinned: the size of each slot's delta
+    hipStream_t estream = nullptr;
+    struct EmitPend { int slot; uint64_t* n_out; uint64_t cap; void* vertices; void* labels; bool kcopy; };
+    EmitPend epend[2];                   // async emissions not yet waited for, oldest first
+    int n_epend = 0;
+    uint32_t enext = 0;                  // slot of the next emission
     bool compressed = true;
     bool sbits_stale = false;            // a young launch skipped the seen bits: the next close rebuilds them
     uint64_t edges_since_reset = 0;      // drives the young-forest launch split (fold_impl)
@@ -931,6 +941,14 @@ int gs_cc_destroy(gs_cc_t* h) {
         if (h->freed[k]) (void)hipEventDestroy(h->freed[k]);
     }
     if (h->copy) (void)hipStreamDestroy(h->copy);
+    if (h->estream) (void)hipStreamSynchronize(h->estream);
+    for (auto& s : h->eslot) {
+        if (s.mem) (void)hipFree(s.mem);
+        if (s.staged) (void)hipEventDestroy(s.staged);
+        if (s.done) (void)hipEventDestroy(s.done);
+    }
+    if (h->ecount) (void)hipHostFree(h->ecount);
+    if (h->estream) (void)hipStreamDestroy(h->estream);
     if (h->tmp) (void)hipFree(h->tmp);
     if (h->own) (void)hipStreamDestroy(h->own);
     delete h;
@@ -994,7 +1012,8 @@ int gs_cc_sync(gs_cc_t* h) {
     GS_TRY(check(h));
     GS_TRY(cc_settle(h));                      // a pending multi-GPU window first (comm.hip)
     DeviceGuard g(h->device);
-    return sync_and_check(h);
+    GS_TRY(sync_and_check(h));
+    return gs_cc_emit_wait(h, 0);              // and every async delta emission
 }
 
 // A fold settles a pending multi-GPU window first: its tail pairs (foreign unions folded with marking
@@ -1164,7 +1183,7 @@ int gs_cc_emit_pairs(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uin
     uint32_t* cnt = static_cast<uint32_t*>(h->tmp);
     uint64_t* off = reinterpret_cast<uint64_t*>(static_cast<char*>(h->tmp) + cnt_b);
     hipLaunchKernelGGL(k_tile_count, dim3(ntiles), dim3(kTileThreads), 0, h->stream, h->parent, h->cap, cnt);
-    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, h->stream, cnt, off, ntiles);
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, h->stream, cnt, off, ntiles, (unsigned long long*)nullptr);
     GS_HIP(hipGetLastError());
     GS_HIP(hipMemcpyAsync(h->hscratch, off + ntiles, 8, hipMemcpyDeviceToHost, h->stream));
     GS_TRY(sync_and_check(h));
@@ -1181,7 +1200,7 @@ int gs_cc_emit_pairs(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uin
             off = reinterpret_cast<uint64_t*>(static_cast<char*>(h->tmp) + cnt_b);
             // ensure_buf may have reallocated: recompute the offsets
             hipLaunchKernelGGL(k_tile_count, dim3(ntiles), dim3(kTileThreads), 0, h->stream, h->parent, h->cap, cnt);
-            hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, h->stream, cnt, off, ntiles);
+            hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, h->stream, cnt, off, ntiles, (unsigned long long*)nullptr);
             vo = static_cast<char*>(h->tmp) + cnt_b + off_b;
             lo = static_cast<char*>(vo) + w * esz;
         }
@@ -1203,69 +1222,194 @@ int gs_cc_emit_pairs(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uin
     return GS_OK;
 }
 
-int gs_cc_emit_delta(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uint64_t* n_out) {
+// ---- delta emission ----
+static int delta_begin(gs_cc_t* h, const char* who, void* vertices, void* labels, uint64_t cap, uint64_t* n_out) {
     GS_TRY(check(h));
     GS_TRY(cc_settle(h));                      // a pending multi-GPU window first (comm.hip)
-    if (!n_out) return fail(GS_ERR_INVALID, "gs_cc_emit_delta: null n_out");
-    if (cap && (!vertices || !labels)) return fail(GS_ERR_INVALID, "gs_cc_emit_delta: null output");
-    if (h->sparse) return fail(GS_ERR_UNSUPPORTED, "gs_cc_emit_delta: sparse-id summary (use gs_cc_emit_pairs)");
-    DeviceGuard g(h->device);
+    if (!n_out) return fail(GS_ERR_INVALID, "%s: null n_out", who);
+    if (cap && (!vertices || !labels)) return fail(GS_ERR_INVALID, "%s: null output", who);
+    if (h->sparse) return fail(GS_ERR_UNSUPPORTED, "%s: sparse-id summary (use gs_cc_emit_pairs)", who);
     if (!h->elab) {                      // first call: every vertex dirty, nothing emitted yet
+        DeviceGuard g(h->device);
         if (hipMalloc(&h->elab, (size_t)h->cap * 4) != hipSuccess || hipMalloc(&h->dbits, mark_bytes(h->cap)) != hipSuccess) {
             (void)hipGetLastError();
             if (h->elab) (void)hipFree(h->elab);
             h->elab = nullptr;
-            return fail(GS_ERR_NOMEM, "gs_cc_emit_delta: state allocation failed");
+            return fail(GS_ERR_NOMEM, "%s: state allocation failed", who);
         }
         GS_HIP(hipMemsetAsync(h->elab, 0xFF, (size_t)h->cap * 4, h->stream));
         GS_HIP(hipMemsetAsync(h->dbits, 0xFF, mark_bytes(h->cap), h->stream));
     }
-    GS_TRY(compress_impl(h));
+    return GS_OK;
+}
+
+// The delta on h->stream in three launches: k_delta_stage (every tile's changed pairs into its own
+// region of the tile staging, h->tmp: counts, offsets, ntiles x kTile pairs), k_tile_scan (offsets;
+// the size also to *total_host if given), k_delta_pack (the pairs packed to vo/lo — device
+// addresses, cap entries — elab and the dirty words updated, only if the delta fits cap). Returns
+// the device word holding the size.
+static int delta_enqueue(gs_cc_t* h, uint64_t cap, void* vo, void* lo, unsigned long long* total_host,
+                         const uint64_t** total) {
     const uint32_t ntiles = (uint32_t)((h->cap + kTile - 1) / kTile);
     const size_t esz = h->cfg.id_bits / 8;
     const size_t cnt_b = ((size_t)ntiles * 4 + 15) & ~(size_t)15;
     const size_t off_b = ((size_t)(ntiles + 1) * 8 + 15) & ~(size_t)15;
-    GS_TRY(ensure_buf(&h->tmp, &h->tmp_bytes, cnt_b + off_b));
+    const size_t tile_pairs = (size_t)ntiles * kTile;
+    GS_TRY(ensure_buf(&h->tmp, &h->tmp_bytes, cnt_b + off_b + 2 * tile_pairs * esz));
     uint32_t* cnt = static_cast<uint32_t*>(h->tmp);
     uint64_t* off = reinterpret_cast<uint64_t*>(static_cast<char*>(h->tmp) + cnt_b);
-    hipLaunchKernelGGL(k_delta_count, dim3(ntiles), dim3(kTileThreads), 0, h->stream, (const uint32_t*)h->parent, h->cap,
-                       (const uint32_t*)h->elab, (const uint32_t*)h->dbits, cnt);
-    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, h->stream, cnt, off, ntiles);
+    char* sv = static_cast<char*>(h->tmp) + cnt_b + off_b;
+    char* sl = sv + tile_pairs * esz;
+#define GS_DELTA(IdT)                                                                                                    \
+    hipLaunchKernelGGL(k_delta_stage<IdT>, dim3((ntiles + kDeltaTiles - 1) / kDeltaTiles), dim3(kTileThreads), 0,       \
+                       h->stream, (const uint32_t*)h->parent, h->cap, (const uint32_t*)h->elab, (const uint32_t*)h->dbits, \
+                       ntiles, cnt, (IdT*)sv, (IdT*)sl);                                                                   \
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, h->stream, cnt, off, ntiles, total_host);                      \
+    hipLaunchKernelGGL(k_delta_pack<IdT>, dim3(ntiles), dim3(256), 0, h->stream, (const IdT*)sv, (const IdT*)sl,           \
+                       (const uint32_t*)cnt, (const uint64_t*)off, ntiles, cap, h->elab, h->dbits, h->cap, (IdT*)vo, (IdT*)lo)
+    if (h->cfg.id_bits == 32) { GS_DELTA(uint32_t); } else { GS_DELTA(int64_t); }
+#undef GS_DELTA
     GS_HIP(hipGetLastError());
-    GS_HIP(hipMemcpyAsync(h->hscratch, off + ntiles, 8, hipMemcpyDeviceToHost, h->stream));
-    GS_TRY(sync_and_check(h));
-    const uint64_t total = h->hscratch[0];
-    *n_out = total;
-    if (total > cap) return fail(GS_ERR_CAPACITY, "gs_cc_emit_delta: %llu changed pairs, capacity %llu (nothing consumed)",
-                                 (unsigned long long)total, (unsigned long long)cap);
-    const bool dev = total == 0 || (is_device_pointer(vertices) && is_device_pointer(labels));
-    void* vo = vertices;
-    void* lo = labels;
-    if (!dev) {
-        GS_TRY(ensure_buf(&h->tmp, &h->tmp_bytes, cnt_b + off_b + 2 * total * esz));
-        cnt = static_cast<uint32_t*>(h->tmp);      // (ensure_buf may have moved tmp: recount)
-        off = reinterpret_cast<uint64_t*>(static_cast<char*>(h->tmp) + cnt_b);
-        hipLaunchKernelGGL(k_delta_count, dim3(ntiles), dim3(kTileThreads), 0, h->stream, (const uint32_t*)h->parent, h->cap,
-                           (const uint32_t*)h->elab, (const uint32_t*)h->dbits, cnt);
-        hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, h->stream, cnt, off, ntiles);
-        vo = static_cast<char*>(h->tmp) + cnt_b + off_b;
-        lo = static_cast<char*>(vo) + total * esz;
+    *total = off + ntiles;
+    return GS_OK;
+}
+
+// The device's view of an output buffer: device memory as is, pinned host memory (hipHostMalloc,
+// hipHostRegister) through its device mapping; nullptr for pageable host memory.
+static void* device_view(void* p) {
+    hipPointerAttribute_t a;
+    if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
     }
-    if (total) {
-        if (h->cfg.id_bits == 32)
-            hipLaunchKernelGGL(k_delta_scatter<uint32_t>, dim3(ntiles), dim3(kTileThreads), 0, h->stream, (const uint32_t*)h->parent,
-                               h->cap, h->elab, (const uint32_t*)h->dbits, (const uint64_t*)off, (uint32_t*)vo, (uint32_t*)lo);
-        else
-            hipLaunchKernelGGL(k_delta_scatter<int64_t>, dim3(ntiles), dim3(kTileThreads), 0, h->stream, (const uint32_t*)h->parent,
-                               h->cap, h->elab, (const uint32_t*)h->dbits, (const uint64_t*)off, (int64_t*)vo, (int64_t*)lo);
-        GS_HIP(hipGetLastError());
-        if (!dev) {
-            GS_HIP(hipMemcpyAsync(vertices, vo, total * esz, hipMemcpyDeviceToHost, h->stream));
-            GS_HIP(hipMemcpyAsync(labels, lo, total * esz, hipMemcpyDeviceToHost, h->stream));
+    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.isManaged) return p;
+    if (a.type == hipMemoryTypeHost && a.devicePointer && a.hostPointer)
+        return static_cast<char*>(a.devicePointer) + (static_cast<char*>(p) - static_cast<char*>(a.hostPointer));
+    return nullptr;
+}
+
+// workgroups of the async copy-out kernel (few: its PCIe writes share the CUs with the next fold)
+static unsigned emit_copy_blocks() {
+    static const unsigned b = [] {
+        const char* e = getenv("GSGPU_EMIT_COPY_BLOCKS");
+        const unsigned v = (e && *e) ? (unsigned)strtoul(e, nullptr, 0) : 64u;
+        return v ? v : 64u;
+    }();
+    return b;
+}
+
+// packed pairs for host outputs: slot si's buffer, 2 x min(cap, capacity) ids
+static int delta_slot(gs_cc_t* h, int si, uint64_t cap, char** sv, char** sl) {
+    const size_t esz = h->cfg.id_bits / 8;
+    const uint64_t scap = std::min<uint64_t>(cap, h->cap);
+    gs_cc::EmitSlot& S = h->eslot[si];
+    GS_TRY(ensure_buf(&S.mem, &S.bytes, std::max<size_t>(2 * scap * esz, 16)));
+    *sv = static_cast<char*>(S.mem);
+    *sl = *sv + scap * esz;
+    return GS_OK;
+}
+
+// Device outputs: packed in place. Host outputs (pinned or pageable): packed in HBM, the size read
+// back, then two DMA copies of exactly the delta.
+int gs_cc_emit_delta(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uint64_t* n_out) {
+    GS_TRY(delta_begin(h, "gs_cc_emit_delta", vertices, labels, cap, n_out));
+    GS_TRY(gs_cc_emit_wait(h, 0));             // async emissions still pending come first
+    DeviceGuard g(h->device);
+    GS_TRY(compress_impl(h));
+    const size_t esz = h->cfg.id_bits / 8;
+    const bool dev = cap == 0 || (is_device_pointer(vertices) && is_device_pointer(labels));
+    char *sv = nullptr, *sl = nullptr;
+    if (!dev) GS_TRY(delta_slot(h, 0, cap, &sv, &sl));
+    const uint64_t* total = nullptr;
+    GS_TRY(delta_enqueue(h, cap, dev ? vertices : sv, dev ? labels : sl, nullptr, &total));
+    GS_HIP(hipMemcpyAsync(h->hscratch, total, 8, hipMemcpyDeviceToHost, h->stream));
+    GS_TRY(sync_and_check(h));
+    const uint64_t n = h->hscratch[0];
+    *n_out = n;
+    if (n > cap) return fail(GS_ERR_CAPACITY, "gs_cc_emit_delta: %llu changed pairs, capacity %llu (nothing consumed)",
+                             (unsigned long long)n, (unsigned long long)cap);
+    if (!dev && n) {
+        GS_HIP(hipMemcpyAsync(vertices, sv, n * esz, hipMemcpyDeviceToHost, h->stream));
+        GS_HIP(hipMemcpyAsync(labels, sl, n * esz, hipMemcpyDeviceToHost, h->stream));
+        return sync_and_check(h);
+    }
+    return GS_OK;
+}
+
+// Enqueued only: the delta is packed into one of two slots on h->stream (the next fold may follow
+// at once) and its size lands in a pinned word; device and pinned buffers are written from the slot
+// by k_delta_copy on estream while the next fold runs, pageable ones by DMA in gs_cc_emit_wait.
+int gs_cc_emit_delta_async(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uint64_t* n_out) {
+    GS_TRY(delta_begin(h, "gs_cc_emit_delta_async", vertices, labels, cap, n_out));
+    if (h->n_epend >= 2) return fail(GS_ERR_INVALID, "gs_cc_emit_delta_async: two emissions pending (gs_cc_emit_wait first)");
+    DeviceGuard g(h->device);
+    if (!h->estream) {
+        GS_HIP(hipStreamCreateWithFlags(&h->estream, hipStreamNonBlocking));
+        GS_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->ecount), 2 * sizeof(unsigned long long), hipHostMallocDefault));
+        for (auto& s : h->eslot) {
+            GS_HIP(hipEventCreateWithFlags(&s.staged, hipEventDisableTiming));
+            GS_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
         }
     }
-    GS_HIP(hipMemsetAsync(h->dbits, 0, mark_bytes(h->cap), h->stream));    // consumed
-    return sync_and_check(h);
+    GS_TRY(compress_impl(h));
+    const int si = (int)(h->enext & 1u);
+    char *sv = nullptr, *sl = nullptr;
+    GS_TRY(delta_slot(h, si, cap, &sv, &sl));
+    unsigned long long* cdev = nullptr;
+    GS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&cdev), h->ecount, 0));
+    const uint64_t* total = nullptr;
+    // the size goes to the pinned word from the copy kernel (a host store at the end of the scan
+    // cost that kernel ~20 us: the release of a kernel that writes host memory) or, for pageable
+    // buffers, by a DMA behind the pack
+    GS_TRY(delta_enqueue(h, cap, sv, sl, nullptr, &total));
+    // buffers the device can write: copied out right away, on estream, by a few workgroups (their
+    // PCIe writes overlap the next fold); pageable ones: by DMA at the wait
+    void* dv = cap ? device_view(vertices) : nullptr;
+    void* dl = cap ? device_view(labels) : nullptr;
+    const bool kcopy = dv && dl;
+    if (!kcopy) GS_HIP(hipMemcpyAsync(h->ecount + si, total, 8, hipMemcpyDeviceToHost, h->stream));
+    GS_HIP(hipEventRecord(h->eslot[si].staged, h->stream));
+    if (kcopy) {
+        GS_HIP(hipStreamWaitEvent(h->estream, h->eslot[si].staged, 0));
+        if (h->cfg.id_bits == 32)
+            hipLaunchKernelGGL(k_delta_copy<uint32_t>, dim3(emit_copy_blocks()), dim3(256), 0, h->estream, (const uint32_t*)sv,
+                               (const uint32_t*)sl, total, cap, (uint32_t*)dv, (uint32_t*)dl, cdev + si);
+        else
+            hipLaunchKernelGGL(k_delta_copy<int64_t>, dim3(emit_copy_blocks()), dim3(256), 0, h->estream, (const int64_t*)sv,
+                               (const int64_t*)sl, total, cap, (int64_t*)dv, (int64_t*)dl, cdev + si);
+        GS_HIP(hipGetLastError());
+        GS_HIP(hipEventRecord(h->eslot[si].done, h->estream));
+    }
+    h->epend[h->n_epend++] = gs_cc::EmitPend{si, n_out, cap, vertices, labels, kcopy};
+    ++h->enext;
+    return GS_OK;
+}
+
+int gs_cc_emit_wait(gs_cc_t* h, uint32_t keep) {
+    GS_TRY(check(h));
+    DeviceGuard g(h->device);
+    const size_t esz = h->cfg.id_bits / 8;
+    uint64_t over = 0, over_cap = 0;
+    while (h->n_epend > (int)keep) {
+        const gs_cc::EmitPend p = h->epend[0];
+        for (int i = 1; i < h->n_epend; ++i) h->epend[i - 1] = h->epend[i];
+        --h->n_epend;
+        GS_HIP(hipEventSynchronize(p.kcopy ? h->eslot[p.slot].done : h->eslot[p.slot].staged));
+        const uint64_t n = h->ecount[p.slot];
+        *p.n_out = n;
+        if (n > p.cap) { over = n; over_cap = p.cap; continue; }
+        if (n && !p.kcopy) {
+            const hipMemcpyKind kind = hipMemcpyDeviceToHost;      // pageable host buffers
+            char* sv = static_cast<char*>(h->eslot[p.slot].mem);
+            const uint64_t scap = std::min<uint64_t>(p.cap, h->cap);
+            GS_HIP(hipMemcpyAsync(p.vertices, sv, n * esz, kind, h->estream));
+            GS_HIP(hipMemcpyAsync(p.labels, sv + scap * esz, n * esz, kind, h->estream));
+            GS_HIP(hipStreamSynchronize(h->estream));
+        }
+    }
+    if (over) return fail(GS_ERR_CAPACITY, "gs_cc_emit_delta_async: %llu changed pairs, capacity %llu (nothing consumed)",
+                          (unsigned long long)over, (unsigned long long)over_cap);
+    return GS_OK;
 }
 
 int gs_cc_find(gs_cc_t* h, const void* ids, void* roots, uint64_t n) {

@@ -1514,24 +1514,58 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_count(const uint32_t* __r
     if (threadIdx.x == 0) tile_count[blockIdx.x] = tot;
 }
 
-// exclusive scan of tile counts in one block (in place); offsets are uint64
+// Exclusive scan of tile counts in one 1024-thread block; offsets are uint64, off[ntiles] = the sum
+// (also to *total_host, a pinned word, if given). Up to kScanLdsTiles tiles the counts go through
+// LDS: coalesced loads in, each thread scans a run of consecutive tiles there (wave shuffles across
+// runs), offsets (< 2^32: at most vertex_capacity pairs) back in place, coalesced stores out. One CU
+// reading lane-strided runs straight from memory issued 64 line requests per load instruction
+// (~25 us at 16384 tiles); larger summaries keep that path.
+constexpr uint32_t kScanLdsTiles = 16384;
 __global__ __launch_bounds__(1024) void k_tile_scan(const uint32_t* __restrict__ cnt, uint64_t* __restrict__ off,
-                                                    uint32_t ntiles) {
-    __shared__ unsigned long long part[1024];
-    const uint32_t per = (ntiles + blockDim.x - 1) / blockDim.x;
-    const uint32_t lo = threadIdx.x * per, hi = min(lo + per, ntiles);
-    unsigned long long s = 0;
-    for (uint32_t i = lo; i < hi; ++i) s += cnt[i];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long run = 0;
-        for (uint32_t t = 0; t < blockDim.x; ++t) { const unsigned long long x = part[t]; part[t] = run; run += x; }
-        off[ntiles] = run;
+                                                    uint32_t ntiles, unsigned long long* __restrict__ total_host) {
+    __shared__ uint32_t sc[kScanLdsTiles];
+    __shared__ unsigned long long wsum[16];
+    const bool lds = ntiles <= kScanLdsTiles;
+    if (lds) {                                   // 16 loads in flight per thread, not one at a time
+        constexpr uint32_t kU = kScanLdsTiles / 1024;
+        uint32_t x[kU];
+#pragma unroll
+        for (uint32_t j = 0; j < kU; ++j) x[j] = cnt[min(j * 1024 + threadIdx.x, ntiles - 1)];
+#pragma unroll
+        for (uint32_t j = 0; j < kU; ++j)
+            if (j * 1024 + threadIdx.x < ntiles) sc[j * 1024 + threadIdx.x] = x[j];
+        __syncthreads();
     }
+    const uint32_t per = (ntiles + blockDim.x - 1) / blockDim.x;
+    const uint32_t lo = min(threadIdx.x * per, ntiles), hi = min(lo + per, ntiles);
+    unsigned long long s = 0;
+    for (uint32_t i = lo; i < hi; ++i) s += lds ? sc[i] : cnt[i];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    unsigned long long incl = s;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    if (lane == 63) wsum[wid] = incl;
     __syncthreads();
-    unsigned long long run = part[threadIdx.x];
-    for (uint32_t i = lo; i < hi; ++i) { off[i] = run; run += cnt[i]; }
+    unsigned long long base = 0, tot = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        if (w < wid) base += wsum[w];
+        tot += wsum[w];
+    }
+    unsigned long long run = base + incl - s;
+    if (lds) {
+        for (uint32_t i = lo; i < hi; ++i) { const uint32_t x = sc[i]; sc[i] = (uint32_t)run; run += x; }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < ntiles; i += blockDim.x) off[i] = sc[i];
+    } else {
+        for (uint32_t i = lo; i < hi; ++i) { off[i] = run; run += cnt[i]; }
+    }
+    if (threadIdx.x == 0) {
+        off[ntiles] = tot;
+        if (total_host) *total_host = tot;
+    }
 }
 
 template <typename IdT>
@@ -1564,57 +1598,136 @@ __device__ __forceinline__ uint32_t delta_bits(const uint32_t* __restrict__ dbit
     return (dbits[base >> 5] >> (base & 16)) & 0xFFFFu;
 }
 
-__global__ __launch_bounds__(kTileThreads) void k_delta_count(const uint32_t* __restrict__ parent, uint32_t n,
+// Pass 1 (nothing consumed): a tile's changed pairs into its own staging region (tile t at
+// t * kTile of sv / sl, in vertex order), their number into tile_count[t]. A thread's 16 vertices
+// are half a dirty word; it loads only the 16-B quads of parent / elab holding dirty vertices.
+// kDeltaTiles tiles per workgroup, their loads issued together (one dbits + one quad latency per
+// workgroup instead of per tile: the kernel is latency-bound, 8 workgroups per CU at a time).
+constexpr int kDeltaTiles = 2;
+template <typename IdT>
+__global__ __launch_bounds__(kTileThreads) void k_delta_stage(const uint32_t* __restrict__ parent, uint32_t n,
                                                               const uint32_t* __restrict__ elab,
-                                                              const uint32_t* __restrict__ dbits,
-                                                              uint32_t* __restrict__ tile_count) {
-    const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kTilePerThread;
-    uint32_t c = 0;
-    if (base < n) {
-        const uint32_t d = delta_bits(dbits, base);
+                                                              const uint32_t* __restrict__ dbits, uint32_t ntiles,
+                                                              uint32_t* __restrict__ tile_count,
+                                                              IdT* __restrict__ sv, IdT* __restrict__ sl) {
+    uint64_t base[kDeltaTiles];
+    uint32_t d[kDeltaTiles], hit[kDeltaTiles], c[kDeltaTiles];
+    uint32_t p[kDeltaTiles][kTilePerThread];
 #pragma unroll
-        for (int k = 0; k < kTilePerThread; ++k) {
-            const uint64_t v = base + k;
-            if (((d >> k) & 1u) && v < n) {
-                const uint32_t p = parent[v];
-                c += (p != kInvalid && p != elab[v]);
+    for (int u = 0; u < kDeltaTiles; ++u) {
+        const uint32_t t = blockIdx.x * kDeltaTiles + u;
+        base[u] = (uint64_t)t * kTile + (uint64_t)threadIdx.x * kTilePerThread;
+        d[u] = (t < ntiles && base[u] < n) ? delta_bits(dbits, base[u]) : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kDeltaTiles; ++u) {
+        hit[u] = 0;
+        c[u] = 0;
+        if (d[u] && base[u] + kTilePerThread <= n) {
+            const uint4* p4 = reinterpret_cast<const uint4*>(parent + base[u]);
+            const uint4* e4 = reinterpret_cast<const uint4*>(elab + base[u]);
+#pragma unroll
+            for (int q = 0; q < kTilePerThread / 4; ++q) {
+                uint4 a = make_uint4(kInvalid, kInvalid, kInvalid, kInvalid), e = a;
+                if ((d[u] >> (4 * q)) & 0xFu) { a = p4[q]; e = e4[q]; }
+                const uint32_t pa[4] = {a.x, a.y, a.z, a.w}, ea[4] = {e.x, e.y, e.z, e.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int k = 4 * q + j;
+                    p[u][k] = pa[j];
+                    if (((d[u] >> k) & 1u) && pa[j] != kInvalid && pa[j] != ea[j]) { hit[u] |= 1u << k; ++c[u]; }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kTilePerThread; ++k) {
+                const uint64_t v = base[u] + k;
+                p[u][k] = kInvalid;
+                if (((d[u] >> k) & 1u) && v < n) {
+                    p[u][k] = parent[v];
+                    if (p[u][k] != kInvalid && p[u][k] != elab[v]) { hit[u] |= 1u << k; ++c[u]; }
+                }
             }
         }
     }
-    uint32_t tot;
-    (void)block_exclusive_scan(c, &tot);
-    if (threadIdx.x == 0) tile_count[blockIdx.x] = tot;
+#pragma unroll
+    for (int u = 0; u < kDeltaTiles; ++u) {
+        const uint32_t t = blockIdx.x * kDeltaTiles + u;
+        uint32_t tot;
+        uint64_t pos = (uint64_t)t * kTile + block_exclusive_scan(c[u], &tot);
+#pragma unroll
+        for (int k = 0; k < kTilePerThread; ++k) {
+            if (!((hit[u] >> k) & 1u)) continue;
+            sv[pos] = static_cast<IdT>(base[u] + k);
+            sl[pos] = static_cast<IdT>(p[u][k]);
+            ++pos;
+        }
+        if (threadIdx.x == 0 && t < ntiles) tile_count[t] = tot;
+    }
+}
+
+// Pass 3, only if the whole delta fits cap (off[ntiles] = its size; uniform, so an overflow consumes
+// nothing and the next delta still holds these pairs): tile t's pairs to out[off[t]..], elab updated,
+// the tile's 128 dirty words (its own line) cleared. One workgroup per tile.
+template <typename IdT>
+__global__ __launch_bounds__(256) void k_delta_pack(const IdT* __restrict__ sv, const IdT* __restrict__ sl,
+                                                    const uint32_t* __restrict__ tile_count,
+                                                    const uint64_t* __restrict__ off, uint32_t ntiles, uint64_t cap,
+                                                    uint32_t* __restrict__ elab, uint32_t* __restrict__ dbits, uint32_t n,
+                                                    IdT* __restrict__ vout, IdT* __restrict__ lout) {
+    if (off[ntiles] > cap) return;
+    const uint32_t t = blockIdx.x;
+    const uint32_t c = tile_count[t];
+    const uint64_t o = off[t], src = (uint64_t)t * kTile;
+    for (uint32_t i = threadIdx.x; i < c; i += blockDim.x) {
+        const IdT v = sv[src + i], l = sl[src + i];
+        vout[o + i] = v;
+        lout[o + i] = l;
+        elab[static_cast<uint64_t>(v)] = static_cast<uint32_t>(l);
+    }
+    const uint64_t w = (uint64_t)t * (kTile / 32) + threadIdx.x;
+    if (threadIdx.x < kTile / 32 && w < ((uint64_t)n + 31) / 32) dbits[w] = 0u;
+}
+
+// Async emission, last step (gs_cc_emit_delta_async into device or pinned host buffers): the packed
+// pairs (*total of them, nothing if that exceeds cap) to the caller's buffers — pinned host memory
+// through its device mapping, 16 B per lane where the buffers allow (a wave writes 1 KiB
+// contiguously). Launched with a few workgroups on a stream of its own: it overlaps the next
+// window's fold, and a full-width grid of PCIe writers slowed that fold by ~20 %.
+template <typename IdT>
+__device__ __forceinline__ void copy_ids(const IdT* __restrict__ src, IdT* __restrict__ dst, uint64_t n) {
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t head = 0;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+        constexpr uint64_t kPer = 16 / sizeof(IdT);
+        const uint64_t nv = n / kPer;
+        const uint4* s4 = reinterpret_cast<const uint4*>(src);
+        uint4* d4 = reinterpret_cast<uint4*>(dst);
+        constexpr int kU = 4;                                     // 4 loads in flight per thread
+        uint64_t i = tid;
+        for (; i + (kU - 1) * nt < nv; i += kU * nt) {
+            uint4 q[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) q[u] = s4[i + u * nt];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) d4[i + u * nt] = q[u];
+        }
+        for (; i < nv; i += nt) d4[i] = s4[i];
+        head = nv * kPer;
+    }
+    for (uint64_t i = head + tid; i < n; i += nt) dst[i] = src[i];
 }
 
 template <typename IdT>
-__global__ __launch_bounds__(kTileThreads) void k_delta_scatter(const uint32_t* __restrict__ parent, uint32_t n,
-                                                                uint32_t* __restrict__ elab,
-                                                                const uint32_t* __restrict__ dbits,
-                                                                const uint64_t* __restrict__ off, IdT* __restrict__ vout,
-                                                                IdT* __restrict__ lout) {
-    const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kTilePerThread;
-    uint32_t p[kTilePerThread];
-    uint32_t hit = 0, c = 0;
-    const uint32_t d = base < n ? delta_bits(dbits, base) : 0u;
-#pragma unroll
-    for (int k = 0; k < kTilePerThread; ++k) {
-        const uint64_t v = base + k;
-        p[k] = kInvalid;
-        if (((d >> k) & 1u) && v < n) {
-            p[k] = parent[v];
-            if (p[k] != kInvalid && p[k] != elab[v]) { hit |= 1u << k; ++c; }
-        }
-    }
-    uint32_t tot;
-    uint64_t pos = off[blockIdx.x] + block_exclusive_scan(c, &tot);
-#pragma unroll
-    for (int k = 0; k < kTilePerThread; ++k) {
-        if (!((hit >> k) & 1u)) continue;
-        vout[pos] = static_cast<IdT>(base + k);
-        lout[pos] = static_cast<IdT>(p[k]);
-        elab[base + k] = p[k];
-        ++pos;
-    }
+__global__ __launch_bounds__(256) void k_delta_copy(const IdT* __restrict__ sv, const IdT* __restrict__ sl,
+                                                    const uint64_t* __restrict__ total, uint64_t cap,
+                                                    IdT* __restrict__ vout, IdT* __restrict__ lout,
+                                                    unsigned long long* __restrict__ count_out) {
+    const uint64_t n = *total;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *count_out = n;
+    if (n > cap) return;
+    copy_ids(sv, vout, n);
+    copy_ids(sl, lout, n);
 }
 
 // Partial-summary export (multi-GPU CombineCC): every pending hook-log entry v (a root hooked

@@ -39,6 +39,7 @@ EXPORTED_SYMBOLS = (
     "gs_cc_create", "gs_cc_destroy", "gs_cc_reset", "gs_cc_set_stream", "gs_cc_get_stream",
     "gs_cc_sync", "gs_cc_fold", "gs_cc_fold_pairs", "gs_cc_merge", "gs_cc_combine",
     "gs_cc_close_window", "gs_cc_stats", "gs_cc_emit_dense", "gs_cc_emit_pairs", "gs_cc_emit_delta",
+    "gs_cc_emit_delta_async", "gs_cc_emit_wait",
     "gs_cc_checksum", "gs_cc_find", "gs_cc_find_flags", "gs_cc_labels_device", "gs_cc_export_marks",
     "gs_cc_fold_pairs32", "gs_cc_export_marks_async", "gs_cc_set_marking", "gs_cc_timing", "gs_cc_kernel_time", "gs_cc_kernel_units", "gs_gen_rmat", "gs_gen_er", "gs_parse_edges",
     "gs_bip_create", "gs_bip_destroy", "gs_bip_reset", "gs_bip_set_stream", "gs_bip_sync", "gs_bip_fold",
@@ -126,6 +127,8 @@ def lib() -> ctypes.CDLL:
         "gs_cc_emit_dense": [vp, vp, u64],
         "gs_cc_emit_pairs": [vp, vp, vp, u64, P(u64)],
         "gs_cc_emit_delta": [vp, vp, vp, u64, P(u64)],
+        "gs_cc_emit_delta_async": [vp, vp, vp, u64, P(u64)],
+        "gs_cc_emit_wait": [vp, ctypes.c_uint32],
         "gs_cc_checksum": [vp, P(u64), P(u64), P(u64)],
         "gs_cc_find": [vp, vp, vp, u64],
         "gs_cc_find_flags": [vp, vp, vp, vp, u64],

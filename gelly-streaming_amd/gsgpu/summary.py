@@ -80,6 +80,7 @@ class DisjointSet:
         call("gs_cc_create", ctypes.byref(h), ctypes.byref(cfg))
         self._h = h
         self.track_marks = bool(track_marks)
+        self._epend = []                        # async delta emissions not yet waited for
         if stream is not None:
             self.set_stream(stream)
 
@@ -257,6 +258,24 @@ class DisjointSet:
         cnt = U64()
         call("gs_cc_emit_delta", self.handle, pv, pl, min(cap, cap2), ctypes.byref(cnt))
         return vertices[:cnt.value], labels[:cnt.value]
+
+    def delta_async(self, vertices, labels) -> None:
+        """gs_cc_emit_delta_async: this window's delta, enqueued only, into device tensors or PINNED
+        host tensors (id_bits wide); the next fold may be enqueued at once. The buffers are valid
+        after emit_wait() returns their entry."""
+        pv, kv, cap = _buf(vertices, self.id_bits, "vertices")
+        pl, kl, cap2 = _buf(labels, self.id_bits, "labels")
+        cnt = U64()
+        call("gs_cc_emit_delta_async", self.handle, pv, pl, min(cap, cap2), ctypes.byref(cnt))
+        self._epend.append((vertices, labels, cnt, kv, kl))
+
+    def emit_wait(self, keep: int = 0):
+        """gs_cc_emit_wait: completes async emissions, oldest first, until at most `keep` are
+        pending; returns [(vertices_prefix, labels_prefix), ...] of the completed ones."""
+        n_done = max(len(self._epend) - keep, 0)
+        done, self._epend = self._epend[:n_done], self._epend[n_done:]
+        call("gs_cc_emit_wait", self.handle, keep)
+        return [(v[:c.value], l[:c.value]) for v, l, c, _, _ in done]
 
     # ---- checkpoint / resume (Merger implements ListCheckpointed, SummaryAggregation.java:127-135) ----
     def snapshot(self) -> Tuple[np.ndarray, np.ndarray]:

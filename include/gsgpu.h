@@ -125,6 +125,18 @@ int gs_cc_emit_pairs(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uin
  * a bigger buffer). Applying every delta in order to a map reproduces gs_cc_emit_pairs. Output
  * element width = id_bits; vertices/labels host or device. Dense ids only. Implies close_window. */
 int gs_cc_emit_delta(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uint64_t* n_out);
+/* gs_cc_emit_delta, enqueued only (the per-window Merger emission without a host wait): the delta is
+ * computed on the handle's stream into one of two device slots — the next fold can be enqueued at
+ * once — and its size into a pinned word. gs_cc_emit_wait copies it to vertices/labels (device or
+ * host memory; pinned host memory copies at full PCIe rate) while the GPU runs whatever was enqueued
+ * after it; the buffers and *n_out are valid once gs_cc_emit_wait has returned that emission. An
+ * emission that did not fit cap consumed nothing (*n_out = its size, gs_cc_emit_wait returns
+ * GS_ERR_CAPACITY) and its pairs stay in the next delta. At most two emissions pending per handle;
+ * gs_cc_emit_delta waits for pending ones first. */
+int gs_cc_emit_delta_async(gs_cc_t* h, void* vertices, void* labels, uint64_t cap, uint64_t* n_out);
+/* Waits for async delta emissions, oldest first, until at most `keep` are pending (0: all; also done
+ * by gs_cc_sync), writing their *n_out. GS_ERR_CAPACITY if one of them did not fit its cap. */
+int gs_cc_emit_wait(gs_cc_t* h, uint32_t keep);
 /* Order-independent checksum of the canonical emission (definition shared with oracle/:
  * sum over seen v of splitmix64(v ^ splitmix64(label ^ 0xD1B54A32D192ED03))). Implies close_window. */
 int gs_cc_checksum(gs_cc_t* h, uint64_t* checksum, uint64_t* n_vertices, uint64_t* n_components);

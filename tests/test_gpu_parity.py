@@ -308,6 +308,69 @@ def test_emit_delta_rebuilds_every_emission(oracle, torch_cuda, bits):
         assert v.size == 0
 
 
+@pytest.mark.parametrize("where", ["pinned", "device"])
+@pytest.mark.parametrize("bits", [32, 64])
+def test_emit_delta_async_rebuilds_every_emission(oracle, torch_cuda, bits, where):
+    """gs_cc_emit_delta_async + gs_cc_emit_wait (the per-window emission without a host wait, two
+    slots in flight): the deltas, applied in order, reproduce every window's emission (oracle
+    checksums); an emission that does not fit fails at the wait and consumes nothing; pageable host
+    buffers are refused (SummaryAggregation.java:110-111)."""
+    torch = torch_cuda
+    from pyoracle import dense_checksum
+    s, d = oracle.gen_rmat(0, 1 << 18, 15, 4)
+    cap, W = 1 << 15, 1 << 15
+    want = oracle.run(s, d, W, partitions=2, emit=EMIT_CHECKSUM, label_cap=cap)
+    ds = DisjointSet(cap, id_bits=bits)
+    dt = torch.int32 if bits == 32 else torch.int64
+
+    def mk(n):
+        return torch.empty(n, dtype=dt).pin_memory() if where == "pinned" else torch.empty(n, dtype=dt, device="cuda")
+
+    bufs = [(mk(cap), mk(cap)) for _ in range(2)]
+    mirror = np.full(cap, -1, dtype=np.int64)
+    sums = []
+
+    def apply(done):
+        for v, l in done:
+            v = v.cpu().numpy().astype(np.int64)
+            l = l.cpu().numpy().astype(np.int64)
+            assert (np.diff(v) > 0).all()
+            mirror[v] = l
+            sums.append(dense_checksum(mirror)[0])
+
+    for w, lo in enumerate(range(0, s.size, W)):
+        ds.fold(s[lo:lo + W], d[lo:lo + W])
+        ds.delta_async(*bufs[w & 1])
+        apply(ds.emit_wait(1))
+    apply(ds.emit_wait(0))
+    assert sums == [int(x) for x in want["checksums"]]
+    pv, pl = ds.pairs()
+    np.testing.assert_array_equal(np.nonzero(mirror >= 0)[0], pv)
+    np.testing.assert_array_equal(mirror[pv], pl)
+    # too small: GS_ERR_CAPACITY at the wait, nothing consumed (the next delta is the whole emission)
+    ds.reset()
+    ds.fold(s[:W], d[:W])
+    ds.delta_async(mk(1), mk(1))
+    with pytest.raises(GsError) as e:
+        ds.emit_wait(0)
+    assert e.value.code == _abi.GS_ERR_CAPACITY
+    v, l = ds.delta()
+    assert v.size == ds.stats()[0]
+    ds.delta_async(*bufs[0])                         # nothing changed since
+    ((v, l),) = ds.emit_wait(0)
+    assert v.numel() == 0
+    npdt = np.int32 if bits == 32 else np.int64       # pageable host memory: copied at the wait
+    ds.fold(s[W:2 * W], d[W:2 * W])
+    ds.delta_async(np.empty(cap, dtype=npdt), np.empty(cap, dtype=npdt))
+    ((v, l),) = ds.emit_wait(0)
+    mirror = np.full(cap, -1, dtype=np.int64)
+    mirror[v.astype(np.int64)] = l                    # (the first delta after reset was the sync one)
+    pv, pl = ds.pairs()
+    changed = np.isin(pv, v.astype(np.int64))
+    np.testing.assert_array_equal(mirror[pv[changed]], pl[changed])
+    assert v.size and (np.diff(v.astype(np.int64)) > 0).all()
+
+
 def test_reset_and_transient_state():
     ds = DisjointSet(64, id_bits=32)
     ds.union(1, 2)
