@@ -125,6 +125,12 @@ def layout(a, world: int, rank: int):
 
 def main():
     a = parse()
+    # stdout carries exactly the one JSON line: native libraries print banners there (RCCL's version
+    # block at communicator init), so fd 1 is pointed at stderr for the run and the line goes to a
+    # duplicate of the original stdout
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w", buffering=1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -410,7 +416,7 @@ def main():
         if not a.no_cpu_baseline and world == 1:
             log("timed region done (%.1f ms/step); cpu baseline..." % (elapsed / a.steps * 1e3))
             line["cpu_baseline"] = cpu_baseline(a, ds, window, src, dst, W_rank, nwin)
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=out, flush=True)
     if gather:
         tree.drain()
     ds.close()
