@@ -259,6 +259,12 @@ constexpr uint32_t kHotThresh = 3;                  // sightings before hot-set 
 // giant filter on (RMAT-26 window 1: 1487 -> 1297 us for one extra full close of 118 us; splits
 // at 2^21 or 2^23, or 3-5 doubling splits, gained less). Only where gbits outgrows L2.
 constexpr uint32_t kYoungSplitDiv = 16;
+// Small plain folds (config 5's 2^16-edge windows): one edge per thread, so a launch spreads over
+// more workgroups and each thread's chain of dependent unions is one union long (a 2^16-edge launch
+// at 4 edges per thread filled 64 workgroups). Config 5: 3.94 -> 5.09 G edges/s, per-window latency
+// p50 29.9 -> 23.5 us; at 2^20 edges per launch config 2 +3 %, config 4 -1.5 % (profiles/r03_small)
+constexpr uint64_t kSmallFoldEdges = 1u << 18;
+constexpr int kSmallEpt = 1;
 
 // ---- debug variables (read once per process; none is needed in production) ----
 //   GSGPU_FOLD_STATS=1       per-window fold counters on stderr (STATS kernel variants; same results)
@@ -271,6 +277,8 @@ struct DebugEnv {
     int fold_mode = kFoldAuto;
     uint32_t ring_min_bits = kRingMinBits;
     uint64_t young_split = ~0ull;                   // ~0: the production rule
+    uint64_t small_fold = kSmallFoldEdges;          // GSGPU_SMALL_FOLD: plain folds of at most this many edges...
+    int small_ept = kSmallEpt;                      // GSGPU_SMALL_EPT: ...take this many edges per thread
     DebugEnv() {
         const char* e = getenv("GSGPU_FOLD_STATS");
         fold_stats = e && atoi(e) != 0;
@@ -281,6 +289,10 @@ struct DebugEnv {
         if (e && *e) ring_min_bits = (uint32_t)strtoul(e, nullptr, 0);
         e = getenv("GSGPU_YOUNG_SPLIT");
         if (e && *e) young_split = strtoull(e, nullptr, 0);
+        e = getenv("GSGPU_SMALL_FOLD");
+        if (e && *e) small_fold = strtoull(e, nullptr, 0);
+        e = getenv("GSGPU_SMALL_EPT");
+        if (e && *e) small_ept = atoi(e) == 1 ? 1 : (atoi(e) == 2 ? 2 : 4);
 
     }
 };
@@ -306,7 +318,7 @@ static void launch_warm_build(gs_cc_t* h, hipEvent_t stop);
 
 template <typename IdT, bool AOS>
 void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool young = false) {
-    const int ept = young ? kYoungEpt : kEdgesPerThread;
+    const int ept = young ? kYoungEpt : (n <= dbg().small_fold ? dbg().small_ept : kEdgesPerThread);
     const bool persist = young && h->cus > 0;
     // The first young launch after reset folds into an EMPTY forest: every hub's first hooks and
     // the giant root's repeated re-hooks collide there, so it keeps at most ~1/16 of its edges in
@@ -338,6 +350,7 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
             (const IdT*)a, (const IdT*)b, f)
     if (h->dstats) { if (h->mark) GS_LAUNCH_FOLD(true, false, 4, true); else GS_LAUNCH_FOLD(false, false, 4, true); }
     else if (ept == kYoungEpt) { if (h->mark) GS_LAUNCH_FOLD(true, false, kYoungEpt, false); else GS_LAUNCH_FOLD(false, false, kYoungEpt, false); }
+    else if (ept == 1) { if (h->mark) GS_LAUNCH_FOLD(true, false, 1, false); else GS_LAUNCH_FOLD(false, false, 1, false); }
     else if (h->mark) { if (vec) GS_LAUNCH_FOLD(true, true, 4, false); else GS_LAUNCH_FOLD(true, false, 4, false); }
     else { if (vec) GS_LAUNCH_FOLD(false, true, 4, false); else GS_LAUNCH_FOLD(false, false, 4, false); }
 #undef GS_LAUNCH_FOLD
