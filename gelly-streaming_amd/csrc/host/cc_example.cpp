@@ -58,13 +58,15 @@ int main(int argc, char** argv) {
     }
     try {
         ConnectedComponents<int64_t> cc(merge_ms, 0, 0, window_edges);
+        // the latest emission, kept current from each window's delta (the emissions are cumulative,
+        // so at a print-window boundary it is exactly what FlattenSet + IdentityFold printed)
         std::map<int64_t, int64_t> latest;
+        std::vector<int64_t> dv, dl;
         auto wins = s.windows(merge_ms, window_edges);
         size_t wi = 0;
         long current_print = -1;
         auto flush = [&]() {
             for (auto& kv : latest) std::printf("(%lld,%lld)\n", (long long)kv.first, (long long)kv.second);
-            latest.clear();
         };
         cc.run(s, [&](DisjointSet<int64_t>& ds) {
             // event time of this emission = end of its window (count windows: index)
@@ -73,7 +75,8 @@ int main(int argc, char** argv) {
             const long pw = print_ms > 0 ? t / print_ms : 0;
             if (current_print >= 0 && pw != current_print) flush();
             current_print = pw;
-            for (auto& kv : ds.getMatches()) latest[kv.first] = kv.second;   // FlattenSet + IdentityFold
+            ds.delta(dv, dl);                        // FlattenSet + IdentityFold at O(changes)
+            for (size_t i = 0; i < dv.size(); ++i) latest[dv[i]] = dl[i];
         });
         flush();
     } catch (const GsError& e) {

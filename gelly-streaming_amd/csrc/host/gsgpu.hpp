@@ -118,6 +118,24 @@ public:
         l.resize(got);
     }
 
+    // the per-window delta of the emission (gs_cc_emit_delta): the (vertex, label) pairs new or
+    // changed since this summary's previous delta, sorted by vertex — a host-side mirror of the
+    // Merger's output stays current at O(changes) per window (SummaryAggregation.java:110-111)
+    void delta(std::vector<K>& v, std::vector<K>& l) {
+        uint64_t cap = size(), got = 0;
+        if (cap == 0) cap = 1;
+        for (;;) {
+            v.resize(cap);
+            l.resize(cap);
+            const int rc = gs_cc_emit_delta(h_, v.data(), l.data(), cap, &got);
+            if (rc == GS_ERR_CAPACITY) { cap = got; continue; }
+            check(rc, "gs_cc_emit_delta");
+            break;
+        }
+        v.resize(got);
+        l.resize(got);
+    }
+
     // Merger checkpoint (ListCheckpointed, SummaryAggregation.java:127-135): the summary as its
     // canonical (vertex, label) pairs; restore = reset + union(v, label) for every pair
     void snapshot(std::vector<K>& v, std::vector<K>& l) { pairs(v, l); }
