@@ -1262,7 +1262,7 @@ static int delta_begin(gs_cc_t* h, const char* who, void* vertices, void* labels
 // addresses, cap entries — elab and the dirty words updated, only if the delta fits cap). Returns
 // the device word holding the size.
 static int delta_enqueue(gs_cc_t* h, uint64_t cap, void* vo, void* lo, unsigned long long* total_host,
-                         const uint64_t** total) {
+                         const uint64_t** total, uint64_t* total_out = nullptr) {
     const uint32_t ntiles = (uint32_t)((h->cap + kTile - 1) / kTile);
     const size_t esz = h->cfg.id_bits / 8;
     const size_t cnt_b = ((size_t)ntiles * 4 + 15) & ~(size_t)15;
@@ -1279,11 +1279,12 @@ static int delta_enqueue(gs_cc_t* h, uint64_t cap, void* vo, void* lo, unsigned 
                        ntiles, cnt, (IdT*)sv, (IdT*)sl);                                                                   \
     hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, h->stream, cnt, off, ntiles, total_host);                      \
     hipLaunchKernelGGL(k_delta_pack<IdT>, dim3(ntiles), dim3(256), 0, h->stream, (const IdT*)sv, (const IdT*)sl,           \
-                       (const uint32_t*)cnt, (const uint64_t*)off, ntiles, cap, h->elab, h->dbits, h->cap, (IdT*)vo, (IdT*)lo)
+                       (const uint32_t*)cnt, (const uint64_t*)off, ntiles, cap, h->elab, h->dbits, h->cap, (IdT*)vo, (IdT*)lo, \
+                       total_out)
     if (h->cfg.id_bits == 32) { GS_DELTA(uint32_t); } else { GS_DELTA(int64_t); }
 #undef GS_DELTA
     GS_HIP(hipGetLastError());
-    *total = off + ntiles;
+    *total = total_out ? total_out : off + ntiles;
     return GS_OK;
 }
 
@@ -1316,8 +1317,8 @@ static int delta_slot(gs_cc_t* h, int si, uint64_t cap, char** sv, char** sl) {
     const size_t esz = h->cfg.id_bits / 8;
     const uint64_t scap = std::min<uint64_t>(cap, h->cap);
     gs_cc::EmitSlot& S = h->eslot[si];
-    GS_TRY(ensure_buf(&S.mem, &S.bytes, std::max<size_t>(2 * scap * esz, 16)));
-    *sv = static_cast<char*>(S.mem);
+    GS_TRY(ensure_buf(&S.mem, &S.bytes, 16 + 2 * scap * esz));     // [size word | vertices | labels]
+    *sv = static_cast<char*>(S.mem) + 16;
     *sl = *sv + scap * esz;
     return GS_OK;
 }
@@ -1374,7 +1375,7 @@ int gs_cc_emit_delta_async(gs_cc_t* h, void* vertices, void* labels, uint64_t ca
     // the size goes to the pinned word from the copy kernel (a host store at the end of the scan
     // cost that kernel ~20 us: the release of a kernel that writes host memory) or, for pageable
     // buffers, by a DMA behind the pack
-    GS_TRY(delta_enqueue(h, cap, sv, sl, nullptr, &total));
+    GS_TRY(delta_enqueue(h, cap, sv, sl, nullptr, &total, static_cast<uint64_t*>(h->eslot[si].mem)));
     // buffers the device can write: copied out right away, on estream, by a few workgroups (their
     // PCIe writes overlap the next fold); pageable ones: by DMA at the wait
     void* dv = cap ? device_view(vertices) : nullptr;
@@ -1413,7 +1414,7 @@ int gs_cc_emit_wait(gs_cc_t* h, uint32_t keep) {
         if (n > p.cap) { over = n; over_cap = p.cap; continue; }
         if (n && !p.kcopy) {
             const hipMemcpyKind kind = hipMemcpyDeviceToHost;      // pageable host buffers
-            char* sv = static_cast<char*>(h->eslot[p.slot].mem);
+            char* sv = static_cast<char*>(h->eslot[p.slot].mem) + 16;       // past the size word
             const uint64_t scap = std::min<uint64_t>(p.cap, h->cap);
             GS_HIP(hipMemcpyAsync(p.vertices, sv, n * esz, kind, h->estream));
             GS_HIP(hipMemcpyAsync(p.labels, sv + scap * esz, n * esz, kind, h->estream));

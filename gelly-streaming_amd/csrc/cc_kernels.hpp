@@ -1674,7 +1674,11 @@ __global__ __launch_bounds__(256) void k_delta_pack(const IdT* __restrict__ sv, 
                                                     const uint32_t* __restrict__ tile_count,
                                                     const uint64_t* __restrict__ off, uint32_t ntiles, uint64_t cap,
                                                     uint32_t* __restrict__ elab, uint32_t* __restrict__ dbits, uint32_t n,
-                                                    IdT* __restrict__ vout, IdT* __restrict__ lout) {
+                                                    IdT* __restrict__ vout, IdT* __restrict__ lout,
+                                                    uint64_t* __restrict__ total_out) {
+    // the size also to the output slot's own word (async emissions: the copy kernel reads it there,
+    // after the next emission may already have reused off[])
+    if (total_out && blockIdx.x == 0 && threadIdx.x == 0) *total_out = off[ntiles];
     if (off[ntiles] > cap) return;
     const uint32_t t = blockIdx.x;
     const uint32_t c = tile_count[t];
