@@ -617,11 +617,15 @@ def test_bench_two_ranks_one_gpu_verified(merge, scaling):
 
 
 @pytest.mark.parametrize("extra", [["--id-bits", "64"], ["--host-input"], ["--host-input", "--id-bits", "64"],
-                                   ["--workload", "c3_single"], ["--emit-host"]],
-                         ids=["int64", "host", "host_int64", "single_window", "emit_host"])
+                                   ["--workload", "c3_single"], ["--emit-host"], ["--emit-host", "--emit-sync"],
+                                   ["--exchange-world1"]],
+                         ids=["int64", "host", "host_int64", "single_window", "emit_host", "emit_host_sync",
+                              "exchange_world1"])
 def test_bench_lines_verified(extra):
     """The extra bench lines (int64 ids, pinned-host input through the double-buffered staging,
-    one window), end to end against the independent torch CC, at RMAT-22 / 2^20-edge windows."""
+    one window, per-window host emission async and blocking, the C-ABI exchange over RCCL at world
+    1), end to end against the independent torch CC, at RMAT-22 / 2^20-edge windows. stdout is the
+    one JSON line (RCCL's banner and every other native print go to stderr)."""
     import subprocess, sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, os.path.join(root, "bench.py"), "--steps", "1", "--warmup", "0", "--scale", "22",
@@ -629,9 +633,11 @@ def test_bench_lines_verified(extra):
     if "--workload" not in extra:
         cmd += ["--window-log2", "20"]
     out = subprocess.check_output(cmd, timeout=300).decode()
-    line = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert len(out.strip().splitlines()) == 1, out[:2000]
+    line = json.loads(out)
     assert line["verify"] == {"edges_consistent": True, "labels_minimal_idempotent": True, "equals_torch_cc": True}
-
+    if "--emit-host" in extra:
+        assert line["emit_host"]["windows"] > 0
 
 # ---------------- BASELINE configs at full size, per-window bit-exact vs the C oracle ----------------
 def _device_stream(gen_kind, n, param, seed):
