@@ -231,6 +231,10 @@ constexpr unsigned kYoungBlocksPerCu = 2;
 // RMAT-26 sweep of the divisor 16 / 32 / 64 / 128 / 256: 16.29 / 16.25 / 16.47 / 17.03 / 18.19 ms
 // per step, profiles/r03_yfirst_sweep.txt; at 2^22 edges 16 keeps the 2-per-CU grid)
 constexpr uint64_t kYoungFirstDiv = 16;
+// ... and at least this many workgroups (config 2's 2^18-edge first launch: floor 8 / 16 / 32 / 64
+// -> 0.613 / 0.610 / 0.608 / 0.566 ms per step, profiles/r03_yfloor.txt; launches of 2^19 edges and
+// more, configs 3 and 4, are above the floor)
+constexpr uint64_t kYoungFirstMinWg = 64;
 // Folding a partial summary (AOS pairs: fold_pairs / the multi-GPU merge): the pairs (v, R) of one
 // component all name its root R; while R's component is not yet joined to the receiver's, every
 // pair in flight CASes the same word (RMAT-26 window-1 deltas: 5-14 ms for 6M pairs). A head
@@ -279,6 +283,7 @@ struct DebugEnv {
     uint64_t young_split = ~0ull;                   // ~0: the production rule
     uint64_t small_fold = kSmallFoldEdges;          // GSGPU_SMALL_FOLD: plain folds of at most this many edges...
     int small_ept = kSmallEpt;                      // GSGPU_SMALL_EPT: ...take this many edges per thread
+    uint64_t young_first_min = kYoungFirstMinWg;    // GSGPU_YOUNG_FIRST_MIN: workgroup floor of the first young launch
     DebugEnv() {
         const char* e = getenv("GSGPU_FOLD_STATS");
         fold_stats = e && atoi(e) != 0;
@@ -291,6 +296,8 @@ struct DebugEnv {
         if (e && *e) young_split = strtoull(e, nullptr, 0);
         e = getenv("GSGPU_SMALL_FOLD");
         if (e && *e) small_fold = strtoull(e, nullptr, 0);
+        e = getenv("GSGPU_YOUNG_FIRST_MIN");
+        if (e && *e) young_first_min = std::max<uint64_t>(1, strtoull(e, nullptr, 0));
         e = getenv("GSGPU_SMALL_EPT");
         if (e && *e) small_ept = atoi(e) == 1 ? 1 : (atoi(e) == 2 ? 2 : 4);
 
@@ -324,7 +331,8 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
     // the giant root's repeated re-hooks collide there, so it keeps at most ~1/16 of its edges in
     // flight (>= 32 workgroups). BASELINE config 2 (RMAT-20, the whole 2^18-edge launch in flight
     // at 2/CU): 0.97 -> 0.64 ms per step; configs 3-5 unchanged (profiles/r03_ygrid2).
-    const uint64_t ycap = h->edges_since_reset ? ~0ull : std::max<uint64_t>(32, n / (kYoungFirstDiv * kFoldThreads * kYoungEpt));
+    const uint64_t ycap = h->edges_since_reset ? ~0ull
+                                               : std::max<uint64_t>(dbg().young_first_min, n / (kYoungFirstDiv * kFoldThreads * kYoungEpt));
     const unsigned grid = persist ? (unsigned)std::min<uint64_t>(std::min<uint64_t>((uint64_t)h->cus * kYoungBlocksPerCu, ycap),
                                                                   grid_for((n + ept - 1) / ept, kFoldThreads, 1u << 20))
                                   : grid_for((n + ept - 1) / ept, kFoldThreads, 16384);
