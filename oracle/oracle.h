@@ -61,7 +61,11 @@ enum {
     GSO_EMIT_NONE = 0,       /* fold + combine + merge only                                   */
     GSO_EMIT_FLATTEN = 1,    /* + FlattenSet (find() for every vertex, ConnectedComponentsExample.java:143-156) */
     GSO_EMIT_CHECKSUM = 2,   /* + canonical checksum per window                               */
-    GSO_EMIT_DENSE = 3       /* + canonical dense labels per window into out_labels[w*cap + v] */
+    GSO_EMIT_DENSE = 3,      /* + canonical dense labels per window into out_labels[w*cap + v] */
+    GSO_EMIT_TRACK = 4       /* + canonical checksum per window from the incremental tracker
+                                (emission.c; ids < label_cap), cross-checked against the full
+                                canonical checksum of the Merger's summary every verify_every
+                                windows and after the last (a difference returns -2)           */
 };
 
 typedef struct {
@@ -70,6 +74,7 @@ typedef struct {
     int      threads;        /* host threads used for the per-partition folds (<= partitions)  */
     int      emit_mode;      /* GSO_EMIT_*                                                     */
     uint64_t label_cap;      /* for GSO_EMIT_DENSE: dense label array length per window        */
+    uint64_t verify_every;   /* for GSO_EMIT_TRACK: full-checksum cross-check period (0 = last only) */
 } gso_run_cfg;
 
 typedef struct {
@@ -101,6 +106,14 @@ int gso_cc_run_counts(const int64_t* init_v, const int64_t* init_l, uint64_t n_i
                       const int64_t* src, const int64_t* dst, uint64_t n, const gso_run_cfg* cfg,
                       uint64_t* out_checksums, uint64_t* out_counts, int64_t* out_labels, int64_t* final_labels,
                       gso_run_stats* stats);
+
+/* ---------------- incremental canonical emission (emission.c) ---------------- */
+typedef struct gso_track gso_track;
+gso_track* gso_track_new(uint64_t cap);            /* dense ids in [0, cap)                    */
+void       gso_track_free(gso_track* t);
+void       gso_track_union(gso_track* t, int64_t u, int64_t v);
+uint64_t   gso_track_checksum(const gso_track* t, uint64_t* n_vertices, uint64_t* n_components);
+int        gso_track_overflow(const gso_track* t);  /* an id outside [0, cap) was seen         */
 
 /* ---------------- deterministic synthetic streams (same definition as the device generators) ---------------- */
 uint64_t gso_splitmix64(uint64_t x);

@@ -87,10 +87,17 @@ int gso_cc_run_counts(const int64_t* init_v, const int64_t* init_l, uint64_t n_i
     fold_job* jobs = (fold_job*)calloc((size_t)T, sizeof(fold_job));
     pthread_t* th = (pthread_t*)calloc((size_t)T, sizeof(pthread_t));
     gso_ds* summary = NULL;            /* Merger.summary = initialVal (empty) */
+    gso_track* track = NULL;           /* GSO_EMIT_TRACK: the incremental canonical emission */
+    int rc = 0;
+    if (cfg->emit_mode == GSO_EMIT_TRACK) {
+        track = gso_track_new(cfg->label_cap);
+        if (!track) { free(partials); free(jobs); free(th); return -1; }
+    }
     if (n_init) {                      /* Merger.restoreState (SummaryAggregation.java:131-135): the
                                           snapshotted summary, rebuilt from its (vertex, label) pairs */
         summary = gso_ds_new();
         for (uint64_t i = 0; i < n_init; ++i) gso_ds_union(summary, init_v[i], init_l[i]);
+        if (track) for (uint64_t i = 0; i < n_init; ++i) gso_track_union(track, init_v[i], init_l[i]);
     }
     uint64_t w = 0;
     volatile uint64_t sink = 0;
@@ -136,9 +143,25 @@ int gso_cc_run_counts(const int64_t* init_v, const int64_t* init_l, uint64_t n_i
                 out_checksums[w] = gso_ds_canonical_checksum(summary, out_counts ? &out_counts[2 * w] : NULL,
                                                              out_counts ? &out_counts[2 * w + 1] : NULL);
             break;
+        case GSO_EMIT_TRACK: {
+            for (uint64_t i = lo; i < lo + len; ++i) gso_track_union(track, src[i], dst[i]);
+            uint64_t nv = 0, nc = 0;
+            const uint64_t h = gso_track_checksum(track, &nv, &nc);
+            if (out_checksums) out_checksums[w] = h;
+            if (out_counts) { out_counts[2 * w] = nv; out_counts[2 * w + 1] = nc; }
+            const int last = lo + len >= n;
+            if (gso_track_overflow(track)) { rc = -3; goto done; }
+            if (last || (cfg->verify_every && (w + 1) % cfg->verify_every == 0)) {
+                uint64_t fv = 0, fc = 0;
+                const uint64_t fh = gso_ds_canonical_checksum(summary, &fv, &fc);
+                if (fh != h || fv != nv || fc != nc) { rc = -2; goto done; }
+            }
+            break;
+        }
         default: break;
         }
     }
+done:;
     double t1 = now_s();
     (void)sink;
     if (stats) {
@@ -153,6 +176,7 @@ int gso_cc_run_counts(const int64_t* init_v, const int64_t* init_l, uint64_t n_i
         else for (uint64_t v = 0; v < cfg->label_cap; ++v) final_labels[v] = -1;
     }
     gso_ds_free(summary);
+    gso_track_free(track);
     free(partials); free(jobs); free(th);
-    return 0;
+    return rc;
 }

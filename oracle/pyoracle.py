@@ -185,13 +185,13 @@ def canonical_to_dense(canon: Dict, cap: int) -> np.ndarray:
 # --------------------------------------------------------------------------------------------
 # ctypes binding of the C restatement
 # --------------------------------------------------------------------------------------------
-EMIT_NONE, EMIT_FLATTEN, EMIT_CHECKSUM, EMIT_DENSE = 0, 1, 2, 3
+EMIT_NONE, EMIT_FLATTEN, EMIT_CHECKSUM, EMIT_DENSE, EMIT_TRACK = 0, 1, 2, 3, 4
 
 
 class _RunCfg(ctypes.Structure):
     _fields_ = [("window_edges", ctypes.c_uint64), ("partitions", ctypes.c_int),
                 ("threads", ctypes.c_int), ("emit_mode", ctypes.c_int),
-                ("label_cap", ctypes.c_uint64)]
+                ("label_cap", ctypes.c_uint64), ("verify_every", ctypes.c_uint64)]
 
 
 class _RunStats(ctypes.Structure):
@@ -259,7 +259,7 @@ class COracle:
     # ---- pipeline ----
     def run(self, src: np.ndarray, dst: np.ndarray, window_edges: int, partitions: int = 1,
             threads: int = 1, emit: int = EMIT_CHECKSUM, label_cap: int = 0,
-            want_final: bool = False, init=None):
+            want_final: bool = False, init=None, verify_every: int = 0):
         """The pipeline over (src, dst); init = (vertices, labels): the Merger restored from that
         snapshot first (untimed), so a run can start in the middle of a stream."""
         src = np.ascontiguousarray(src, dtype=np.int64)
@@ -267,7 +267,7 @@ class COracle:
         n = int(src.size)
         W = window_edges if window_edges > 0 else max(n, 1)
         nwin = (n + W - 1) // W if n else 0
-        cfg = _RunCfg(window_edges, partitions, threads, emit, label_cap)
+        cfg = _RunCfg(window_edges, partitions, threads, emit, label_cap, verify_every)
         st = _RunStats()
         sums = np.zeros(max(nwin, 1), dtype=np.uint64)
         counts = np.zeros((max(nwin, 1), 2), dtype=np.uint64)     # per window: (vertices, components)
@@ -279,6 +279,8 @@ class COracle:
             il = np.ascontiguousarray(init[1], dtype=np.int64)
         rc = self.L.gso_cc_run_counts(_p(iv), _p(il), 0 if iv is None else int(iv.size), _p(src), _p(dst), n,
                                       ctypes.byref(cfg), _p(sums), _p(counts), _p(labels), _p(final), ctypes.byref(st))
+        if rc == -2:
+            raise RuntimeError("gso_cc_run: the incremental emission tracker disagrees with the summary's canonical checksum")
         if rc != 0:
             raise RuntimeError("gso_cc_run failed: %d" % rc)
         return {"windows": int(st.windows), "checksums": sums[:nwin], "counts": counts[:nwin], "labels": labels,

@@ -5,6 +5,11 @@ configuration (the library reads its debug variables once per process; csrc/cc_a
   windows bit-exact vs the C oracle's fixture (tests/golden/headline_rmat26.json), two back-to-back
   passes with reset, final labels vs an independent torch CC (tests/headline_check.py); the same
   with the reference's Long (int64) ids.
+* test_headline_config_production[fold_windows]: the bench's timed call (gs_cc_fold_windows) over the
+  whole stream in one call and in calls of 8 windows, each call's last window vs the fixture.
+* test_c5_config_production: BASELINE config 5 (RMAT-24, 4,096 windows of 2^16 edges) — all 4,096
+  windows vs the C oracle's fixture (tests/golden/c5_rmat24.json), per-window calls and the
+  gs_cc_fold_windows path (one call; calls of 256 windows).
 * test_headline_config_eight_ranks_one_gpu: the same stream as BASELINE config 3's 8-GPU strong
   layout (2^24-edge global windows, 2^21 edges per rank), 8 ranks through the C-ABI exchange on
   one GPU in allgather, gather and tree modes, all 64 windows vs the fixture
@@ -36,7 +41,8 @@ def _last_json(out: bytes):
     return json.loads([l for l in out.decode().splitlines() if l.startswith("{")][-1])
 
 
-@pytest.mark.parametrize("args", [["--steps", "2"], ["--id-bits", "64", "--no-torch"]], ids=["int32_two_passes", "int64"])
+@pytest.mark.parametrize("args", [["--steps", "2"], ["--id-bits", "64", "--no-torch"], ["--fold-windows", "--no-torch"]],
+                         ids=["int32_two_passes", "int64", "fold_windows"])
 def test_headline_config_production(args):
     out = subprocess.check_output([sys.executable, os.path.join(HERE, "headline_check.py")] + args, env=_env({}),
                                   timeout=900)
@@ -44,6 +50,17 @@ def test_headline_config_production(args):
     print(r)
     assert r["fixture_windows_equal"], r
     assert r["final_equals_torch_cc"] is not False and r["labels_minimal_idempotent"], r
+    assert r["ok"], r
+
+
+@pytest.mark.parametrize("args", [["--fold-windows", "--chunk", "256"], ["--id-bits", "64", "--no-torch"]],
+                         ids=["int32_fold_windows", "int64"])
+def test_c5_config_production(args):
+    out = subprocess.check_output([sys.executable, os.path.join(HERE, "headline_check.py"), "--fixture", "c5"] + args,
+                                  env=_env({}), timeout=900)
+    r = _last_json(out)
+    print(r)
+    assert r["windows"] == 4096 and r["fixture_windows_equal"], r
     assert r["ok"], r
 
 

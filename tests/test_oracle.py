@@ -230,3 +230,32 @@ def test_headline_fixture_window1_live(oracle):
     r = oracle.run(s, d, W, partitions=3, threads=3, emit=EMIT_CHECKSUM)
     assert int(r["checksums"][0]) == int(fx["checksums"][0])
     assert [int(x) for x in r["counts"][0]] == [fx["vertices"][0], fx["components"][0]]
+
+
+@pytest.mark.parametrize("kind,param,n,W,seed", [("rmat", 16, 1 << 20, 1 << 12, 3), ("er", 1 << 16, 1 << 17, 1 << 10, 2),
+                                                 ("rmat", 12, 1 << 16, 333, 5)])
+def test_emission_tracker_matches_full_checksum(oracle, kind, param, n, W, seed):
+    """oracle/emission.c (GSO_EMIT_TRACK, used to mint the 4,096-window config-5 fixture) gives the
+    same per-window checksum, vertex and component counts as the full canonical checksum of the
+    Merger's summary (gso_ds_canonical_checksum) on every window; its own cross-check runs too."""
+    from pyoracle import EMIT_TRACK
+    s, d = oracle.gen_rmat(0, n, param, seed) if kind == "rmat" else oracle.gen_er(0, n, param, seed)
+    cap = (1 << param) if kind == "rmat" else param
+    a = oracle.run(s, d, W, partitions=4, threads=4, emit=EMIT_CHECKSUM, label_cap=cap)
+    b = oracle.run(s, d, W, partitions=4, threads=4, emit=EMIT_TRACK, label_cap=cap, verify_every=7)
+    np.testing.assert_array_equal(a["checksums"], b["checksums"])
+    np.testing.assert_array_equal(a["counts"], b["counts"])
+
+
+def test_c5_fixture_first_windows_live(oracle):
+    """tests/golden/c5_rmat24.json (tracker, P = 8) agrees with a live full-checksum oracle run of its
+    first 32 windows at another partition count (P = 3), and its counts are monotone."""
+    fx = json.load(open(os.path.join(GOLD, "c5_rmat24.json")))
+    assert fx["windows"] == 4096 and len(fx["checksums"]) == 4096 and fx["window_edges"] == 1 << 16
+    assert fx["vertices"] == sorted(fx["vertices"]) and fx["vertices"][-1] <= 1 << fx["scale"]
+    W, k = fx["window_edges"], 32
+    s, d = oracle.gen_rmat(0, k * W, fx["scale"], fx["seed"])
+    r = oracle.run(s, d, W, partitions=3, threads=3, emit=EMIT_CHECKSUM)
+    assert [int(x) for x in r["checksums"]] == [int(x) for x in fx["checksums"][:k]]
+    assert [int(x) for x in r["counts"][:, 0]] == fx["vertices"][:k]
+    assert [int(x) for x in r["counts"][:, 1]] == fx["components"][:k]
