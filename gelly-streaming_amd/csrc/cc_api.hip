@@ -779,6 +779,13 @@ int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int ns
     h->minkey_valid = false;
     FoldArgs f{0, h->parent, nullptr, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, nullptr};
     KTimer t(h, GS_K_MERGE);
+    if (h->sparse) {                                 // (id, id) int64 pairs, hashed to slots
+        const dim3 grid(grid_for(cap, 256, (unsigned)std::max(64, 4096 / nslots)), (unsigned)nslots);
+        klaunch(k_fold_slots_sparse, grid, dim3(256), h->stream, t.start(), t.stop(), slots, slot_words, skip, (uint64_t)0,
+                cap, f, sparse_args(h));
+        GS_HIP(hipGetLastError());
+        return GS_OK;
+    }
     const uint64_t head = cap > kMergeBulk ? std::min<uint64_t>(cap, kMergeHead) : 0;
     if (head) {
         const dim3 grid(grid_for(head, 256, 64), (unsigned)nslots);
@@ -790,6 +797,15 @@ int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int ns
     return GS_OK;
 }
 void cc_count_folded(gs_cc_t* h, uint64_t n) { h->edges_since_reset += n; }
+
+int cc_fold_pairs_any(gs_cc_t* h, const void* pairs, uint64_t n) {
+    GS_TRY(check(h));
+    GS_TRY(cc_settle(h));
+    h->fold_timer = GS_K_MERGE;
+    const int rc = fold_impl(h, pairs, nullptr, n, true, h->sparse ? 64 : 32);
+    h->fold_timer = GS_K_FOLD;
+    return rc;
+}
 
 void cc_set_settle(gs_cc_t* h, int (*fn)(void*), void* ctx) {
     h->settle_fn = fn;
@@ -807,7 +823,7 @@ int cc_settle(gs_cc_t* h) {
 
 int cc_export_async(gs_cc_t* h, void* pairs, uint64_t cap, unsigned long long* dcount, uint64_t expect) {
     GS_TRY(check(h));
-    if (!h->mark_buf || h->sparse) return fail(GS_ERR_UNSUPPORTED, "export: no marks on this handle");
+    if (!h->mark_buf) return fail(GS_ERR_UNSUPPORTED, "export: no marks on this handle");
     // (cap may be smaller than the log: the pending tail stays for the next export; the count word
     // receives the whole pending number, so the caller can tell)
     DeviceGuard g(h->device);
@@ -828,8 +844,6 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
     if (cfg->id_bits != 32 && cfg->id_bits != 64) return fail(GS_ERR_INVALID, "gs_cc_create: id_bits must be 32 or 64");
     const bool sparse = (cfg->flags & GS_CC_SPARSE_IDS) != 0;
     if (sparse && cfg->id_bits != 64) return fail(GS_ERR_INVALID, "gs_cc_create: GS_CC_SPARSE_IDS needs id_bits 64");
-    if (sparse && (cfg->flags & GS_CC_TRACK_MARKS))
-        return fail(GS_ERR_UNSUPPORTED, "gs_cc_create: GS_CC_TRACK_MARKS needs dense ids (the exchange is dense-id)");
     if (sparse && (cfg->vertex_capacity == 0 || cfg->vertex_capacity > (1ull << 30)))
         return fail(GS_ERR_INVALID, "gs_cc_create: sparse vertex_capacity must be in [1, 2^30]");
     if (cfg->vertex_capacity == 0 || cfg->vertex_capacity > 0xFFFFFFFFull)
@@ -1494,8 +1508,12 @@ int gsgpu::export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long
     {
         const unsigned grid = expect == ~0ull ? 1024u : (unsigned)std::min<uint64_t>(std::max<uint64_t>((expect + 255) / 256, 8), 1024);
         KTimer t(h, GS_K_EXPORT);
-        klaunch(k_export_log, dim3(grid), dim3(256), h->stream, t.start(), t.stop(), (const uint32_t*)h->mark_buf,
-                h->mark_ctr, (const uint32_t*)h->parent, (uint32_t*)out, cap, counter);
+        if (h->sparse)                               // (id, root id) as int64 pairs
+            klaunch(k_export_log_sparse, dim3(grid), dim3(256), h->stream, t.start(), t.stop(), (const uint32_t*)h->mark_buf,
+                    h->mark_ctr, (const uint32_t*)h->parent, sparse_args(h), (int64_t*)out, cap, counter);
+        else
+            klaunch(k_export_log, dim3(grid), dim3(256), h->stream, t.start(), t.stop(), (const uint32_t*)h->mark_buf,
+                    h->mark_ctr, (const uint32_t*)h->parent, (uint32_t*)out, cap, counter);
     }
     GS_HIP(hipGetLastError());
     return GS_OK;
@@ -1503,9 +1521,10 @@ int gsgpu::export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long
 
 static int export_check(gs_cc_t* h, const char* fn) {
     if (!h->mark_buf) return fail(GS_ERR_UNSUPPORTED, "%s: handle created without GS_CC_TRACK_MARKS", fn);
-    if (h->sparse) return fail(GS_ERR_UNSUPPORTED, "%s: sparse-id summary", fn);
     return GS_OK;
 }
+// bytes per exported pair: (uint32 vertex, uint32 root) dense, (int64 id, int64 root id) sparse
+static size_t pair_bytes(const gs_cc_t* h) { return h->sparse ? 16 : 8; }
 
 int gs_cc_export_marks(gs_cc_t* h, void* pairs, uint64_t cap, uint64_t* n_out) {
     GS_TRY(check(h));
@@ -1517,7 +1536,7 @@ int gs_cc_export_marks(gs_cc_t* h, void* pairs, uint64_t cap, uint64_t* n_out) {
     const bool dev = cap == 0 || is_device_pointer(pairs);
     void* out = pairs;
     if (!dev) {
-        GS_TRY(ensure_buf(&h->tmp, &h->tmp_bytes, cap * 8));
+        GS_TRY(ensure_buf(&h->tmp, &h->tmp_bytes, cap * pair_bytes(h)));
         out = h->tmp;
     }
     GS_TRY(export_launch(h, out, cap, h->dscratch));
@@ -1526,7 +1545,7 @@ int gs_cc_export_marks(gs_cc_t* h, void* pairs, uint64_t cap, uint64_t* n_out) {
     const uint64_t total = h->hscratch[0];
     *n_out = total < cap ? total : cap;
     if (!dev && *n_out) {
-        GS_HIP(hipMemcpyAsync(pairs, out, *n_out * 8, hipMemcpyDeviceToHost, h->stream));
+        GS_HIP(hipMemcpyAsync(pairs, out, *n_out * pair_bytes(h), hipMemcpyDeviceToHost, h->stream));
         GS_TRY(sync_and_check(h));
     }
     if (total > cap) return fail(GS_ERR_CAPACITY, "gs_cc_export_marks: %llu marked, capacity %llu (rest kept)",

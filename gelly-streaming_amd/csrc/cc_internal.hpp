@@ -17,6 +17,9 @@ int cc_info(gs_cc_t* h, CcInfo* out);
 int cc_export_async(gs_cc_t* h, void* pairs, uint64_t cap, unsigned long long* dcount, uint64_t expect = ~0ull);
 int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int nslots, int skip, uint64_t cap);
 void cc_count_folded(gs_cc_t* h, uint64_t n);
+// folds n exported partial-summary pairs (device buffer) as CombineCC does: uint32 (vertex, root)
+// pairs for dense handles, int64 (id, root id) pairs for sparse-id handles; timed as a merge
+int cc_fold_pairs_any(gs_cc_t* h, const void* pairs, uint64_t n);
 // a pending exchange verification of the handle's last window (comm.hip): cc_settle runs it once
 void cc_set_settle(gs_cc_t* h, int (*fn)(void*), void* ctx);
 int cc_settle(gs_cc_t* h);

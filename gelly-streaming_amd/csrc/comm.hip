@@ -33,12 +33,23 @@ namespace gsgpu {
 namespace {
 
 // pairs [n, m) of buf = copies of pair 0 (a repeated union is a no-op): fixed-size slots for the
-// all-gather
-__global__ void k_pad_pairs(uint2* __restrict__ buf, uint64_t n, uint64_t m) {
-    const uint2 p = buf[0];
+// all-gather. P = uint2 (dense (vertex, root) uint32 pairs) or P16 (sparse (id, root id) int64
+// pairs, 8-B aligned inside count-headed slots)
+struct P16 { unsigned long long a, b; };
+template <typename P>
+__global__ void k_pad_pairs(P* __restrict__ buf, uint64_t n, uint64_t m) {
+    const P p = buf[0];
     for (uint64_t i = n + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x)
         buf[i] = p;
 }
+void pad_pairs(bool sparse, uint32_t* buf, uint64_t n, uint64_t m, hipStream_t s) {
+    const dim3 grid((unsigned)std::min<uint64_t>((m - n + 255) / 256, 4096));
+    if (sparse) hipLaunchKernelGGL(k_pad_pairs<P16>, grid, dim3(256), 0, s, reinterpret_cast<P16*>(buf), n, m);
+    else hipLaunchKernelGGL(k_pad_pairs<uint2>, grid, dim3(256), 0, s, reinterpret_cast<uint2*>(buf), n, m);
+}
+// bytes / 32-bit words per exported pair
+inline uint64_t pbytes(const CcInfo& in) { return in.sparse ? 16 : 8; }
+inline uint64_t pwords(const CcInfo& in) { return in.sparse ? 4 : 2; }
 
 // ---- in-process group (tests): threads on one device ----
 struct LocalGroup {
@@ -91,6 +102,7 @@ struct gs_comm {
     hipEvent_t ev_ready = nullptr, ev_done = nullptr;
     // exchange buffers (device), sized at the first merge for the handle's capacity
     uint64_t cap_pairs = 0;
+    uint64_t pair_bytes = 0;                       // 8: dense (uint32 vertex, root); 16: sparse (int64 ids)
     uint32_t* sendbuf = nullptr;                   // cap_pairs pairs (2 x the handle's capacity)
     uint32_t* sendbuf2 = nullptr;                  // allgather: exports alternate between the two, so a
                                                    // pending window's tail survives the next export
@@ -228,22 +240,22 @@ int ensure(void** p, size_t* have, size_t need, hipStream_t s) {
 
 int prepare(gs_comm_t* c, gs_cc_t* h, CcInfo* info) {
     GS_TRY(cc_info(h, info));
-    if (info->sparse) return fail(GS_ERR_UNSUPPORTED, "gs_cc_merge_window: sparse-id summary (the exchange is dense-id)");
     if (!info->marks) return fail(GS_ERR_UNSUPPORTED, "gs_cc_merge_window: handle created without GS_CC_TRACK_MARKS");
     if (info->device != c->device) return fail(GS_ERR_INVALID, "gs_cc_merge_window: handle on device %d, communicator on %d",
                                                info->device, c->device);
     const uint64_t need = 2ull * info->cap;        // an export never exceeds 2 x capacity pairs
-    if (c->cap_pairs < need) {
+    if (c->cap_pairs < need || c->pair_bytes != pbytes(*info)) {
         if (c->sendbuf) (void)hipFree(c->sendbuf);
         if (c->sendbuf2) (void)hipFree(c->sendbuf2);
         c->sendbuf = c->sendbuf2 = nullptr;
-        if (hipMalloc(&c->sendbuf, (size_t)(need + 1) * 8) != hipSuccess ||                  // + a count word
-            hipMalloc(&c->sendbuf2, (size_t)(need + 1) * 8) != hipSuccess) {
+        if (hipMalloc(&c->sendbuf, (size_t)(need + 1) * pbytes(*info)) != hipSuccess ||      // + a count word
+            hipMalloc(&c->sendbuf2, (size_t)(need + 1) * pbytes(*info)) != hipSuccess) {
             (void)hipGetLastError();
             c->cap_pairs = 0;
             return fail(GS_ERR_NOMEM, "exchange buffers of %llu pairs", (unsigned long long)need);
         }
         c->cap_pairs = need;
+        c->pair_bytes = pbytes(*info);
     }
     return GS_OK;
 }
@@ -253,14 +265,16 @@ int prepare(gs_comm_t* c, gs_cc_t* h, CcInfo* info) {
 // joined) each slot is its own fold call, whose short head launch makes the big joins first
 // (cc_api.hip kMergeHead); otherwise runs of slots go in one call.
 constexpr uint64_t kBulkDeltaPairs = 1ull << 21;
-int fold_slots(gs_cc_t* h, const uint32_t* buf, uint64_t m, const std::vector<uint64_t>& cnt, const std::vector<char>& skip) {
+int fold_slots(gs_cc_t* h, const CcInfo& in, const uint32_t* buf, uint64_t m, const std::vector<uint64_t>& cnt,
+               const std::vector<char>& skip) {
     const int P = (int)cnt.size();
+    const uint64_t pw = pwords(in);
     uint64_t mx = 0;
     for (int q = 0; q < P; ++q) if (!skip[q]) mx = std::max(mx, cnt[q]);
     if (mx == 0) return GS_OK;
     if (mx > kBulkDeltaPairs) {
         for (int q = 0; q < P; ++q)
-            if (!skip[q] && cnt[q]) GS_TRY(gs_cc_fold_pairs32(h, buf + 2 * (uint64_t)q * m, cnt[q]));
+            if (!skip[q] && cnt[q]) GS_TRY(cc_fold_pairs_any(h, buf + pw * (uint64_t)q * m, cnt[q]));
         return GS_OK;
     }
     int q = 0;
@@ -269,7 +283,7 @@ int fold_slots(gs_cc_t* h, const uint32_t* buf, uint64_t m, const std::vector<ui
         int e = q;
         while (e + 1 < P && !skip[e + 1] && cnt[e + 1]) ++e;
         const uint64_t npairs = (uint64_t)(e - q) * m + cnt[e];     // the last slot: its real pairs only
-        GS_TRY(gs_cc_fold_pairs32(h, buf + 2 * (uint64_t)q * m, npairs));
+        GS_TRY(cc_fold_pairs_any(h, buf + pw * (uint64_t)q * m, npairs));
         q = e + 1;
     }
     return GS_OK;
@@ -291,20 +305,18 @@ int exchange_exact(gs_comm_t* c, gs_cc_t* h, const CcInfo& in, uint64_t* maxc) {
     *maxc = m;
     if (m) {
         const uint64_t n = cnt[c->rank];
-        if (n && n < m)
-            hipLaunchKernelGGL(k_pad_pairs, dim3((unsigned)std::min<uint64_t>((m - n + 255) / 256, 4096)), dim3(256), 0, s,
-                               reinterpret_cast<uint2*>(c->sendbuf), n, m);
+        if (n && n < m) pad_pairs(in.sparse, c->sendbuf, n, m, s);
         GS_HIP(hipGetLastError());
-        GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)P * m * 8, s));
-        GS_TRY(allgather(c, c->sendbuf, c->recvbuf, m * 8, s));
+        GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)P * m * pbytes(in), s));
+        GS_TRY(allgather(c, c->sendbuf, c->recvbuf, m * pbytes(in), s));
         std::vector<char> skip(P, 0);
         skip[c->rank] = 1;
         GS_TRY(gs_cc_set_marking(h, 0));           // the others' deltas are theirs to export
-        const int rc = fold_slots(h, c->recvbuf, m, cnt, skip);
+        const int rc = fold_slots(h, in, c->recvbuf, m, cnt, skip);
         GS_TRY(gs_cc_set_marking(h, in.marking ? 1 : 0));   // the caller's marking state back
         GS_TRY(rc);
-        c->bytes_sent += m * 8 * (P - 1);
-        c->bytes_recv += m * 8 * (P - 1);
+        c->bytes_sent += m * pbytes(in) * (P - 1);
+        c->bytes_recv += m * pbytes(in) * (P - 1);
     }
     return GS_OK;
 }
@@ -360,22 +372,20 @@ int settle_allgather(gs_comm_t* c, bool close) {
     cc_count_folded(h, folded);
     if (mt) {                                                   // tails past S: one more all-gather
         ++c->overflows;
-        uint32_t* t = send + 2 + 2 * S;                         // this rank's pairs [S, n)
+        uint32_t* t = send + 2 + pwords(in) * S;                // this rank's pairs [S, n)
         const uint64_t n = tail[c->rank];
-        if (n && n < mt)
-            hipLaunchKernelGGL(k_pad_pairs, dim3((unsigned)std::min<uint64_t>((mt - n + 255) / 256, 4096)), dim3(256), 0, s,
-                               reinterpret_cast<uint2*>(t), n, mt);
+        if (n && n < mt) pad_pairs(in.sparse, t, n, mt, s);
         GS_HIP(hipGetLastError());
-        GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)P * mt * 8, s));
-        GS_TRY(allgather(c, t, c->recvbuf, mt * 8, s));
+        GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)P * mt * pbytes(in), s));
+        GS_TRY(allgather(c, t, c->recvbuf, mt * pbytes(in), s));
         std::vector<char> skip(P, 0);
         skip[c->rank] = 1;
         GS_TRY(gs_cc_set_marking(h, 0));
-        const int rc = fold_slots(h, c->recvbuf, mt, tail, skip);
+        const int rc = fold_slots(h, in, c->recvbuf, mt, tail, skip);
         GS_TRY(gs_cc_set_marking(h, in.marking ? 1 : 0));
         GS_TRY(rc);
-        c->bytes_sent += mt * 8 * (P - 1);
-        c->bytes_recv += mt * 8 * (P - 1);
+        c->bytes_sent += mt * pbytes(in) * (P - 1);
+        c->bytes_recv += mt * pbytes(in) * (P - 1);
         if (close) GS_TRY(gs_cc_close_window(h));              // (from merge_window: its close follows)
     }
     c->spec_slot = next_slot(c, maxc);
@@ -416,7 +426,7 @@ int merge_allgather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
         GS_TRY(settle_allgather(c, false));
     }
     const uint64_t S = c->spec_slot;
-    const uint64_t slot_words = 2 + 2 * S;                       // [u64 count][S pairs]
+    const uint64_t slot_words = 2 + pwords(in) * S;              // [u64 count][S pairs]
     GS_TRY(ensure(reinterpret_cast<void**>(&c->slotbuf), &c->slot_bytes, (size_t)P * slot_words * 4, s));
     GS_TRY(allgather(c, send, c->slotbuf, slot_words * 4, s));
     // the count words (one per slot, strided) go to the host on a side stream, so the slots' fold
@@ -449,8 +459,8 @@ int merge_gather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
         GS_HIP(hipStreamSynchronize(s));
         const uint64_t n = c->hcnt[P];
         GS_TRY(send(c, c->dcnt + P, sizeof(unsigned long long), 0, s));
-        if (n) GS_TRY(send(c, c->sendbuf, n * 8, 0, s));
-        c->bytes_sent += n * 8;
+        if (n) GS_TRY(send(c, c->sendbuf, n * pbytes(in), 0, s));
+        c->bytes_sent += n * pbytes(in);
         return gs_cc_close_window(h);
     }
     if (!c->root_marking_off) {                    // rank 0 never exports
@@ -468,12 +478,12 @@ int merge_gather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
     uint64_t total = 0, mx = 0;
     for (int q = 1; q < P; ++q) { cnt[q] = c->hcnt[q]; total += cnt[q]; mx = std::max(mx, cnt[q]); }
     if (total) {
-        GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)total * 8, s));
+        GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)total * pbytes(in), s));
         {
             Group g(c);
             uint64_t off = 0;
             for (int q = 1; q < P; ++q) {
-                if (cnt[q]) GS_TRY(recv(c, c->recvbuf + 2 * off, cnt[q] * 8, q, s));
+                if (cnt[q]) GS_TRY(recv(c, c->recvbuf + pwords(in) * off, cnt[q] * pbytes(in), q, s));
                 off += cnt[q];
             }
             GS_TRY(g.end());
@@ -481,13 +491,13 @@ int merge_gather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
         if (mx > kBulkDeltaPairs) {                // big deltas one call each (head launch first)
             uint64_t off = 0;
             for (int q = 1; q < P; ++q) {
-                if (cnt[q]) GS_TRY(gs_cc_fold_pairs32(h, c->recvbuf + 2 * off, cnt[q]));
+                if (cnt[q]) GS_TRY(cc_fold_pairs_any(h, c->recvbuf + pwords(in) * off, cnt[q]));
                 off += cnt[q];
             }
         } else {
-            GS_TRY(gs_cc_fold_pairs32(h, c->recvbuf, total));
+            GS_TRY(cc_fold_pairs_any(h, c->recvbuf, total));
         }
-        c->bytes_recv += total * 8;
+        c->bytes_recv += total * pbytes(in);
     }
     return gs_cc_close_window(h);
 }
@@ -510,8 +520,8 @@ int merge_tree(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
             const uint64_t n = c->hcnt[P];
             const int peer = c->rank - step;
             GS_TRY(send(c, c->dcnt + P, sizeof(unsigned long long), peer, s));
-            if (n) GS_TRY(send(c, c->sendbuf, n * 8, peer, s));
-            c->bytes_sent += n * 8;
+            if (n) GS_TRY(send(c, c->sendbuf, n * pbytes(in), peer, s));
+            c->bytes_sent += n * pbytes(in);
             break;
         }
         if (c->rank % (2 * step) == 0 && c->rank + step < P) {
@@ -521,11 +531,11 @@ int merge_tree(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
             GS_HIP(hipStreamSynchronize(s));
             const uint64_t n = c->hcnt[0];
             if (n) {
-                GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)n * 8, s));
-                GS_TRY(recv(c, c->recvbuf, n * 8, peer, s));
-                GS_TRY(gs_cc_fold_pairs32(h, c->recvbuf, n));
+                GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)n * pbytes(in), s));
+                GS_TRY(recv(c, c->recvbuf, n * pbytes(in), peer, s));
+                GS_TRY(cc_fold_pairs_any(h, c->recvbuf, n));
             }
-            c->bytes_recv += n * 8;
+            c->bytes_recv += n * pbytes(in);
         }
     }
     return gs_cc_close_window(h);

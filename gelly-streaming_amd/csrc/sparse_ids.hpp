@@ -113,6 +113,58 @@ __global__ __launch_bounds__(256) void k_merge_sparse(const uint32_t* __restrict
     }
 }
 
+// Partial-summary export of a sparse-id summary (multi-GPU CombineCC, comm.hip): as k_export_log,
+// every pending hook-log entry (a slot hooked since the last export, or a self-loop first touch)
+// becomes the pair (id, id of its root slot) as two int64 words: the receiver hashes both ids into
+// its own slots and unions them (DisjointSet.merge over the pairs, DisjointSet.java:127-131). The
+// root's id is any member's of the component (slot roots are not id minima); a union only needs
+// one. ctr = [length, read cursor, finished workgroups]; at most cap pairs written, the rest stay.
+__global__ __launch_bounds__(256) void k_export_log_sparse(const uint32_t* __restrict__ log, unsigned long long* __restrict__ ctr,
+                                                           const uint32_t* __restrict__ parent, SparseArgs s,
+                                                           int64_t* __restrict__ pairs, uint64_t cap,
+                                                           unsigned long long* __restrict__ count) {
+    const unsigned long long len = ctr[0], rd = ctr[1];
+    const unsigned long long n = len - rd;
+    const unsigned long long take = n < cap ? n : cap;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *count = n;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < take;
+         i += (unsigned long long)gridDim.x * blockDim.x) {
+        const uint32_t v = log[rd + i];
+        pairs[2 * i] = slot_key(s, v);
+        pairs[2 * i + 1] = slot_key(s, find_root_ro(parent, v));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && len >= rd) {             // the last workgroup consumes what was written
+        const unsigned long long done = atomicAdd(&ctr[2], 1ull);
+        if (done == gridDim.x - 1) {
+            if (rd + take == len) { ctr[0] = 0; ctr[1] = 0; }
+            else ctr[1] = rd + take;
+            ctr[2] = 0;
+        }
+    }
+}
+
+// Folds received sparse partial summaries laid out in slots (comm.hip's speculative all-gather):
+// slot q = [uint64 count][cap pairs (id, id) as int64], slot_words 32-bit words apart; pairs
+// [lo, min(count, hi)) of every slot but `skip` are hashed to slots (inserted if new) and unioned.
+// blockIdx.y = slot. No marks (the others' deltas are theirs to export).
+__global__ __launch_bounds__(256) void k_fold_slots_sparse(const uint32_t* __restrict__ slots, uint64_t slot_words, int skip,
+                                                           uint64_t lo, uint64_t hi, FoldArgs f, SparseArgs s) {
+    const int q = blockIdx.y;
+    if (q == skip) return;                           // uniform
+    const uint32_t* sq = slots + (uint64_t)q * slot_words;
+    const unsigned long long cnt = *reinterpret_cast<const unsigned long long*>(sq);
+    const uint64_t n = cnt < hi ? cnt : hi;
+    const int64_t* pairs = reinterpret_cast<const int64_t*>(sq + 2);
+    FoldStats st;
+    for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t a = sparse_slot<true>(s, pairs[2 * i]), b = sparse_slot<true>(s, pairs[2 * i + 1]);
+        const bool ok[1] = {a != kInvalid && b != kInvalid};
+        const uint32_t u[1] = {ok[0] ? a : 0u}, v[1] = {ok[0] ? b : 0u};
+        union_group<false, false, 1>(f, u, v, ok, st);
+    }
+}
+
 // minkey[r] = key of every root r (parent compressed: parent[s] is s's root)
 __global__ __launch_bounds__(256) void k_minkey_init(const uint32_t* __restrict__ parent, uint32_t n, SparseArgs s,
                                                      int64_t* __restrict__ minkey) {

@@ -305,9 +305,9 @@ class DisjointSet:
         return int(p.value or 0)
 
     def export_marks(self, out, cap_pairs: Optional[int] = None) -> int:
-        """Write this window's partial-summary pairs (uint32 interleaved) into ``out``;
-        returns the number of pairs written."""
-        p, keep, total = _buf(out, 32, "out")
+        """Write this window's partial-summary pairs into ``out`` — uint32 (vertex, root) interleaved,
+        or int64 (id, root id) for a sparse-id summary; returns the number of pairs written."""
+        p, keep, total = _buf(out, 64 if self.sparse else 32, "out")
         cap = total // 2 if cap_pairs is None else int(cap_pairs)
         n = U64()
         call("gs_cc_export_marks", self.handle, p, cap, ctypes.byref(n))

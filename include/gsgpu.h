@@ -65,8 +65,9 @@ enum {
                                     negatives included), hashed to slots on the device;
                                     vertex_capacity = most distinct ids (<= 2^30). Canonical
                                     labels are still the minimum id of each component.
-                                    gs_cc_emit_dense, gs_cc_export_marks and
-                                    gs_cc_labels_device are not available in this mode.      */
+                                    gs_cc_emit_dense, gs_cc_emit_delta and
+                                    gs_cc_labels_device are not available in this mode; with
+                                    GS_CC_TRACK_MARKS the exchange carries int64 pairs.      */
 };
 
 typedef struct gs_cc gs_cc_t;
@@ -150,7 +151,8 @@ int gs_cc_find_flags(gs_cc_t* h, const void* ids, void* roots, uint8_t* found, u
 int gs_cc_labels_device(gs_cc_t* h, const void** dev_ptr);
 
 /* ---- partial-summary exchange (windowAll / tree merge) ----
- * Requires GS_CC_TRACK_MARKS (dense ids). Writes the (vertex, root) pairs (uint32, interleaved) of
+ * Requires GS_CC_TRACK_MARKS. Writes the (vertex, root) pairs (uint32, interleaved; with
+ * GS_CC_SPARSE_IDS (id, id of the root's component) as int64, interleaved, 16 B per pair) of
  * every vertex whose root status changed in this handle since the last export (roots it hooked,
  * singletons made by self-loops: the handle's hook log, at most 2 x vertex_capacity entries), and
  * consumes them; pairs past cap stay for the next export. Folding these pairs into another

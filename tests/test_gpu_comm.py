@@ -6,7 +6,9 @@ ConnectedComponentsTree, SummaryTreeReduce.java:95-123).
 * world 1 through RCCL itself (ncclCommInitRank with one rank: the exchange code path with real
   RCCL collectives; a one-GPU box cannot host two RCCL ranks);
 * world 2..8 through the in-process group (gs_comm_create_local): one thread per rank, every
-  rank a handle on this GPU — the same exchange code, collectives by device copies.
+  rank a handle on this GPU — the same exchange code, collectives by device copies;
+* sparse-id summaries (GS_CC_SPARSE_IDS: any Java long, the reference's K = Long,
+  ConnectedComponentsExample.java:61) through the exchange: (id, root id) int64 pairs.
 """
 import threading
 
@@ -397,3 +399,60 @@ def test_fold_windows_batch(oracle, world, mode):
     for r in ([0] if mode == "tree" else range(world)):     # tree: rank 0 is the Merger
         assert finals[r][0] == int(want["checksums"][-1])
         np.testing.assert_array_equal(finals[r][1], want["final"])
+
+
+def _sparse_ids(oracle, n, scale, seed):
+    """An RMAT stream whose ids are spread over the whole int64 range (negative ids, ids >= 2^32,
+    INT64_MIN and INT64_MAX among them) by a fixed injective map, as the reference's Long keys allow."""
+    s, d = oracle.gen_rmat(0, n, scale, seed)
+    mul = np.uint64(0x9E3779B97F4A7C15)                   # odd: a bijection of uint64
+    with np.errstate(over="ignore"):
+        ms = (s.astype(np.uint64) * mul).view(np.int64)
+        md = (d.astype(np.uint64) * mul).view(np.int64)
+    ms[:3] = [np.iinfo(np.int64).min, np.iinfo(np.int64).max, -1]
+    md[:3] = [-1, 5, np.iinfo(np.int64).min]
+    return ms, md
+
+
+@pytest.mark.parametrize("mode", ["allgather", "gather", "tree"])
+@pytest.mark.parametrize("world", [1, 4])
+def test_sparse_ids_through_the_exchange(oracle, world, mode):
+    """Sparse (any int64) ids across ranks: every rank folds its slice of each window into a
+    GS_CC_SPARSE_IDS handle; gs_cc_merge_window carries (id, root id) int64 pairs; the Merger's
+    emission (every replica in allgather mode) equals the oracle's with `world` partitions, window
+    by window (world 1: RCCL with one rank)."""
+    import torch
+    s, d = _sparse_ids(oracle, 120000, 14, 21 + world)
+    W = 20000
+    want = oracle.run(s, d, W, partitions=world, emit=EMIT_CHECKSUM)
+    ts, td = torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()
+    torch.cuda.synchronize()
+    comms = Comm.local_group(world, 0) if world > 1 else [Comm.create(unique_id(), 0, 1, 0)]
+    sums = [[] for _ in range(world)]
+    errors = []
+
+    def rank(r):
+        try:
+            ds = DisjointSet(1 << 15, id_bits=64, track_marks=True, sparse=True)
+            for lo in range(0, s.size, W):
+                ln = min(W, s.size - lo)
+                a, b = lo + (ln * r) // world, lo + (ln * (r + 1)) // world
+                ds.fold(ts[a:b], td[a:b])
+                ds.merge_window(comms[r], mode)
+                sums[r].append(ds.checksum())
+            ds.close()
+        except Exception as e:
+            errors.append((r, repr(e)))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th), "a rank hung"
+    for c in comms:
+        c.close()
+    assert not errors, errors
+    exp = [(int(c), int(v), int(k)) for c, (v, k) in zip(want["checksums"], want["counts"])]
+    for r in (range(world) if mode == "allgather" else [0]):
+        assert [tuple(x) for x in sums[r]] == exp, "rank %d" % r

@@ -1,0 +1,147 @@
+// barrier_lab.hip — what a window boundary costs on gfx950: a kernel boundary (back-to-back
+// dependent launches on one stream) against a grid barrier inside one co-resident (cooperative)
+// launch. Measurement tool for DESIGN.md; not part of libgsgpu.
+//   hipcc -O3 --offload-arch=gfx950 -o tools/barrier_lab tools/barrier_lab.hip
+//   ./tools/barrier_lab            (prints one JSON line)
+// Every spin loop is bounded in time (kSpinTicks of the 100 MHz s_memrealtime clock, 20 ms): a
+// barrier that never completes sets an error word and falls through, so no wave can hang the GPU.
+#include <hip/hip_runtime.h>
+#include <hip/hip_cooperative_groups.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            fprintf(stderr, "%s failed: %s (line %d)\n", #x, hipGetErrorString(e_), __LINE__); \
+            exit(1);                                                                           \
+        }                                                                                      \
+    } while (0)
+
+constexpr unsigned long long kSpinTicks = 2000000ull;      // 20 ms at 100 MHz
+
+// one load + one store per thread: a launch that touches memory like a tiny fold window
+__global__ void k_touch(unsigned* __restrict__ a, unsigned n, unsigned it) {
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = a[i] + it;
+}
+
+struct Bar {
+    unsigned* count;   // arrivals of the current generation
+    unsigned* gen;     // generation word (own 128-B line)
+    unsigned* err;     // spin cap hit
+};
+
+// flat grid barrier: thread 0 of every workgroup releases its workgroup's stores (agent scope),
+// arrives on one counter; the last arrival resets it and bumps the generation; the others poll it.
+// g = the generation this workgroup waits to leave (read once at kernel start: no workgroup can
+// bump it before every workgroup has arrived, so all start from the same value).
+__device__ __forceinline__ void grid_barrier(const Bar& b, unsigned nblocks, unsigned& g) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const unsigned a = __hip_atomic_fetch_add(b.count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (a == nblocks - 1) {
+            __hip_atomic_store(b.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(b.gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(b.gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) {
+                if (__hip_atomic_load(b.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;   // a peer timed out
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) { atomicOr(b.err, 1u); break; }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        g += 1;
+    }
+    __syncthreads();
+}
+
+__global__ void k_barriers(Bar b, unsigned iters, unsigned* __restrict__ a, unsigned n, int store) {
+    unsigned g = 0;
+    if (threadIdx.x == 0) g = __hip_atomic_load(b.gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    for (unsigned it = 0; it < iters; ++it) {
+        if (store && i < n) a[i] = a[i] + it;
+        grid_barrier(b, gridDim.x, g);
+    }
+}
+
+__global__ void k_cg_barriers(unsigned iters, unsigned* __restrict__ a, unsigned n, int store) {
+    cooperative_groups::grid_group grid = cooperative_groups::this_grid();
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    for (unsigned it = 0; it < iters; ++it) {
+        if (store && i < n) a[i] = a[i] + it;
+        grid.sync();
+    }
+}
+
+int main(int argc, char** argv) {
+    const unsigned iters = argc > 1 ? (unsigned)atoi(argv[1]) : 2000;
+    setvbuf(stdout, nullptr, _IONBF, 0);
+    int dev = 0, cus = 0;
+    CK(hipSetDevice(dev));
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    unsigned* a = nullptr;
+    const unsigned n = 1u << 20;
+    CK(hipMalloc(&a, n * 4));
+    CK(hipMemset(a, 0, n * 4));
+    unsigned* ctl = nullptr;
+    CK(hipMalloc(&ctl, 1024));
+    CK(hipMemset(ctl, 0, 1024));
+    Bar b{ctl, ctl + 32, ctl + 64};
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float ms = 0.f;
+    printf("{\"cus\": %d, \"iters\": %u", cus, iters);
+    const unsigned blocks_list[] = {(unsigned)cus, 2u * cus, 4u * cus};
+    for (unsigned threads : {256u, 1024u}) {
+        for (unsigned blocks : blocks_list) {
+            if (threads == 1024 && blocks > (unsigned)cus) continue;
+            // kernel boundaries: iters dependent launches of a one-load-one-store kernel
+            hipLaunchKernelGGL(k_touch, dim3(blocks), dim3(threads), 0, s, a, n, 0u);
+            CK(hipStreamSynchronize(s));
+            CK(hipEventRecord(e0, s));
+            for (unsigned it = 0; it < iters; ++it) hipLaunchKernelGGL(k_touch, dim3(blocks), dim3(threads), 0, s, a, n, it);
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            printf(", \"launch_us_%ux%u\": %.3f", blocks, threads, ms * 1e3 / iters);
+            // occupancy: the cooperative launch needs every workgroup resident
+            int per_cu = 0;
+            CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_barriers, threads, 0));
+            if ((unsigned)per_cu * cus < blocks) { printf(", \"bar_%ux%u\": null", blocks, threads); continue; }
+            for (int store = 0; store < 2; ++store) {
+                void* args[] = {&b, (void*)&iters, &a, (void*)&n, &store};
+                CK(hipLaunchCooperativeKernel((const void*)k_barriers, dim3(blocks), dim3(threads), args, 0, s));
+                CK(hipStreamSynchronize(s));
+                CK(hipEventRecord(e0, s));
+                CK(hipLaunchCooperativeKernel((const void*)k_barriers, dim3(blocks), dim3(threads), args, 0, s));
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                printf(", \"bar%s_us_%ux%u\": %.3f", store ? "_store" : "", blocks, threads, ms * 1e3 / iters);
+                unsigned e = 0;
+                CK(hipMemcpy(&e, ctl + 64, 4, hipMemcpyDeviceToHost));
+                if (e) { printf(", \"spin_cap_hit\": 1}\n"); return 2; }
+                void* cargs[] = {(void*)&iters, &a, (void*)&n, &store};
+                CK(hipEventRecord(e0, s));
+                CK(hipLaunchCooperativeKernel((const void*)k_cg_barriers, dim3(blocks), dim3(threads), cargs, 0, s));
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                printf(", \"cg%s_us_%ux%u\": %.3f", store ? "_store" : "", blocks, threads, ms * 1e3 / iters);
+            }
+        }
+    }
+    unsigned err = 0;
+    CK(hipMemcpy(&err, ctl + 64, 4, hipMemcpyDeviceToHost));
+    printf(", \"spin_cap_hit\": %u}\n", err);
+    return err ? 2 : 0;
+}

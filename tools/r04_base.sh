@@ -14,6 +14,8 @@ run() {   # name limit cmd...
   echo "$name rc=$rc"; tail -1 "$OUT/$name.json" | cut -c1-400
   [ $rc -eq 0 ] || { tail -5 "$OUT/$name.err"; exit 3; }
 }
+run c5fix 600 python -u tests/headline_check.py --fixture c5 --fold-windows --chunk 256
+run c3fw 600 python -u tests/headline_check.py --fold-windows --no-torch --steps 0
 run bench_c3 300 python -u bench.py --steps 5 --no-cpu-baseline
 run bench_c5 300 python -u bench.py --workload c5 --steps 3 --no-cpu-baseline
 run bench_c4 300 python -u bench.py --workload c4 --steps 3 --no-cpu-baseline
