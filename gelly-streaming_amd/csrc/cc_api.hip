@@ -771,10 +771,17 @@ static int export_launch(gs_cc_t* h, void* out, uint64_t cap, unsigned long long
 // min(count, cap) read on the device; marking is off for these folds (the others' deltas are theirs
 // to export). Big slots (young windows: components not yet joined) fold a short head of every
 // slot first (see kMergeHead), then the rest.
-int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int nslots, int skip, uint64_t cap) {
+int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int nslots, int skip, uint64_t cap,
+                  const uint64_t* caps) {
     GS_TRY(check(h));
     DeviceGuard g(h->device);
     if (nslots <= 1 || cap == 0) return GS_OK;
+    SlotCaps sc;
+    if (caps) {
+        if (nslots > kMaxSlotCaps) return fail(GS_ERR_INVALID, "cc_fold_slots: %d slots with capacities (at most %d)", nslots, kMaxSlotCaps);
+        sc.n = (uint32_t)nslots;
+        for (int q = 0; q < nslots; ++q) sc.v[q] = caps[q];
+    }
     h->compressed = false;
     h->minkey_valid = false;
     FoldArgs f{0, h->parent, nullptr, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, nullptr};
@@ -782,17 +789,17 @@ int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int ns
     if (h->sparse) {                                 // (id, id) int64 pairs, hashed to slots
         const dim3 grid(grid_for(cap, 256, (unsigned)std::max(64, 4096 / nslots)), (unsigned)nslots);
         klaunch(k_fold_slots_sparse, grid, dim3(256), h->stream, t.start(), t.stop(), slots, slot_words, skip, (uint64_t)0,
-                cap, f, sparse_args(h));
+                cap, f, sparse_args(h), sc);
         GS_HIP(hipGetLastError());
         return GS_OK;
     }
     const uint64_t head = cap > kMergeBulk ? std::min<uint64_t>(cap, kMergeHead) : 0;
     if (head) {
         const dim3 grid(grid_for(head, 256, 64), (unsigned)nslots);
-        klaunch(k_fold_slots, grid, dim3(256), h->stream, t.start(), nullptr, slots, slot_words, skip, (uint64_t)0, head, f);
+        klaunch(k_fold_slots, grid, dim3(256), h->stream, t.start(), nullptr, slots, slot_words, skip, (uint64_t)0, head, f, sc);
     }
     const dim3 grid(grid_for(cap - head, 256, (unsigned)std::max(64, 4096 / nslots)), (unsigned)nslots);
-    klaunch(k_fold_slots, grid, dim3(256), h->stream, head ? nullptr : t.start(), t.stop(), slots, slot_words, skip, head, cap, f);
+    klaunch(k_fold_slots, grid, dim3(256), h->stream, head ? nullptr : t.start(), t.stop(), slots, slot_words, skip, head, cap, f, sc);
     GS_HIP(hipGetLastError());
     return GS_OK;
 }

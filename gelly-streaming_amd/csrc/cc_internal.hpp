@@ -15,7 +15,9 @@ struct CcInfo {
 };
 int cc_info(gs_cc_t* h, CcInfo* out);
 int cc_export_async(gs_cc_t* h, void* pairs, uint64_t cap, unsigned long long* dcount, uint64_t expect = ~0ull);
-int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int nslots, int skip, uint64_t cap);
+// caps (host array, nslots entries, or null = every slot holds cap pairs): slot q's own capacity
+int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int nslots, int skip, uint64_t cap,
+                  const uint64_t* caps = nullptr);
 void cc_count_folded(gs_cc_t* h, uint64_t n);
 // folds n exported partial-summary pairs (device buffer) as CombineCC does: uint32 (vertex, root)
 // pairs for dense handles, int64 (id, root id) pairs for sparse-id handles; timed as a merge

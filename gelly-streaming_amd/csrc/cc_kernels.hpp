@@ -1114,15 +1114,23 @@ __global__ __launch_bounds__(256) void k_merge_dense(const uint32_t* __restrict_
     }
 }
 
+// Per-slot pair capacities of a slot fold (the gather exchange: every sender's slot has its own
+// size); n == 0: every slot holds `hi` pairs
+struct SlotCaps {
+    uint32_t n = 0;
+    uint64_t v[kMaxSlotCaps] = {};
+};
+
 // Folds received partial summaries laid out in slots (multi-GPU exchange, comm.hip): slot q =
-// [uint64 count][cap pairs (v, root)], slot_words 32-bit words apart; pairs [lo, min(count, hi))
-// of every slot but `skip` are unioned (DisjointSet.merge over the pairs). The counts are read on
-// the device, so the fold is enqueued before the host has seen them. Ids are range-checked (a
-// peer's buffer). blockIdx.y = slot.
+// [uint64 count][cap pairs (v, root)], slot_words 32-bit words apart; pairs [lo, min(count, hi,
+// caps[q]))) of every slot but `skip` are unioned (DisjointSet.merge over the pairs). The counts are
+// read on the device, so the fold is enqueued before the host has seen them. Ids are
+// range-checked (a peer's buffer). blockIdx.y = slot.
 __global__ __launch_bounds__(256) void k_fold_slots(const uint32_t* __restrict__ slots, uint64_t slot_words, int skip,
-                                                    uint64_t lo, uint64_t hi, FoldArgs f) {
+                                                    uint64_t lo, uint64_t hi, FoldArgs f, SlotCaps caps) {
     const int q = blockIdx.y;
     if (q == skip) return;                           // uniform
+    if (caps.n && caps.v[q] < hi) hi = caps.v[q];
     const uint32_t* s = slots + (uint64_t)q * slot_words;
     const unsigned long long cnt = *reinterpret_cast<const unsigned long long*>(s);
     const uint64_t n = cnt < hi ? cnt : hi;

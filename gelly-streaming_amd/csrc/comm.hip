@@ -125,6 +125,7 @@ struct gs_comm {
     uint64_t pend_slot = 0;                        // its slot size S
     uint32_t* pend_buf = nullptr;                  // its export (the tail pairs [S, n) are sent from it)
     uint64_t last_delta = 0;                       // the largest delta of the last verified window
+    std::vector<uint64_t> gslot;                   // gather: every sender's speculative slot (empty: exact round next)
     uint64_t bytes_sent = 0, bytes_recv = 0, exchanges = 0, overflows = 0;
 };
 
@@ -396,9 +397,10 @@ int settle_allgather(gs_comm_t* c, bool close) {
 int abort_exchange(gs_comm_t* c, int rc);
 
 // cc_settle's callback: a failed verification fails the group (peers may be in the tail round)
+int settle_gather(gs_comm_t* c, bool close);
 int settle_cb(void* ctx) {
     gs_comm_t* c = static_cast<gs_comm_t*>(ctx);
-    const int rc = settle_allgather(c, true);
+    const int rc = c->mode == GS_MERGE_GATHER ? settle_gather(c, true) : settle_allgather(c, true);
     return rc == GS_OK ? rc : abort_exchange(c, rc);
 }
 
@@ -450,9 +452,12 @@ int merge_allgather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
 
 // windowAll: every other rank sends its delta straight to rank 0 (the Merger), which folds them
 // all and emits; the other ranks only close their own summaries (their giant filters).
-int merge_gather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
+// The exact round (the first window of a stream): counts sent first and read by the host, then
+// exactly the pairs. It sizes every sender's speculative slot (gslot).
+int merge_gather_exact(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
     const int P = c->world;
     hipStream_t s = in.stream;
+    c->gslot.assign(P, 0);
     if (c->rank != 0) {
         GS_TRY(cc_export_async(h, c->sendbuf, c->cap_pairs, c->dcnt + P));
         GS_HIP(hipMemcpyAsync(c->hcnt + P, c->dcnt + P, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
@@ -461,6 +466,8 @@ int merge_gather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
         GS_TRY(send(c, c->dcnt + P, sizeof(unsigned long long), 0, s));
         if (n) GS_TRY(send(c, c->sendbuf, n * pbytes(in), 0, s));
         c->bytes_sent += n * pbytes(in);
+        c->gslot[c->rank] = next_slot(c, n);
+        c->last_delta = n;
         return gs_cc_close_window(h);
     }
     if (!c->root_marking_off) {                    // rank 0 never exports
@@ -476,7 +483,12 @@ int merge_gather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
     GS_HIP(hipStreamSynchronize(s));
     std::vector<uint64_t> cnt(P, 0);
     uint64_t total = 0, mx = 0;
-    for (int q = 1; q < P; ++q) { cnt[q] = c->hcnt[q]; total += cnt[q]; mx = std::max(mx, cnt[q]); }
+    for (int q = 1; q < P; ++q) {
+        cnt[q] = c->hcnt[q];
+        total += cnt[q];
+        mx = std::max(mx, cnt[q]);
+        c->gslot[q] = next_slot(c, cnt[q]);
+    }
     if (total) {
         GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)total * pbytes(in), s));
         {
@@ -499,7 +511,117 @@ int merge_gather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
         }
         c->bytes_recv += total * pbytes(in);
     }
+    c->last_delta = mx;
     return gs_cc_close_window(h);
+}
+
+// The speculative gather's verification (as settle_allgather): a sender whose delta outgrew its
+// slot sends the tail [S, n) from the same export; rank 0 knows which senders overflowed from the
+// count words of their slots (on the host by now), receives those tails, folds them and, when
+// called from cc_settle (an emission read), closes again. Each side then sizes that sender's next
+// slot from the same count, so both agree without another message.
+int settle_gather(gs_comm_t* c, bool close) {
+    if (!c->pending) return GS_OK;
+    c->pending = false;
+    gs_cc_t* h = c->bound;
+    CcInfo in;
+    GS_TRY(cc_info(h, &in));
+    DeviceGuard g(in.device);
+    const int P = c->world;
+    hipStream_t s = in.stream;
+    GS_HIP(hipEventSynchronize(c->ev_counts));      // normally complete long ago
+    if (c->rank != 0) {
+        const uint64_t n = c->hcnt[P], S = c->pend_slot;
+        if (n > c->cap_pairs - 1) return fail(GS_ERR_CAPACITY, "delta of %llu pairs past the export buffer", (unsigned long long)n);
+        if (n > S) {
+            ++c->overflows;
+            GS_TRY(send(c, c->pend_buf + 2 + pwords(in) * S, (n - S) * pbytes(in), 0, s));
+            c->bytes_sent += (n - S) * pbytes(in);
+        }
+        c->gslot[c->rank] = next_slot(c, n);
+        c->last_delta = n;
+        return GS_OK;
+    }
+    std::vector<uint64_t> tail(P, 0);
+    uint64_t total = 0, mx = 0, folded = 0;
+    for (int q = 1; q < P; ++q) {
+        const uint64_t n = c->hcnt[q];
+        if (n > c->cap_pairs - 1) return fail(GS_ERR_CAPACITY, "rank %d delta of %llu pairs past the export buffer", q,
+                                              (unsigned long long)n);
+        tail[q] = n > c->gslot[q] ? n - c->gslot[q] : 0;
+        folded += n - tail[q];
+        total += tail[q];
+        mx = std::max(mx, n);
+        c->gslot[q] = next_slot(c, n);
+    }
+    cc_count_folded(h, folded);
+    c->last_delta = mx;
+    if (total) {
+        ++c->overflows;
+        GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)total * pbytes(in), s));
+        {
+            Group gr(c);
+            uint64_t off = 0;
+            for (int q = 1; q < P; ++q) {
+                if (tail[q]) GS_TRY(recv(c, c->recvbuf + pwords(in) * off, tail[q] * pbytes(in), q, s));
+                off += tail[q];
+            }
+            GS_TRY(gr.end());
+        }
+        GS_TRY(cc_fold_pairs_any(h, c->recvbuf, total));
+        c->bytes_recv += total * pbytes(in);
+        if (close) GS_TRY(gs_cc_close_window(h));
+    }
+    return GS_OK;
+}
+
+// Speculative gather (from the second window of a stream): each sender exports its whole delta
+// behind a count word and sends [count | S_q pairs] in ONE message, S_q sized from its own last
+// delta; rank 0 receives every slot, folds them with the counts read on the device and closes —
+// no host wait on either side (verified lazily by settle_gather, as the all-gather is).
+int merge_gather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
+    const int P = c->world;
+    hipStream_t s = in.stream;
+    if (c->gslot.empty() || P > kMaxSlotCaps) return merge_gather_exact(c, h, in);
+    if (c->rank != 0) {
+        uint32_t* send_buf = (c->pend_buf == c->sendbuf) ? c->sendbuf2 : c->sendbuf;
+        const uint64_t S = c->gslot[c->rank];
+        GS_TRY(cc_export_async(h, send_buf + 2, c->cap_pairs - 1, reinterpret_cast<unsigned long long*>(send_buf),
+                               2 * c->last_delta));
+        GS_TRY(send(c, send_buf, (2 + pwords(in) * S) * 4, 0, s));
+        GS_HIP(hipEventRecord(c->ev_slots, s));                 // the count word to the host, aside
+        GS_HIP(hipStreamWaitEvent(c->side, c->ev_slots, 0));
+        GS_HIP(hipMemcpyAsync(c->hcnt + P, send_buf, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->side));
+        GS_HIP(hipEventRecord(c->ev_counts, c->side));
+        c->bytes_sent += (2 + pwords(in) * S) * 4;
+        GS_TRY(gs_cc_close_window(h));
+        c->pending = true;
+        c->pend_slot = S;
+        c->pend_buf = send_buf;
+        cc_set_settle(h, settle_cb, c);
+        return GS_OK;
+    }
+    uint64_t smax = 0;
+    for (int q = 1; q < P; ++q) smax = std::max(smax, c->gslot[q]);
+    const uint64_t slot_words = 2 + pwords(in) * smax;
+    GS_TRY(ensure(reinterpret_cast<void**>(&c->slotbuf), &c->slot_bytes, (size_t)P * slot_words * 4, s));
+    {
+        Group g(c);
+        for (int q = 1; q < P; ++q)
+            GS_TRY(recv(c, c->slotbuf + (uint64_t)q * slot_words, (2 + pwords(in) * c->gslot[q]) * 4, q, s));
+        GS_TRY(g.end());
+    }
+    GS_HIP(hipEventRecord(c->ev_slots, s));
+    GS_HIP(hipStreamWaitEvent(c->side, c->ev_slots, 0));
+    GS_HIP(hipMemcpy2DAsync(c->hcnt, sizeof(unsigned long long), c->slotbuf, slot_words * 4, sizeof(unsigned long long), P,
+                            hipMemcpyDeviceToHost, c->side));
+    GS_HIP(hipEventRecord(c->ev_counts, c->side));
+    GS_TRY(cc_fold_slots(h, c->slotbuf, slot_words, P, 0, smax, c->gslot.data()));
+    GS_TRY(gs_cc_close_window(h));                              // optimistic: no delta outgrew its slot
+    for (int q = 1; q < P; ++q) c->bytes_recv += (2 + pwords(in) * c->gslot[q]) * 4;
+    c->pending = true;
+    cc_set_settle(h, settle_cb, c);
+    return GS_OK;
 }
 
 // ConnectedComponentsTree's pairwise rounds (SummaryTreeReduce.enhance): in round r (step 2^r)
@@ -680,6 +802,7 @@ int merge_window(gs_cc_t* h, gs_comm_t* c, int mode) {
     if (in.reset_gen != c->reset_gen) {              // the handle was reset: a new stream
         c->reset_gen = in.reset_gen;
         c->spec_slot = 0;                            // its first window runs the exact round again
+        c->gslot.clear();
     }
     DeviceGuard g(in.device);
     switch (mode) {

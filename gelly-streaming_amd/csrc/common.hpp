@@ -13,6 +13,7 @@
 namespace gsgpu {
 
 constexpr uint32_t kInvalid = 0xFFFFFFFFu;   // parent[v] of a vertex not in the summary
+constexpr int kMaxSlotCaps = 16;              // slots of a fold with per-slot capacities (SlotCaps)
 
 std::string& last_error();
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));

@@ -149,9 +149,10 @@ __global__ __launch_bounds__(256) void k_export_log_sparse(const uint32_t* __res
 // [lo, min(count, hi)) of every slot but `skip` are hashed to slots (inserted if new) and unioned.
 // blockIdx.y = slot. No marks (the others' deltas are theirs to export).
 __global__ __launch_bounds__(256) void k_fold_slots_sparse(const uint32_t* __restrict__ slots, uint64_t slot_words, int skip,
-                                                           uint64_t lo, uint64_t hi, FoldArgs f, SparseArgs s) {
+                                                           uint64_t lo, uint64_t hi, FoldArgs f, SparseArgs s, SlotCaps caps) {
     const int q = blockIdx.y;
     if (q == skip) return;                           // uniform
+    if (caps.n && caps.v[q] < hi) hi = caps.v[q];
     const uint32_t* sq = slots + (uint64_t)q * slot_words;
     const unsigned long long cnt = *reinterpret_cast<const unsigned long long*>(sq);
     const uint64_t n = cnt < hi ? cnt : hi;

@@ -121,26 +121,33 @@ def test_local_group_young_windows_big_deltas(oracle):
         np.testing.assert_array_equal(finals[r], want["final"])
 
 
+@pytest.mark.parametrize("mode", ["allgather", "gather"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_local_group_speculative_slot_overflow(oracle, world):
-    """allgather's speculative slot is sized from the last window's deltas: a tiny first window
-    (one self-loop) then an Erdos-Renyi window whose deltas outgrow the 4K-pair slot — the exact
-    round must carry the tails (overflow counted on every rank), and every emission stays exact."""
+def test_local_group_speculative_slot_overflow(oracle, world, mode):
+    """The speculative slots (allgather: one per rank, all-gathered; gather: each sender's own,
+    sent to rank 0) are sized from the last window's deltas: a tiny first window (one self-loop)
+    then an Erdos-Renyi window whose deltas outgrow the 4K-pair slot — the tail round must carry the
+    tails (allgather: overflow counted alike on every rank; gather: on rank 0), and every emission
+    stays exact."""
     cap = 1 << 16
     W = 1 << 17
     s1 = np.zeros(W, dtype=np.int64)                 # window 1: the self-loop (0, 0), W times
     s2, d2 = oracle.gen_er(0, 3 * W, cap, 4)        # windows 2-4: 3 x 2^17 uniform edges
     s = np.concatenate([s1, s2]); d = np.concatenate([s1, d2])
     want = oracle.run(s, d, W, partitions=world, emit=EMIT_CHECKSUM, label_cap=cap, want_final=True)
-    sums, finals, info = _run_local(world, "allgather", s, d, cap, W)
-    for r in range(world):
+    sums, finals, info = _run_local(world, mode, s, d, cap, W)
+    for r in (range(world) if mode == "allgather" else [0]):
         assert sums[r] == [int(x) for x in want["checksums"]], "rank %d" % r
         np.testing.assert_array_equal(finals[r], want["final"])
-    assert all(i[5] >= 1 for i in info) and len({i[5] for i in info}) == 1, info
+    if mode == "allgather":
+        assert all(i[5] >= 1 for i in info) and len({i[5] for i in info}) == 1, info
+    else:
+        assert info[0][5] >= 1 and all(i[5] >= 1 for i in info[1:]), info
 
 
+@pytest.mark.parametrize("mode", ["allgather", "gather"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_lazy_verification_overflow_in_a_batch(oracle, world):
+def test_lazy_verification_overflow_in_a_batch(oracle, world, mode):
     """The speculative all-gather is verified lazily (comm.hip settle_allgather): with
     gs_cc_fold_windows nothing consumes an emission between windows, so an outgrown slot's tail
     round runs only after the NEXT window's local fold. The final emission must still be exact and
@@ -165,7 +172,7 @@ def test_lazy_verification_overflow_in_a_batch(oracle, world):
             ts = torch.from_numpy(per[r][0].astype(np.int32)).cuda()
             td = torch.from_numpy(per[r][1].astype(np.int32)).cuda()
             ds = DisjointSet(cap, id_bits=32, track_marks=True)
-            assert ds.fold_windows(ts, td, W // world, comm=comms[r], mode="allgather") == s.size // W
+            assert ds.fold_windows(ts, td, W // world, comm=comms[r], mode=mode) == s.size // W
             finals[r] = (ds.checksum()[0], ds.dense().astype(np.int64))
             ov[r] = comms[r].info()[5]
             ds.close()
@@ -181,10 +188,10 @@ def test_lazy_verification_overflow_in_a_batch(oracle, world):
     for c in comms:
         c.close()
     assert not errors, errors
-    for r in range(world):
+    for r in (range(world) if mode == "allgather" else [0]):
         assert finals[r][0] == int(want["checksums"][-1]), "rank %d" % r
         np.testing.assert_array_equal(finals[r][1], want["final"])
-    assert all(o >= 1 for o in ov) and len(set(ov)) == 1, ov
+    assert all(o >= 1 for o in ov) and (mode == "gather" or len(set(ov)) == 1), ov
 
 
 def test_merge_window_errors():
@@ -338,7 +345,7 @@ def test_c5_eight_ranks_small_windows_latency(oracle):
           % (steady[len(steady) // 2], steady[min(len(steady) - 1, int(len(steady) * 0.99))]))
 
 
-@pytest.mark.parametrize("world,mode", [(1, None), (1, "allgather"), (3, "allgather"), (4, "tree")])
+@pytest.mark.parametrize("world,mode", [(1, None), (1, "allgather"), (3, "allgather"), (3, "gather"), (4, "tree")])
 def test_fold_windows_batch(oracle, world, mode):
     """gs_cc_fold_windows (the per-window fold + close / merge loop inside the library) ends in the
     same emission as the oracle's last window; every window is folded, and merged over the comm
@@ -396,7 +403,7 @@ def test_fold_windows_batch(oracle, world, mode):
     assert not errors, errors
     assert wins == [nwin] * world
     assert all(i[4] == nwin for i in info), info            # one exchange per window
-    for r in ([0] if mode == "tree" else range(world)):     # tree: rank 0 is the Merger
+    for r in ([0] if mode in ("tree", "gather") else range(world)):   # tree / gather: rank 0 is the Merger
         assert finals[r][0] == int(want["checksums"][-1])
         np.testing.assert_array_equal(finals[r][1], want["final"])
 
