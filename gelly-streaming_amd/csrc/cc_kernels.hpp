@@ -667,6 +667,11 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
                                                        FoldArgs f) {
     const uint64_t n = f.n;
     const bool filt = *f.giant != kInvalid;          // wave-uniform
+    // no giant yet: the close after this launch is a full pass (k_compress: the slot this launch
+    // reads has built == giant == kInvalid, so it cannot be incremental), which rebuilds the seen
+    // bitmap from parent[] — first touches skip their seen-bit atomic (Erdos-Renyi windows before the
+    // giant forms: ~1 M memory-side atomics per 2^20-edge window)
+    if (!filt) f.sbits = nullptr;
     FoldStats st;
     const uint64_t groups = (n + EPT - 1) / EPT;
     if (f.work) {
@@ -843,6 +848,7 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
     __shared__ uint2 rings[kHotThreads / 64][kRingCap];
     const uint64_t n = f.n;
     const bool filt = *f.giant != kInvalid;          // uniform
+    if (!filt) f.sbits = nullptr;                    // the next close is a full pass (k_fold)
     if (filt) lds_fill<2 * kHotBuckets>(reinterpret_cast<uint32_t*>(tab), reinterpret_cast<const uint32_t*>(hot.table), 2 * kHotBuckets);
     // the root gbits were built for (= the giant's label at the last close); survivors' giant
     // flags use it in place of a parent[] read (union_group_g). Off (kInvalid) without a filter
@@ -1131,6 +1137,7 @@ __global__ __launch_bounds__(256) void k_fold_slots(const uint32_t* __restrict__
     const int q = blockIdx.y;
     if (q == skip) return;                           // uniform
     if (caps.n && caps.v[q] < hi) hi = caps.v[q];
+    if (*f.giant == kInvalid) f.sbits = nullptr;     // the next close is a full pass (k_fold)
     const uint32_t* s = slots + (uint64_t)q * slot_words;
     const unsigned long long cnt = *reinterpret_cast<const unsigned long long*>(s);
     const uint64_t n = cnt < hi ? cnt : hi;
@@ -1289,14 +1296,29 @@ __global__ __launch_bounds__(1024) void k_pick_giant(const uint32_t* __restrict_
 // itself (a short read-only walk), so a close needs no separate pick launch; workgroup 0 clears
 // the hot set when g is another component than the hot set's owner, and writes g to the output
 // slot as the next close's giant and the root gbits were built for.
+// Prefetch of the next window's edges (gs_cc_fold_windows, small windows): workgroup b of the
+// close loads the 2 x 1 KiB of src / dst that workgroup b of the next one-edge-per-thread fold
+// reads (the same workgroup index: the same XCD under round-robin dispatch), at kernel start, and
+// consumes the registers at the end, so the loads overlap the close and the fold's first dependent
+// load finds its lines in the caches instead of HBM.
+struct EdgePrefetch {
+    const u32x4* a = nullptr;
+    const u32x4* b = nullptr;
+    uint32_t wgs = 0;            // fold workgroups covered (256 edges each)
+};
+
 __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent, uint32_t n,
                                                   uint32_t* __restrict__ gbits, uint32_t* __restrict__ sbits,
                                                   const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                   uint32_t* __restrict__ owner, uint2* __restrict__ hot, int rebuild_seen,
                                                   uint32_t* __restrict__ cbits, uint32_t* __restrict__ dbits,
-                                                  const uint32_t* __restrict__ samp_in, uint32_t* __restrict__ samp_out) {
+                                                  const uint32_t* __restrict__ samp_in, uint32_t* __restrict__ samp_out,
+                                                  EdgePrefetch pf) {
     __shared__ uint32_t s_g, s_inc, s_clear;
     __shared__ PickLds L;
+    u32x4 pfq{0u, 0u, 0u, 0u};
+    const bool pfon = blockIdx.x < pf.wgs && threadIdx.x < 128;
+    if (pfon) pfq = (threadIdx.x < 64 ? pf.a : pf.b)[(uint64_t)blockIdx.x * 64 + (threadIdx.x & 63)];
     // no giant known (none picked yet, or a re-pick found none): the mode of the labels the last
     // full pass recorded at the sample positions, the same in every workgroup (a giant that forms
     // mid-stream, e.g. an Erdos-Renyi stream past average degree 1, gets its filter at the next
@@ -1419,6 +1441,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
             }
         }
     }
+    if (pfon) asm volatile("" : : "v"(pfq.x ^ pfq.y ^ pfq.z ^ pfq.w));   // keep the prefetch loads
 }
 
 // wave64 / block reductions

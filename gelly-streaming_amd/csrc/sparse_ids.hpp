@@ -69,6 +69,7 @@ template <bool AOS, bool MARK>
 __global__ __launch_bounds__(256) void k_fold_sparse(const int64_t* __restrict__ a, const int64_t* __restrict__ b,
                                                      FoldArgs f, SparseArgs s) {
     const bool filt = *f.giant != kInvalid;
+    if (!filt) f.sbits = nullptr;                    // the next close is a full pass (k_fold)
     FoldStats st;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g * 2 < f.n; g += stride) {
@@ -153,6 +154,7 @@ __global__ __launch_bounds__(256) void k_fold_slots_sparse(const uint32_t* __res
     const int q = blockIdx.y;
     if (q == skip) return;                           // uniform
     if (caps.n && caps.v[q] < hi) hi = caps.v[q];
+    if (*f.giant == kInvalid) f.sbits = nullptr;     // the next close is a full pass (k_fold)
     const uint32_t* sq = slots + (uint64_t)q * slot_words;
     const unsigned long long cnt = *reinterpret_cast<const unsigned long long*>(sq);
     const uint64_t n = cnt < hi ? cnt : hi;

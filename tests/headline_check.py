@@ -22,8 +22,9 @@ Checks (BASELINE.json configs[2] on one GPU; tests/test_gpu_variants.py runs thi
     stream (hook-to-min + pointer jumping: bench.py torch_min_labels) and are minimal/idempotent;
   * --fold-windows: bench.py's timed call itself, gs_cc_fold_windows (the per-window loop inside the
     library), from a reset over the whole stream in one call, then the last window's emission
-    checksum against the fixture; and again in calls of --chunk windows, each call's last window
-    against the fixture.
+    checksum against the fixture; again in calls of --chunk windows, each call's last window
+    against the fixture; and the whole stream once more from a reset (for small windows the
+    replay of the HIP graph the first call captured).
 Prints one JSON line.
 """
 from __future__ import annotations
@@ -108,7 +109,11 @@ def main():
             ds.fold_windows(src[w0 * W:hi * W], dst[w0 * W:hi * W], W)
             chunked.append((hi - 1, ds.checksum()))
         bad = [w for w, g in chunked if tuple(g) != tuple(want[w])]
-        fw = {"windows": nw, "whole_ok": nw == len(want) and tuple(whole) == tuple(want[-1]),
+        ds.reset()                         # ... and the whole stream again: small windows replay the
+        nw2 = ds.fold_windows(src, dst, W)  # HIP graph the first call captured (cc_api.hip)
+        again = ds.checksum()
+        fw = {"windows": nw, "whole_ok": nw == len(want) and tuple(whole) == tuple(want[-1]) and
+              nw2 == nw and tuple(again) == tuple(whole),
               "chunked_ok": not bad, "chunked_first_bad": bad[0] if bad else None, "chunks": len(chunked),
               "final_checksum": str(whole[0])}
         print("fold_windows: %s (%.1f s)" % (fw, time.time() - t0), file=sys.stderr, flush=True)
