@@ -94,18 +94,6 @@ struct gs_cc {
     EmitPend epend[2];                   // async emissions not yet waited for, oldest first
     int n_epend = 0;
     uint32_t enext = 0;                  // slot of the next emission
-    EdgePrefetch prefetch;               // the next close prefetches these edges (gs_cc_fold_windows)
-    // gs_cc_fold_windows from a fresh summary, captured once into a HIP graph and replayed (below)
-    struct WindowsGraph {
-        hipGraphExec_t exec = nullptr;
-        const void* src = nullptr;
-        const void* dst = nullptr;
-        uint64_t n = 0, window_edges = 0;
-        // host state the captured sequence leaves behind (restored after every replay)
-        uint64_t edges_since_reset = 0, ring_launches = 0, closes = 0, pick_edges = 0;
-        bool sbits_stale = false;
-        hipEvent_t in = nullptr, out = nullptr;   // h->stream -> own stream -> h->stream
-    } wgraph;
     bool compressed = true;
     bool sbits_stale = false;            // a young launch skipped the seen bits: the next close rebuilds them
     uint64_t edges_since_reset = 0;      // drives the young-forest launch split (fold_impl)
@@ -143,8 +131,6 @@ struct gs_cc {
     uint64_t launches[GS_K_COUNT] = {};
     uint64_t units[GS_K_COUNT] = {};     // edges (folds, merges) or vertices (closes) the timed launches took
 };
-
-static void drop_windows_graph(gs_cc_t* h);
 
 namespace {
 
@@ -299,8 +285,6 @@ struct DebugEnv {
     uint64_t small_fold = kSmallFoldEdges;          // GSGPU_SMALL_FOLD: plain folds of at most this many edges...
     int small_ept = kSmallEpt;                      // GSGPU_SMALL_EPT: ...take this many edges per thread
     uint64_t young_first_min = kYoungFirstMinWg;    // GSGPU_YOUNG_FIRST_MIN: workgroup floor of the first young launch
-    bool prefetch = true;                           // GSGPU_PREFETCH=0: no edge prefetch in small-window closes (A/B)
-    bool graphs = true;                             // GSGPU_GRAPHS=0: no HIP-graph replay of gs_cc_fold_windows (A/B)
     DebugEnv() {
         const char* e = getenv("GSGPU_FOLD_STATS");
         fold_stats = e && atoi(e) != 0;
@@ -315,10 +299,6 @@ struct DebugEnv {
         if (e && *e) small_fold = strtoull(e, nullptr, 0);
         e = getenv("GSGPU_YOUNG_FIRST_MIN");
         if (e && *e) young_first_min = std::max<uint64_t>(1, strtoull(e, nullptr, 0));
-        e = getenv("GSGPU_GRAPHS");
-        if (e && *e) graphs = atoi(e) != 0;
-        e = getenv("GSGPU_PREFETCH");
-        if (e && *e) prefetch = atoi(e) != 0;
         e = getenv("GSGPU_SMALL_EPT");
         if (e && *e) small_ept = atoi(e) == 1 ? 1 : (atoi(e) == 2 ? 2 : 4);
 
@@ -666,14 +646,10 @@ int compress_impl(gs_cc_t* h) {
             klaunch(k_pick_giant, dim3(1), dim3(1024), h->stream, t.start(), nullptr, (const uint32_t*)h->parent, h->cap,
                     in, (int)force);
         ++h->closes;
-        EdgePrefetch pf = h->prefetch;
-        unsigned grid = grid_for(h->cap, 1024, kCompressGrid);
-        if (pf.wgs > grid) pf.wgs = 0;
-        klaunch(k_compress, dim3(grid), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
+        klaunch(k_compress, dim3(grid_for(h->cap, 1024, kCompressGrid)), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
                 h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot,
-                (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits, samp_in, samp_out, pf);
+                (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits, samp_in, samp_out);
         h->sbits_stale = false;
-        h->prefetch = EdgePrefetch{};
     }
     GS_HIP(hipGetLastError());
     h->compressed = true;
@@ -983,9 +959,6 @@ int gs_cc_destroy(gs_cc_t* h) {
     DeviceGuard g(h->device);
     if (h->own) (void)hipStreamSynchronize(h->own);
     if (h->stream && h->stream != h->own) (void)hipStreamSynchronize(h->stream);
-    drop_windows_graph(h);
-    if (h->wgraph.in) (void)hipEventDestroy(h->wgraph.in);
-    if (h->wgraph.out) (void)hipEventDestroy(h->wgraph.out);
     for (auto& p : h->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : h->pool) (void)hipEventDestroy(e);
     if (h->parent) (void)hipFree(h->parent);
@@ -1181,97 +1154,17 @@ int gs_cc_close_window(gs_cc_t* h) {
     return compress_impl(h);
 }
 
-static void drop_windows_graph(gs_cc_t* h) {
-    auto& G = h->wgraph;
-    if (G.exec) (void)hipGraphExecDestroy(G.exec);
-    G.exec = nullptr;
-    G.src = G.dst = nullptr;
-}
-
 // The per-window host loop of gs_cc_fold_windows (fold, then close or merge), enqueued on h->stream.
 static int fold_windows_loop(gs_cc_t* h, gs_comm_t* comm, int mode, const char* a, const char* b, uint64_t n,
-                             uint64_t window_edges, bool dev, uint64_t* windows_out) {
+                             uint64_t window_edges, uint64_t* windows_out) {
     const size_t esz = h->cfg.id_bits / 8;
     uint64_t w = 0;
     for (uint64_t off = 0; off < n; off += window_edges, ++w) {
         const uint64_t m = std::min(window_edges, n - off);
         GS_TRY(fold_impl(h, a + off * esz, b + off * esz, m, false, h->cfg.id_bits));   // (no settle: above)
-        // small windows: this window's close prefetches the next window's edges for its fold
-        // (one edge per thread, 256 per workgroup: k_compress EdgePrefetch)
-        const uint64_t nx = off + m < n ? std::min(window_edges, n - off - m) : 0;
-        if (dev && !comm && esz == 4 && nx == m && m % 256 == 0 && m <= dbg().small_fold && dbg().small_ept == 1 &&
-            h->edges_since_reset >= h->cap / 4 && !h->sparse && dbg().prefetch &&
-            ((reinterpret_cast<uintptr_t>(a + (off + m) * esz) | reinterpret_cast<uintptr_t>(b + (off + m) * esz)) & 15) == 0)
-            h->prefetch = EdgePrefetch{reinterpret_cast<const u32x4*>(a + (off + m) * esz),
-                                       reinterpret_cast<const u32x4*>(b + (off + m) * esz), (uint32_t)(m / 256)};
         GS_TRY(comm ? gs_cc_merge_window(h, comm, mode) : gs_cc_close_window(h));
         if (windows_out) *windows_out = w + 1;
     }
-    return GS_OK;
-}
-
-// A batch of small windows is host-bound: two or three launches per window, each costing the host
-// more than its kernel runs (BASELINE config 5: 2^16-edge windows). From a FRESH summary (right
-// after create or gs_cc_reset) the launch sequence depends only on (src, dst, n, window_edges):
-// every host decision (young split, fold variant, grid, close slot parity, giant picks) follows
-// from the edges folded since reset. So the first such call is captured into a HIP graph (on the
-// handle's own stream, joined to h->stream by events: the caller's stream may be the legacy
-// default stream, which cannot capture) and every later identical call from a fresh summary replays
-// it with one hipGraphLaunch, then restores the host state the sequence leaves behind.
-constexpr uint64_t kGraphMinWindows = 64;
-static bool graph_eligible(const gs_cc_t* h, gs_comm_t* comm, bool dev, uint64_t n, uint64_t window_edges) {
-    return !comm && dev && !h->sparse && !h->timing && !dbg().fold_stats && !h->dstats && h->n_epend == 0 &&
-           !h->settle_fn && h->edges_since_reset == 0 && h->closes == 0 && h->ring_launches == 0 && h->compressed &&
-           !h->sbits_stale && window_edges <= dbg().small_fold && n / window_edges >= kGraphMinWindows && dbg().graphs;
-}
-
-static int fold_windows_graph(gs_cc_t* h, const char* a, const char* b, uint64_t n, uint64_t window_edges,
-                              uint64_t* windows_out) {
-    auto& G = h->wgraph;
-    const uint64_t nwin = (n + window_edges - 1) / window_edges;
-    if (!G.in) {
-        GS_HIP(hipEventCreateWithFlags(&G.in, hipEventDisableTiming));
-        GS_HIP(hipEventCreateWithFlags(&G.out, hipEventDisableTiming));
-    }
-    hipStream_t user = h->stream;
-    GS_HIP(hipEventRecord(G.in, user));
-    GS_HIP(hipStreamWaitEvent(h->own, G.in, 0));
-    if (!(G.exec && G.src == a && G.dst == b && G.n == n && G.window_edges == window_edges)) {
-        drop_windows_graph(h);
-        h->stream = h->own;
-        hipGraph_t graph = nullptr;
-        if (hipStreamBeginCapture(h->own, hipStreamCaptureModeRelaxed) != hipSuccess) {
-            h->stream = user;
-            (void)hipGetLastError();
-            return fail(GS_ERR_HIP, "gs_cc_fold_windows: stream capture failed to begin");
-        }
-        const int rc = fold_windows_loop(h, nullptr, 0, a, b, n, window_edges, true, nullptr);
-        const hipError_t ec = hipStreamEndCapture(h->own, &graph);
-        h->stream = user;
-        if (rc != GS_OK) { if (graph) (void)hipGraphDestroy(graph); return rc; }
-        if (ec != hipSuccess || !graph) { (void)hipGetLastError(); return fail(GS_ERR_HIP, "gs_cc_fold_windows: stream capture failed"); }
-        const hipError_t ei = hipGraphInstantiate(&G.exec, graph, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(graph);
-        if (ei != hipSuccess) { G.exec = nullptr; (void)hipGetLastError(); return fail(GS_ERR_HIP, "gs_cc_fold_windows: graph instantiation failed"); }
-        G.src = a; G.dst = b; G.n = n; G.window_edges = window_edges;
-        G.edges_since_reset = h->edges_since_reset;
-        G.ring_launches = h->ring_launches;
-        G.closes = h->closes;
-        G.pick_edges = h->pick_edges;
-        G.sbits_stale = h->sbits_stale;
-    }
-    GS_HIP(hipGraphLaunch(G.exec, h->own));
-    GS_HIP(hipEventRecord(G.out, h->own));
-    GS_HIP(hipStreamWaitEvent(user, G.out, 0));
-    h->edges_since_reset = G.edges_since_reset;
-    h->ring_launches = G.ring_launches;
-    h->closes = G.closes;
-    h->pick_edges = G.pick_edges;
-    h->sbits_stale = G.sbits_stale;
-    h->compressed = true;
-    h->minkey_valid = false;
-    h->prefetch = EdgePrefetch{};
-    if (windows_out) *windows_out = nwin;
     return GS_OK;
 }
 
@@ -1283,12 +1176,7 @@ int gs_cc_fold_windows(gs_cc_t* h, gs_comm_t* comm, int mode, const void* src, c
     if (n && (!src || !dst)) return fail(GS_ERR_INVALID, "gs_cc_fold_windows: null edge buffer");
     const char* a = static_cast<const char*>(src);
     const char* b = static_cast<const char*>(dst);
-    const bool dev = n && is_device_pointer(src) && is_device_pointer(dst);
-    if (graph_eligible(h, comm, dev, n, window_edges)) {
-        DeviceGuard g(h->device);
-        return fold_windows_graph(h, a, b, n, window_edges, windows_out);
-    }
-    GS_TRY(fold_windows_loop(h, comm, mode, a, b, n, window_edges, dev, windows_out));
+    GS_TRY(fold_windows_loop(h, comm, mode, a, b, n, window_edges, windows_out));
     return cc_settle(h);                             // the last window's exchange verified
 }
 

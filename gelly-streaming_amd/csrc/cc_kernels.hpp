@@ -1296,29 +1296,14 @@ __global__ __launch_bounds__(1024) void k_pick_giant(const uint32_t* __restrict_
 // itself (a short read-only walk), so a close needs no separate pick launch; workgroup 0 clears
 // the hot set when g is another component than the hot set's owner, and writes g to the output
 // slot as the next close's giant and the root gbits were built for.
-// Prefetch of the next window's edges (gs_cc_fold_windows, small windows): workgroup b of the
-// close loads the 2 x 1 KiB of src / dst that workgroup b of the next one-edge-per-thread fold
-// reads (the same workgroup index: the same XCD under round-robin dispatch), at kernel start, and
-// consumes the registers at the end, so the loads overlap the close and the fold's first dependent
-// load finds its lines in the caches instead of HBM.
-struct EdgePrefetch {
-    const u32x4* a = nullptr;
-    const u32x4* b = nullptr;
-    uint32_t wgs = 0;            // fold workgroups covered (256 edges each)
-};
-
 __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent, uint32_t n,
                                                   uint32_t* __restrict__ gbits, uint32_t* __restrict__ sbits,
                                                   const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                   uint32_t* __restrict__ owner, uint2* __restrict__ hot, int rebuild_seen,
                                                   uint32_t* __restrict__ cbits, uint32_t* __restrict__ dbits,
-                                                  const uint32_t* __restrict__ samp_in, uint32_t* __restrict__ samp_out,
-                                                  EdgePrefetch pf) {
+                                                  const uint32_t* __restrict__ samp_in, uint32_t* __restrict__ samp_out) {
     __shared__ uint32_t s_g, s_inc, s_clear;
     __shared__ PickLds L;
-    u32x4 pfq{0u, 0u, 0u, 0u};
-    const bool pfon = blockIdx.x < pf.wgs && threadIdx.x < 128;
-    if (pfon) pfq = (threadIdx.x < 64 ? pf.a : pf.b)[(uint64_t)blockIdx.x * 64 + (threadIdx.x & 63)];
     // no giant known (none picked yet, or a re-pick found none): the mode of the labels the last
     // full pass recorded at the sample positions, the same in every workgroup (a giant that forms
     // mid-stream, e.g. an Erdos-Renyi stream past average degree 1, gets its filter at the next
@@ -1441,7 +1426,6 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
             }
         }
     }
-    if (pfon) asm volatile("" : : "v"(pfq.x ^ pfq.y ^ pfq.z ^ pfq.w));   // keep the prefetch loads
 }
 
 // wave64 / block reductions

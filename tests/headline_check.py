@@ -23,8 +23,7 @@ Checks (BASELINE.json configs[2] on one GPU; tests/test_gpu_variants.py runs thi
   * --fold-windows: bench.py's timed call itself, gs_cc_fold_windows (the per-window loop inside the
     library), from a reset over the whole stream in one call, then the last window's emission
     checksum against the fixture; again in calls of --chunk windows, each call's last window
-    against the fixture; and the whole stream once more from a reset (for small windows the
-    replay of the HIP graph the first call captured).
+    against the fixture; and the whole stream once more from a reset (the same result again).
 Prints one JSON line.
 """
 from __future__ import annotations
@@ -109,8 +108,8 @@ def main():
             ds.fold_windows(src[w0 * W:hi * W], dst[w0 * W:hi * W], W)
             chunked.append((hi - 1, ds.checksum()))
         bad = [w for w, g in chunked if tuple(g) != tuple(want[w])]
-        ds.reset()                         # ... and the whole stream again: small windows replay the
-        nw2 = ds.fold_windows(src, dst, W)  # HIP graph the first call captured (cc_api.hip)
+        ds.reset()                         # ... and the whole stream again from a reset
+        nw2 = ds.fold_windows(src, dst, W)
         again = ds.checksum()
         fw = {"windows": nw, "whole_ok": nw == len(want) and tuple(whole) == tuple(want[-1]) and
               nw2 == nw and tuple(again) == tuple(whole),
