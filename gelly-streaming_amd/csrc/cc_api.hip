@@ -67,6 +67,8 @@ struct gs_cc {
     uint32_t* gbits = nullptr;           // giant-component filter bitmap (1 bit per vertex)
     uint32_t* sbits = nullptr;           // seen bitmap (1 bit per vertex), set on first touch
     uint32_t* cbits = nullptr;           // ring folds: first touches claimed under the giant root
+    uint32_t* hkbits[2] = {nullptr, nullptr}; // roots hooked before any giant exists, by close parity
+    bool hkbits_ok = true;               // every fold since the last close marked its hooked roots
     uint32_t* dbits = nullptr;           // delta emission: vertices a close may have relabelled since the last delta
     uint32_t* elab = nullptr;            // delta emission: the labels last emitted (kInvalid: never)
     uint32_t* derr = nullptr;            // derr[0] deferred device error flags; derr[1..5] giant state
@@ -340,6 +342,11 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
     ensure_stats(h);
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
     f.mark_len = h->mark_ctr;
+    // hooked roots marked (while no giant exists, k_fold) by mature SoA launches only: in the young
+    // forest the marks would cost an atomic per hook for a close whose grandparent reads hit L2
+    // anyway (an RMAT window 1's non-roots hang under a few hub roots)
+    if (!young && !AOS && h->hkbits[0]) f.hbits = h->hkbits[h->closes & 1];
+    else h->hkbits_ok = false;
     // a big young launch (>= capacity/16 edges, i.e. window 1 of the headline) leaves the seen
     // bitmap to the close that follows it — a full pass in any case while the forest is this
     // young — and saves one device-scope atomic per new vertex (window 1: ~6.4M)
@@ -422,6 +429,8 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
     f.mark_len = h->mark_ctr;
     f.cbits = kUseCbits ? h->cbits : nullptr;
+    if (h->hkbits[0]) f.hbits = h->hkbits[h->closes & 1];
+    else h->hkbits_ok = false;
     KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_RING : h->fold_timer, n);
     const bool st = h->dstats != nullptr;
     const dim3 grid(grid_for(n / 4, kHotThreads, (unsigned)std::max(h->cus, 1)));
@@ -518,6 +527,7 @@ SparseArgs sparse_args(gs_cc_t* h) {
 constexpr uint64_t kSparseYoungChunk = 1ull << 18;
 void launch_fold_sparse(gs_cc_t* h, const int64_t* a, const int64_t* b, uint64_t n, bool aos) {
     const SparseArgs sa = sparse_args(h);
+    h->hkbits_ok = false;
     const uint64_t young_limit = h->cfg.vertex_capacity / 4;
     uint64_t off = 0;
     while (off < n) {
@@ -646,10 +656,14 @@ int compress_impl(gs_cc_t* h) {
             klaunch(k_pick_giant, dim3(1), dim3(1024), h->stream, t.start(), nullptr, (const uint32_t*)h->parent, h->cap,
                     in, (int)force);
         ++h->closes;
+        // (the close about to run is number closes - 1 now: it reads the marks of its parity)
+        const uint32_t* hb_in = (h->hkbits[0] && h->hkbits_ok) ? h->hkbits[(h->closes - 1) & 1] : nullptr;
+        uint32_t* hb_next = h->hkbits[0] ? h->hkbits[h->closes & 1] : nullptr;
         klaunch(k_compress, dim3(grid_for(h->cap, 1024, kCompressGrid)), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
                 h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot,
-                (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits, samp_in, samp_out);
+                (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits, samp_in, samp_out, hb_in, hb_next);
         h->sbits_stale = false;
+        h->hkbits_ok = true;
     }
     GS_HIP(hipGetLastError());
     h->compressed = true;
@@ -793,6 +807,7 @@ int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int ns
     h->minkey_valid = false;
     FoldArgs f{0, h->parent, nullptr, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, nullptr};
     KTimer t(h, GS_K_MERGE);
+    h->hkbits_ok = false;
     if (h->sparse) {                                 // (id, id) int64 pairs, hashed to slots
         const dim3 grid(grid_for(cap, 256, (unsigned)std::max(64, 4096 / nslots)), (unsigned)nslots);
         klaunch(k_fold_slots_sparse, grid, dim3(256), h->stream, t.start(), t.stop(), slots, slot_words, skip, (uint64_t)0,
@@ -897,6 +912,11 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
         return bail(fail(GS_ERR_NOMEM, "scratch allocation failed"));
     }
     std::memset(h->hscratch, 0, 8 * sizeof(unsigned long long));
+    if (!sparse && (hipMalloc(&h->hkbits[0], mark_bytes(h->cap)) != hipSuccess ||
+                    hipMalloc(&h->hkbits[1], mark_bytes(h->cap)) != hipSuccess)) {
+        (void)hipGetLastError();
+        return bail(fail(GS_ERR_NOMEM, "hooked-root bitmaps allocation failed"));
+    }
     if (sparse && (hipMalloc(&h->keys, sizeof(int64_t) << h->hbits) != hipSuccess ||
                    hipMalloc(&h->minkey, sizeof(int64_t) * (size_t)h->cap) != hipSuccess ||
                    hipMalloc(&h->nkeys, sizeof(unsigned long long)) != hipSuccess)) {
@@ -969,6 +989,7 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->gbits) (void)hipFree(h->gbits);
     if (h->sbits) (void)hipFree(h->sbits);
     if (h->cbits) (void)hipFree(h->cbits);
+    for (auto* hb : h->hkbits) if (hb) (void)hipFree(hb);
     if (h->dbits) (void)hipFree(h->dbits);
     if (h->elab) (void)hipFree(h->elab);
     if (h->dstats) (void)hipFree(h->dstats);
@@ -1013,6 +1034,8 @@ int gs_cc_reset(gs_cc_t* h) {
     GS_HIP(hipMemsetAsync(h->gbits, 0, mark_bytes(h->cap), h->stream));
     GS_HIP(hipMemsetAsync(h->sbits, 0, mark_bytes(h->cap), h->stream));
     GS_HIP(hipMemsetAsync(h->cbits, 0, mark_bytes(h->cap), h->stream));
+    for (auto* hb : h->hkbits) if (hb) GS_HIP(hipMemsetAsync(hb, 0, mark_bytes(h->cap), h->stream));
+    h->hkbits_ok = true;
     if (h->elab) {                       // a new stream: the next delta is the whole emission
         GS_HIP(hipMemsetAsync(h->elab, 0xFF, (size_t)h->cap * 4, h->stream));
         GS_HIP(hipMemsetAsync(h->dbits, 0, mark_bytes(h->cap), h->stream));
@@ -1110,6 +1133,7 @@ int gs_cc_merge(gs_cc_t* into, gs_cc_t* from) {
     }
     into->compressed = false;
     into->minkey_valid = false;
+    into->hkbits_ok = false;
     if (into->sparse) {
         KTimer t(into, GS_K_MERGE);
         const dim3 grid(grid_for(from->cap, 256, 16384));

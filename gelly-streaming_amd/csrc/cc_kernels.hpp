@@ -85,10 +85,14 @@ struct FoldStats {
     uint32_t early = 0, hooks = 0, casfail = 0, inits = 0;
 };
 
+// hbits (or null): the hooked-root bitmap of a fold before any giant exists (k_compress: the full
+// pass that must follow reads it instead of every vertex's grandparent) — a root that stops being a
+// root here gets its bit
 template <bool MARK, bool STATS = false>
 __device__ __forceinline__ uint32_t union_edge(uint32_t* __restrict__ parent, uint32_t* __restrict__ sbits,
                                                uint32_t u, uint32_t v, uint32_t pu, uint32_t pv,
-                                               FoldStats* st = nullptr, bool halve = true) {
+                                               FoldStats* st = nullptr, bool halve = true,
+                                               uint32_t* __restrict__ hbits = nullptr) {
     if (u == v) {                                   // union(u,u): makeSet only
         if (pu == kInvalid) {
             const uint32_t old = atomicCAS(&parent[u], kInvalid, u);
@@ -131,6 +135,7 @@ __device__ __forceinline__ uint32_t union_edge(uint32_t* __restrict__ parent, ui
         const uint32_t old = atomicCAS(&parent[hi], expect, lo);
         if (old == expect) {                        // hooked: hi is no longer a root
             if (hf) set_seen(sbits, hi);
+            else if (hbits) set_mark(hbits, hi);    // (a fresh hi never had children: no mark)
             if (STATS) ++st->hooks;
             return MARK ? hi : kInvalid;
         }
@@ -217,6 +222,7 @@ struct FoldArgs {
     unsigned long long* work = nullptr;   // k_fold: dynamic chunk counter (young forest), or null
     unsigned long long* mark_len = nullptr;   // MARK: the hook log's length word (mark = the log)
     uint32_t* cbits = nullptr;   // ring folds: vertices claimed straight under the giant root (k_compress)
+    uint32_t* hbits = nullptr;   // hooked-root bitmap, used by the kernel only while no giant exists
 };
 
 // ---- LDS hot set (steady state) ----
@@ -528,7 +534,8 @@ __device__ __forceinline__ void union_group(const FoldArgs& f, const uint32_t (&
 #pragma unroll
     for (int k = 0; k < EPT; ++k)
         m[k] = ok[k] ? union_edge<MARK, STATS>(f.parent, f.sbits, u[k], v[k], pu[k], pv[k], &st,
-                                               f.halve == 1 || (f.halve > 1 && ((u[k] * 0x9E3779B1u) >> 29) == 0)) : kInvalid;
+                                               f.halve == 1 || (f.halve > 1 && ((u[k] * 0x9E3779B1u) >> 29) == 0),
+                                               f.hbits) : kInvalid;
     if (MARK) log_append<EPT>(f.mark, f.mark_len, m);
 }
 
@@ -575,7 +582,7 @@ __device__ __forceinline__ void union_group_g(const FoldArgs& f, const uint32_t 
             if (STATS) { ++st.inits; ++st.hooks; }
             m[k] = MARK ? x : kInvalid;
         } else {
-            m[k] = ok[k] ? union_edge<MARK, STATS>(f.parent, f.sbits, u[k], v[k], pu[k], pv[k], &st, f.halve != 0) : kInvalid;
+            m[k] = ok[k] ? union_edge<MARK, STATS>(f.parent, f.sbits, u[k], v[k], pu[k], pv[k], &st, f.halve != 0, f.hbits) : kInvalid;
         }
     }
     if (MARK && marks_out) {                         // the caller appends them (ring_flush_final)
@@ -672,6 +679,7 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
     // bitmap from parent[] — first touches skip their seen-bit atomic (Erdos-Renyi windows before the
     // giant forms: ~1 M memory-side atomics per 2^20-edge window)
     if (!filt) f.sbits = nullptr;
+    else f.hbits = nullptr;                          // (hooked roots are marked only before a giant)
     FoldStats st;
     const uint64_t groups = (n + EPT - 1) / EPT;
     if (f.work) {
@@ -849,6 +857,7 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
     const uint64_t n = f.n;
     const bool filt = *f.giant != kInvalid;          // uniform
     if (!filt) f.sbits = nullptr;                    // the next close is a full pass (k_fold)
+    else f.hbits = nullptr;
     if (filt) lds_fill<2 * kHotBuckets>(reinterpret_cast<uint32_t*>(tab), reinterpret_cast<const uint32_t*>(hot.table), 2 * kHotBuckets);
     // the root gbits were built for (= the giant's label at the last close); survivors' giant
     // flags use it in place of a parent[] read (union_group_g). Off (kInvalid) without a filter
@@ -1301,7 +1310,8 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                                                   const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                   uint32_t* __restrict__ owner, uint2* __restrict__ hot, int rebuild_seen,
                                                   uint32_t* __restrict__ cbits, uint32_t* __restrict__ dbits,
-                                                  const uint32_t* __restrict__ samp_in, uint32_t* __restrict__ samp_out) {
+                                                  const uint32_t* __restrict__ samp_in, uint32_t* __restrict__ samp_out,
+                                                  const uint32_t* __restrict__ hb_in, uint32_t* __restrict__ hb_next) {
     __shared__ uint32_t s_g, s_inc, s_clear;
     __shared__ PickLds L;
     // no giant known (none picked yet, or a re-pick found none): the mode of the labels the last
@@ -1379,6 +1389,15 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
         }
     } else {
         const uint32_t sb = samp_shift(n);
+        // Hooked-root bitmap (hb_in, non-null only when every fold since the last close marked the
+        // roots it hooked, i.e. none had a giant to filter with, so this close cannot be incremental):
+        // a vertex's parent p that was a root at the last close (every seen vertex pointed to one)
+        // and is unmarked is still a root, so its grandparent read (a random 4-B read of parent[]
+        // per seen vertex: HBM / Infinity-Cache bound, ~170 us per close of an Erdos-Renyi window
+        // before the giant forms) becomes a bit test in a V/8-byte bitmap that stays in L2. Every
+        // parent word written since the last close is a root at the time of writing (a hook's lo, a
+        // claim's gR, a halving's grandparent), so "unmarked" is exact.
+        const bool usehb = hb_in != nullptr && in[1] == kInvalid;
         for (uint64_t blk = (uint64_t)blockIdx.x * 1024; blk < n; blk += (uint64_t)gridDim.x * 1024) {
             const uint32_t base = (uint32_t)blk + threadIdx.x * 4;
             uint32_t p[4];
@@ -1389,12 +1408,19 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
 #pragma unroll
                 for (int k = 0; k < 4; ++k) p[k] = ((uint64_t)base + k < n) ? parent[base + k] : kInvalid;
             }
+            bool need[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) need[k] = p[k] != kInvalid && p[k] != base + k;
+            if (usehb) {
+                uint32_t hw[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) hw[k] = need[k] ? hb_in[p[k] >> 5] : 0u;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) need[k] = need[k] && ((hw[k] >> (p[k] & 31)) & 1u);
+            }
             uint32_t gp[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t v = base + k;
-                gp[k] = (p[k] != kInvalid && p[k] != v) ? parent[p[k]] : p[k];
-            }
+            for (int k = 0; k < 4; ++k) gp[k] = need[k] ? parent[p[k]] : p[k];
             uint32_t nib = 0, seen = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -1422,6 +1448,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                     sbits[base >> 5] = sw;
                     if (cbits) cbits[base >> 5] = 0u;    // this pass labelled the claimed vertices too
                     if (dbits) dbits[base >> 5] = sw;    // a full pass may relabel any seen vertex
+                    if (hb_next) hb_next[base >> 5] = 0u;   // the next window's hooked-root marks start empty
                 }
             }
         }
