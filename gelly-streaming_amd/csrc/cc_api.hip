@@ -70,6 +70,15 @@ struct gs_cc {
     uint32_t* hkbits[2] = {nullptr, nullptr}; // roots hooked before any giant exists, by close parity
     bool hkbits_ok = true;               // every fold since the last close marked its hooked roots
     uint32_t* dbits = nullptr;           // delta emission: vertices a close may have relabelled since the last delta
+    // list-mode closes (cc_kernels.hpp ListCtl): control words, the NGL (seen vertices outside the
+    // giant) and the touch log, each double-buffered by close parity
+    uint32_t* lctl = nullptr;
+    uint2* ngl[2] = {nullptr, nullptr};
+    uint32_t* tlog[2] = {nullptr, nullptr};
+    uint32_t ngl_sub = 0;
+    bool ilist_ok = true;                // every fold since the last close logged its first touches
+    uint32_t ilist_folds = 0;            // logged folds since the last close
+    uint32_t ilist_slots = 0;            // touch-log slots they took (one per wave)
     uint32_t* elab = nullptr;            // delta emission: the labels last emitted (kInvalid: never)
     uint32_t* derr = nullptr;            // derr[0] deferred device error flags; derr[1..5] giant state
     uint32_t* psamp = nullptr;           // 2 x kPickSamples labels a full-pass close recorded (k_compress)
@@ -271,6 +280,9 @@ constexpr uint32_t kYoungSplitDiv = 16;
 // at 4 edges per thread filled 64 workgroups). Config 5: 3.94 -> 5.09 G edges/s, per-window latency
 // p50 29.9 -> 23.5 us; at 2^20 edges per launch config 2 +3 %, config 4 -1.5 % (profiles/r03_small)
 constexpr uint64_t kSmallFoldEdges = 1u << 18;
+// list-mode closes: one-edge-per-thread folds log their first touches into one touch-log slot per
+// wave, up to kTlogSlots slots per window (2^18 edges; beyond: the close is a bitmap or full one)
+constexpr uint32_t kTlogSlots = 4096;
 constexpr int kSmallEpt = 1;
 
 // ---- debug variables (read once per process; none is needed in production) ----
@@ -287,6 +299,7 @@ struct DebugEnv {
     uint64_t small_fold = kSmallFoldEdges;          // GSGPU_SMALL_FOLD: plain folds of at most this many edges...
     int small_ept = kSmallEpt;                      // GSGPU_SMALL_EPT: ...take this many edges per thread
     uint64_t young_first_min = kYoungFirstMinWg;    // GSGPU_YOUNG_FIRST_MIN: workgroup floor of the first young launch
+    bool list_close = true;                         // GSGPU_LIST_CLOSE=0: no list-mode closes (A/B)
     DebugEnv() {
         const char* e = getenv("GSGPU_FOLD_STATS");
         fold_stats = e && atoi(e) != 0;
@@ -303,6 +316,8 @@ struct DebugEnv {
         if (e && *e) young_first_min = std::max<uint64_t>(1, strtoull(e, nullptr, 0));
         e = getenv("GSGPU_SMALL_EPT");
         if (e && *e) small_ept = atoi(e) == 1 ? 1 : (atoi(e) == 2 ? 2 : 4);
+        e = getenv("GSGPU_LIST_CLOSE");
+        if (e && *e) list_close = atoi(e) != 0;
 
     }
 };
@@ -353,6 +368,17 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
     if (young && !AOS && n >= h->cap / kYoungSplitDiv) {
         f.sbits = nullptr;
         h->sbits_stale = true;
+    }
+    // one-edge-per-thread mature SoA folds log their first touches (touch-log slots) for a list-mode
+    // close; any other fold makes the next close a bitmap or full one
+    const uint32_t waves = grid * (kFoldThreads / 64);
+    if (h->lctl && !young && !AOS && !h->dbits && dbg().list_close && ept == 1 && !persist &&
+        (uint64_t)grid * kFoldThreads >= n && h->ilist_slots + waves <= kTlogSlots) {
+        f.tlog = h->tlog[h->closes & 1] + (size_t)h->ilist_slots * kSlotWords;
+        ++h->ilist_folds;
+        h->ilist_slots += waves;
+    } else {
+        h->ilist_ok = false;
     }
     if (persist) {
         f.work = reinterpret_cast<unsigned long long*>(h->derr + kWorkWord);
@@ -431,6 +457,7 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     f.cbits = kUseCbits ? h->cbits : nullptr;
     if (h->hkbits[0]) f.hbits = h->hkbits[h->closes & 1];
     else h->hkbits_ok = false;
+    h->ilist_ok = false;
     KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_RING : h->fold_timer, n);
     const bool st = h->dstats != nullptr;
     const dim3 grid(grid_for(n / 4, kHotThreads, (unsigned)std::max(h->cus, 1)));
@@ -528,6 +555,7 @@ constexpr uint64_t kSparseYoungChunk = 1ull << 18;
 void launch_fold_sparse(gs_cc_t* h, const int64_t* a, const int64_t* b, uint64_t n, bool aos) {
     const SparseArgs sa = sparse_args(h);
     h->hkbits_ok = false;
+    h->ilist_ok = false;
     const uint64_t young_limit = h->cfg.vertex_capacity / 4;
     uint64_t off = 0;
     while (off < n) {
@@ -649,6 +677,26 @@ int compress_impl(gs_cc_t* h) {
                            (h->closes == 0 || h->edges_since_reset - h->pick_edges >= kPickMinEdges);
         const bool pick = force || h->closes < kEarlyPicks;
         if (force) h->pick_edges = h->edges_since_reset;
+        ListClose lc;
+        unsigned grid = grid_for(h->cap, 1024, kCompressGrid);
+        if (h->lctl) {
+            const uint64_t c = h->closes;
+            lc.ctl = h->lctl;
+            lc.ngl_in = h->ngl[c & 1];
+            lc.ngl_out = h->ngl[(c + 1) & 1];
+            lc.ngl_sub = h->ngl_sub;
+            lc.tlog = h->tlog[c & 1];
+            lc.nslots = h->ilist_slots;
+            lc.c3 = (uint32_t)(c % 3);
+            lc.n3 = (uint32_t)((c + 1) % 3);
+            lc.z3 = (uint32_t)((c + 2) % 3);
+            lc.unlogged = (!h->ilist_ok || h->dbits) ? 1u : 0u;
+            lc.list_next = (h->ilist_ok && h->ilist_folds > 0 && !h->dbits && dbg().list_close) ? 1u : 0u;
+            grid = (grid + kListSub - 1) / kListSub * kListSub;      // whole sets of list workgroups
+        }
+        h->ilist_ok = true;
+        h->ilist_folds = 0;
+        h->ilist_slots = 0;
         uint32_t* in = giant_state(h);
         const uint32_t* samp_in = h->psamp + (h->closes & 1) * kPickSamples;
         uint32_t* samp_out = h->psamp + ((h->closes + 1) & 1) * kPickSamples;
@@ -659,9 +707,9 @@ int compress_impl(gs_cc_t* h) {
         // (the close about to run is number closes - 1 now: it reads the marks of its parity)
         const uint32_t* hb_in = (h->hkbits[0] && h->hkbits_ok) ? h->hkbits[(h->closes - 1) & 1] : nullptr;
         uint32_t* hb_next = h->hkbits[0] ? h->hkbits[h->closes & 1] : nullptr;
-        klaunch(k_compress, dim3(grid_for(h->cap, 1024, kCompressGrid)), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
+        klaunch(k_compress, dim3(grid), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
                 h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot,
-                (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits, samp_in, samp_out, hb_in, hb_next);
+                (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits, samp_in, samp_out, hb_in, hb_next, lc);
         h->sbits_stale = false;
         h->hkbits_ok = true;
     }
@@ -808,6 +856,7 @@ int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int ns
     FoldArgs f{0, h->parent, nullptr, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, nullptr};
     KTimer t(h, GS_K_MERGE);
     h->hkbits_ok = false;
+    h->ilist_ok = false;
     if (h->sparse) {                                 // (id, id) int64 pairs, hashed to slots
         const dim3 grid(grid_for(cap, 256, (unsigned)std::max(64, 4096 / nslots)), (unsigned)nslots);
         klaunch(k_fold_slots_sparse, grid, dim3(256), h->stream, t.start(), t.stop(), slots, slot_words, skip, (uint64_t)0,
@@ -917,6 +966,19 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
         (void)hipGetLastError();
         return bail(fail(GS_ERR_NOMEM, "hooked-root bitmaps allocation failed"));
     }
+    if (!sparse) {
+        // NGL: up to capacity/64 vertices outside the giant (more: bitmap closes); touch log:
+        // kTlogSlots slots per interval
+        h->ngl_sub = (uint32_t)std::min<uint64_t>(4096, std::max<uint64_t>(64, (uint64_t)h->cap / 64 / kListSub));
+        if (hipMalloc(&h->lctl, ListCtl::kWords * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc(&h->ngl[0], (size_t)kListSub * h->ngl_sub * sizeof(uint2)) != hipSuccess ||
+            hipMalloc(&h->ngl[1], (size_t)kListSub * h->ngl_sub * sizeof(uint2)) != hipSuccess ||
+            hipMalloc(&h->tlog[0], (size_t)kTlogSlots * kSlotWords * 4) != hipSuccess ||
+            hipMalloc(&h->tlog[1], (size_t)kTlogSlots * kSlotWords * 4) != hipSuccess) {
+            (void)hipGetLastError();
+            return bail(fail(GS_ERR_NOMEM, "list-close buffers allocation failed"));
+        }
+    }
     if (sparse && (hipMalloc(&h->keys, sizeof(int64_t) << h->hbits) != hipSuccess ||
                    hipMalloc(&h->minkey, sizeof(int64_t) * (size_t)h->cap) != hipSuccess ||
                    hipMalloc(&h->nkeys, sizeof(unsigned long long)) != hipSuccess)) {
@@ -990,6 +1052,9 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->sbits) (void)hipFree(h->sbits);
     if (h->cbits) (void)hipFree(h->cbits);
     for (auto* hb : h->hkbits) if (hb) (void)hipFree(hb);
+    if (h->lctl) (void)hipFree(h->lctl);
+    for (auto* q : h->ngl) if (q) (void)hipFree(q);
+    for (auto* q : h->tlog) if (q) (void)hipFree(q);
     if (h->dbits) (void)hipFree(h->dbits);
     if (h->elab) (void)hipFree(h->elab);
     if (h->dstats) (void)hipFree(h->dstats);
@@ -1036,6 +1101,10 @@ int gs_cc_reset(gs_cc_t* h) {
     GS_HIP(hipMemsetAsync(h->cbits, 0, mark_bytes(h->cap), h->stream));
     for (auto* hb : h->hkbits) if (hb) GS_HIP(hipMemsetAsync(hb, 0, mark_bytes(h->cap), h->stream));
     h->hkbits_ok = true;
+    if (h->lctl) GS_HIP(hipMemsetAsync(h->lctl, 0, ListCtl::kWords * sizeof(uint32_t), h->stream));
+    h->ilist_ok = true;
+    h->ilist_folds = 0;
+    h->ilist_slots = 0;
     if (h->elab) {                       // a new stream: the next delta is the whole emission
         GS_HIP(hipMemsetAsync(h->elab, 0xFF, (size_t)h->cap * 4, h->stream));
         GS_HIP(hipMemsetAsync(h->dbits, 0, mark_bytes(h->cap), h->stream));
@@ -1134,6 +1203,7 @@ int gs_cc_merge(gs_cc_t* into, gs_cc_t* from) {
     into->compressed = false;
     into->minkey_valid = false;
     into->hkbits_ok = false;
+    into->ilist_ok = false;
     if (into->sparse) {
         KTimer t(into, GS_K_MERGE);
         const dim3 grid(grid_for(from->cap, 256, 16384));

@@ -88,16 +88,29 @@ struct FoldStats {
 // hbits (or null): the hooked-root bitmap of a fold before any giant exists (k_compress: the full
 // pass that must follow reads it instead of every vertex's grandparent) — a root that stops being a
 // root here gets its bit
+// nl (or null): a logging fold (touch log, below) also collects the vertices this edge
+// first-touches (at most two)
+struct NewV {
+    uint32_t a = kInvalid, b = kInvalid;
+};
+__device__ __forceinline__ void first_touch(uint32_t* __restrict__ sbits, NewV* nl, uint32_t x) {
+    if (nl) {
+        if (nl->a == kInvalid) nl->a = x;
+        else nl->b = x;
+    }
+    set_seen(sbits, x);
+}
+
 template <bool MARK, bool STATS = false>
 __device__ __forceinline__ uint32_t union_edge(uint32_t* __restrict__ parent, uint32_t* __restrict__ sbits,
                                                uint32_t u, uint32_t v, uint32_t pu, uint32_t pv,
                                                FoldStats* st = nullptr, bool halve = true,
-                                               uint32_t* __restrict__ hbits = nullptr) {
+                                               uint32_t* __restrict__ hbits = nullptr, NewV* nl = nullptr) {
     if (u == v) {                                   // union(u,u): makeSet only
         if (pu == kInvalid) {
             const uint32_t old = atomicCAS(&parent[u], kInvalid, u);
             if (old == kInvalid) {
-                set_seen(sbits, u);
+                first_touch(sbits, nl, u);
                 if (MARK) return u;
             }
         }
@@ -124,7 +137,7 @@ __device__ __forceinline__ uint32_t union_edge(uint32_t* __restrict__ parent, ui
             const uint32_t old = atomicCAS(&parent[lo], kInvalid, lo);
             lf = false;
             if (old == kInvalid) {
-                set_seen(sbits, lo);
+                first_touch(sbits, nl, lo);
             } else if (old != lo) {                 // initialised and hooked meanwhile
                 const uint32_t r = find_root(parent, old, parent[old], halve);
                 if (uhi) rv = r; else ru = r;
@@ -134,7 +147,7 @@ __device__ __forceinline__ uint32_t union_edge(uint32_t* __restrict__ parent, ui
         const uint32_t expect = hf ? kInvalid : hi;
         const uint32_t old = atomicCAS(&parent[hi], expect, lo);
         if (old == expect) {                        // hooked: hi is no longer a root
-            if (hf) set_seen(sbits, hi);
+            if (hf) first_touch(sbits, nl, hi);
             else if (hbits) set_mark(hbits, hi);    // (a fresh hi never had children: no mark)
             if (STATS) ++st->hooks;
             return MARK ? hi : kInvalid;
@@ -188,6 +201,67 @@ __device__ __forceinline__ void log_append(uint32_t* __restrict__ log, unsigned 
     }
 }
 
+// ---- list-mode closes (small windows) ----
+// While the seen vertices outside the giant are few (config 5: ~10^4 of 2^24), a close visits a
+// list of them (the NGL) plus the window's first touches (the touch log) instead of scanning three
+// V-bit bitmaps: the close follows the window, not V.
+// Touch log: one slot per fold wave (kSlotWords words, whole 128-B lines: word 0 the count, then up
+// to 2 x 64 first touches), written by that wave alone with plain stores, no atomic (a returning
+// atomic per wave put ~1 us on config 5's fold). The host numbers the slots of an interval's folds.
+// A logging fold still sets the seen bits, so whether the close can take the list (below) is the
+// close's own decision: a fold reads no control word (two more dependent loads at the head of a
+// 6 us launch cost ~1 us).
+// NGL: (vertex, label) pairs in kListSub sub-lists (sub-list = the close's workgroup index mod
+// kListSub), appended one atomic per wave, so that the appends spread over kListSub count words. An
+// entry whose label is still a root keeps it (parent[v] is that label since the last close): one
+// read of parent[label] per entry instead of parent[v] then parent[parent[v]].
+// Control words (one array per handle, ListCtl below), by close number c (interval c = the folds
+// between close c-1 and close c):
+//   NC(k, s)   entries of NGL sub-list s written by close c with (c + 1) % 3 == k
+//   LVALID(k)  close c-1 built a complete NGL with a giant, expecting logging folds (list_next)
+//   LOVF(k)    an NGL sub-list overflowed (the list is incomplete: no list close)
+// Close c reads index c % 3, appends (c + 1) % 3 and zeroes what no launch before close c + 1
+// reads: NC / LOVF at (c + 2) % 3.
+constexpr uint32_t kListSub = 256;
+constexpr uint32_t kSlotWords = 160;                 // 1 + 128 entries, rounded up to 5 lines
+struct ListCtl {
+    __host__ __device__ static constexpr uint32_t NC(uint32_t k) { return k * kListSub; }
+    __host__ __device__ static constexpr uint32_t LVALID(uint32_t k) { return 3 * kListSub + 32 * k; }
+    __host__ __device__ static constexpr uint32_t LOVF(uint32_t k) { return 3 * kListSub + 128 + 32 * k; }
+    static constexpr uint32_t kWords = 3 * kListSub + 256;
+};
+
+// Appends the lanes' entries (m[k].x != kInvalid) to a sub-list of capacity cap: one atomicAdd per
+// wave call (any set of active lanes). Entries past cap are dropped and *ovf is set; the count keeps
+// growing (readers take min(count, cap) and check ovf).
+template <int N>
+__device__ __forceinline__ void list_append(uint2* __restrict__ list, uint32_t* __restrict__ cnt, uint32_t cap,
+                                            uint32_t* __restrict__ ovf, const uint2 (&m)[N]) {
+    const uint64_t lt = (1ull << __lane_id()) - 1;
+    uint64_t masks[N];
+    uint32_t total = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        masks[k] = __ballot(m[k].x != kInvalid);
+        total += (uint32_t)__popcll(masks[k]);
+    }
+    if (total == 0) return;                          // uniform over the active lanes
+    const uint64_t active = __ballot(1);
+    const int leader = __ffsll((long long)active) - 1;
+    uint32_t base = 0;
+    if ((int)__lane_id() == leader) {
+        base = atomicAdd(cnt, total);
+        if (base + total > cap) atomicOr(ovf, 1u);
+    }
+    uint32_t pos = __shfl(base, leader, 64);
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const uint32_t at = pos + (uint32_t)__popcll(masks[k] & lt);
+        if (m[k].x != kInvalid && at < cap) list[at] = m[k];
+        pos += (uint32_t)__popcll(masks[k]);
+    }
+}
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 struct RangeCheck {
@@ -223,7 +297,34 @@ struct FoldArgs {
     unsigned long long* mark_len = nullptr;   // MARK: the hook log's length word (mark = the log)
     uint32_t* cbits = nullptr;   // ring folds: vertices claimed straight under the giant root (k_compress)
     uint32_t* hbits = nullptr;   // hooked-root bitmap, used by the kernel only while no giant exists
+    // logging fold (k_fold, one edge per thread, one pass): the touch-log slot of this launch's
+    // wave 0; in the kernel, tlog is the wave's own slot and tcnt its entry count in LDS
+    uint32_t* tlog = nullptr;
+    uint32_t* tcnt = nullptr;
 };
+
+// A wave's first touches (t[k] != kInvalid) appended to its touch-log slot: ballots over the active
+// lanes, the running count in LDS (every lane of a wave calls this at most once per launch).
+template <int N>
+__device__ __forceinline__ void slot_append(uint32_t* __restrict__ slot, uint32_t* tcnt, const uint32_t (&t)[N]) {
+    const uint64_t lt = (1ull << __lane_id()) - 1;
+    uint64_t masks[N];
+    uint32_t total = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        masks[k] = __ballot(t[k] != kInvalid);
+        total += (uint32_t)__popcll(masks[k]);
+    }
+    if (total == 0) return;
+    uint32_t pos = *tcnt;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        if (t[k] != kInvalid) slot[1 + pos + __popcll(masks[k] & lt)] = t[k];
+        pos += (uint32_t)__popcll(masks[k]);
+    }
+    const uint64_t active = __ballot(1);
+    if ((int)__lane_id() == __ffsll((long long)active) - 1) *tcnt = pos;
+}
 
 // ---- LDS hot set (steady state) ----
 // The filter's two gbits lookups per edge miss L2 half the time (an 8 MiB bitmap against a 4 MiB
@@ -531,11 +632,27 @@ __device__ __forceinline__ void union_group(const FoldArgs& f, const uint32_t (&
         pv[k] = ok[k] ? f.parent[v[k]] : 0u;
     }
     uint32_t m[EPT];
+    if (f.tlog) {                                    // logging fold: first touches into the touch log too
+        NewV nl[EPT];
 #pragma unroll
-    for (int k = 0; k < EPT; ++k)
-        m[k] = ok[k] ? union_edge<MARK, STATS>(f.parent, f.sbits, u[k], v[k], pu[k], pv[k], &st,
-                                               f.halve == 1 || (f.halve > 1 && ((u[k] * 0x9E3779B1u) >> 29) == 0),
-                                               f.hbits) : kInvalid;
+        for (int k = 0; k < EPT; ++k)
+            m[k] = ok[k] ? union_edge<MARK, STATS>(f.parent, f.sbits, u[k], v[k], pu[k], pv[k], &st,
+                                                   f.halve == 1 || (f.halve > 1 && ((u[k] * 0x9E3779B1u) >> 29) == 0),
+                                                   f.hbits, &nl[k]) : kInvalid;
+        uint32_t t[2 * EPT];
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            t[2 * k] = nl[k].a;
+            t[2 * k + 1] = nl[k].b;
+        }
+        slot_append<2 * EPT>(f.tlog, f.tcnt, t);
+    } else {
+#pragma unroll
+        for (int k = 0; k < EPT; ++k)
+            m[k] = ok[k] ? union_edge<MARK, STATS>(f.parent, f.sbits, u[k], v[k], pu[k], pv[k], &st,
+                                                   f.halve == 1 || (f.halve > 1 && ((u[k] * 0x9E3779B1u) >> 29) == 0),
+                                                   f.hbits) : kInvalid;
+    }
     if (MARK) log_append<EPT>(f.mark, f.mark_len, m);
 }
 
@@ -680,6 +797,14 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
     // giant forms: ~1 M memory-side atomics per 2^20-edge window)
     if (!filt) f.sbits = nullptr;
     else f.hbits = nullptr;                          // (hooked roots are marked only before a giant)
+    // logging fold (ListCtl): this wave's touch-log slot
+    __shared__ uint32_t s_tcnt[kFoldThreads / 64];
+    const uint32_t wave = threadIdx.x >> 6;
+    if (f.tlog) {
+        f.tlog += ((size_t)blockIdx.x * (kFoldThreads / 64) + wave) * kSlotWords;
+        f.tcnt = &s_tcnt[wave];
+        if ((threadIdx.x & 63) == 0) s_tcnt[wave] = 0;
+    }
     FoldStats st;
     const uint64_t groups = (n + EPT - 1) / EPT;
     if (f.work) {
@@ -698,6 +823,7 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
         for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += stride)
             fold_edges_at<IdT, AOS, MARK, VEC, EPT, STATS>(a, b, f, filt, g, st);
     }
+    if (f.tlog && (threadIdx.x & 63) == 0) f.tlog[0] = s_tcnt[wave];   // every slot's count, 0 included
     if (STATS) {
         atomicAdd(&f.stats[2], (unsigned long long)st.early);
         atomicAdd(&f.stats[3], (unsigned long long)st.hooks);
@@ -1305,13 +1431,27 @@ __global__ __launch_bounds__(1024) void k_pick_giant(const uint32_t* __restrict_
 // itself (a short read-only walk), so a close needs no separate pick launch; workgroup 0 clears
 // the hot set when g is another component than the hot set's owner, and writes g to the output
 // slot as the next close's giant and the root gbits were built for.
+// List-mode arguments of a close (ListCtl above); ctl == nullptr: no lists (sparse handles).
+struct ListClose {
+    uint32_t* ctl = nullptr;
+    const uint2* ngl_in = nullptr;       // NGL read by this close (kListSub sub-lists of ngl_sub entries)
+    uint2* ngl_out = nullptr;            // NGL this close writes
+    uint32_t ngl_sub = 0;
+    const uint32_t* tlog = nullptr;      // the touch log of the interval this close ends (nslots slots)
+    uint32_t nslots = 0;
+    uint32_t c3 = 0, n3 = 0, z3 = 0;     // close number mod 3, + 1, + 2
+    uint32_t unlogged = 0;               // a fold of the interval did not log (or delta emission is on)
+    uint32_t list_next = 0;              // build the NGL: the next interval's folds are expected to log
+};
+
 __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent, uint32_t n,
                                                   uint32_t* __restrict__ gbits, uint32_t* __restrict__ sbits,
                                                   const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                   uint32_t* __restrict__ owner, uint2* __restrict__ hot, int rebuild_seen,
                                                   uint32_t* __restrict__ cbits, uint32_t* __restrict__ dbits,
                                                   const uint32_t* __restrict__ samp_in, uint32_t* __restrict__ samp_out,
-                                                  const uint32_t* __restrict__ hb_in, uint32_t* __restrict__ hb_next) {
+                                                  const uint32_t* __restrict__ hb_in, uint32_t* __restrict__ hb_next,
+                                                  ListClose lc) {
     __shared__ uint32_t s_g, s_inc, s_clear;
     __shared__ PickLds L;
     // no giant known (none picked yet, or a re-pick found none): the mode of the labels the last
@@ -1319,6 +1459,15 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
     // mid-stream, e.g. an Erdos-Renyi stream past average degree 1, gets its filter at the next
     // close instead of at the next host-side pick)
     uint32_t g_samp = kInvalid;
+    // the list-mode control words, loaded before any store of this kernel (independent of the
+    // giant walk below)
+    uint32_t c_lv = 0, c_lo = 0, c_nc = 0;
+    const uint32_t sub = blockIdx.x & (kListSub - 1);
+    if (lc.ctl) {
+        c_lv = lc.ctl[ListCtl::LVALID(lc.c3)];
+        c_lo = lc.ctl[ListCtl::LOVF(lc.c3)];
+        c_nc = lc.ctl[ListCtl::NC(lc.c3) + sub];
+    }
     if (samp_in && in[0] == kInvalid) g_samp = mode_of_samples(samp_in, L);      // uniform
     if (threadIdx.x == 0) {
         const uint32_t g0 = in[0] != kInvalid ? in[0] : g_samp;
@@ -1336,8 +1485,27 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
             out[1] = g;
         }
     }
+    if (threadIdx.x == 0) {
+        // 0: full pass, 1: bitmap-incremental, 2: list (ListCtl: a complete NGL, and every fold of
+        // the interval logged its first touches)
+        if (lc.ctl) {
+            if (s_inc && c_lv && !c_lo && !lc.unlogged) s_inc = 2u;
+            if (blockIdx.x == 0) {
+                lc.ctl[ListCtl::LVALID(lc.n3)] = (s_g != kInvalid && lc.list_next) ? 1u : 0u;
+                lc.ctl[ListCtl::LOVF(lc.z3)] = 0u;
+            }
+        }
+    }
+    if (lc.ctl && blockIdx.x == 0) {
+        for (uint32_t i = threadIdx.x; i < kListSub; i += blockDim.x) lc.ctl[ListCtl::NC(lc.z3) + i] = 0u;
+    }
     __syncthreads();
     const uint32_t g = s_g;
+    // this close writes the next NGL (seen vertices outside the giant) into sub-list blockIdx % kListSub
+    const bool build = lc.ctl && lc.list_next && g != kInvalid;
+    uint2* ngl_o = build ? lc.ngl_out + (size_t)sub * lc.ngl_sub : nullptr;
+    uint32_t* ngl_c = build ? lc.ctl + ListCtl::NC(lc.n3) + sub : nullptr;
+    uint32_t* ngl_v = build ? lc.ctl + ListCtl::LOVF(lc.n3) : nullptr;
     if (s_clear && hot) {                            // workgroup 0 only: the hot set belonged to another component
         for (uint32_t i = threadIdx.x; i < kHotBuckets; i += blockDim.x) hot[i] = make_uint2(0u, 0u);
         if (threadIdx.x == 0) {
@@ -1346,7 +1514,62 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
         }
     }
     const int lane = threadIdx.x & 63;
-    if (s_inc) {                                     // one bitmap word (32 vertices) per thread
+    if (s_inc == 2u) {
+        // list close: the last NGL (sub-list `sub` by the workgroups with that index mod kListSub)
+        // and the interval's touch-log slots (one per wave, strided over the grid's waves). Their
+        // labels may change (a hooked root); every other seen vertex is a giant member labelled g.
+        // Stores: parent by fetch_min (lab < parent[v]), gbits by fetch_or (the items are
+        // scattered: no thread owns their lines). Loops are wave-uniform.
+        // p: v's parent word, or its label at the last close (an NGL entry: parent[v] still
+        // points there unless that root was hooked since)
+        auto visit = [&](uint32_t v, uint32_t p, bool have) {
+            uint32_t lab = kInvalid;
+            if (have) {
+                lab = p;
+                if (p != v) {
+                    const uint32_t gp = parent[p];
+                    if (gp != p) {
+                        lab = find_root_ro(parent, gp);
+                        __hip_atomic_fetch_min(&parent[v], lab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                } else {
+                    const uint32_t q = parent[v];        // a root then: hooked since?
+                    if (q != v) {
+                        lab = find_root_ro(parent, q);
+                        __hip_atomic_fetch_min(&parent[v], lab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+                if (lab == g) __hip_atomic_fetch_or(&gbits[v >> 5], 1u << (v & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            const uint2 m[1] = {make_uint2((have && lab != g) ? v : kInvalid, lab)};
+            if (build) list_append<1>(ngl_o, ngl_c, lc.ngl_sub, ngl_v, m);
+        };
+        const uint32_t wpb = blockDim.x >> 6, wv = threadIdx.x >> 6;
+        const uint32_t part = blockIdx.x / kListSub, nparts = gridDim.x / kListSub;
+        const uint32_t cn = min(c_nc, lc.ngl_sub);
+        const uint2* li = lc.ngl_in + (size_t)sub * lc.ngl_sub;
+        for (uint32_t i0 = part * blockDim.x + wv * 64; i0 < cn; i0 += nparts * blockDim.x) {
+            const uint32_t i = i0 + lane;
+            const uint2 e = i < cn ? li[i] : make_uint2(0u, 0u);
+            visit(e.x, e.y, i < cn);
+        }
+        // slots: the waves of the workgroups past the first kListSub (those have no NGL share
+        // unless the NGL is long); a slot's count and first 64 entries are loaded together
+        const uint32_t w0 = gridDim.x > kListSub ? kListSub : 0u;
+        for (uint32_t sl = (blockIdx.x - w0) * wpb + wv; blockIdx.x >= w0 && sl < lc.nslots; sl += (gridDim.x - w0) * wpb) {
+            const uint32_t* slot = lc.tlog + (size_t)sl * kSlotWords;
+            const uint32_t c0 = slot[0];
+            const uint32_t e0 = slot[1 + lane];
+            const uint32_t sc = min(c0, 2u * 64u);
+            const uint32_t p0 = (uint32_t)lane < sc ? parent[e0] : 0u;
+            visit(e0, p0, (uint32_t)lane < sc);
+            if (sc > 64) {
+                const uint32_t e1 = slot[65 + lane];
+                const bool h1 = 64u + lane < sc;
+                visit(e1, h1 ? parent[e1] : 0u, h1);
+            }
+        }
+    } else if (s_inc) {                              // one bitmap word (32 vertices) per thread
         const uint32_t nwords = (uint32_t)((n + 31) >> 5);
         for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += gridDim.x * blockDim.x) {
             uint32_t cand = sbits[w] & ~gbits[w];
@@ -1373,8 +1596,10 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                     const uint32_t v = (w << 5) + vb[k];
                     gp[k] = (k < m && p[k] != v) ? parent[p[k]] : p[k];
                 }
+                uint2 ng[8];
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
+                    ng[k] = make_uint2(kInvalid, 0u);
                     if (k >= m) continue;
                     const uint32_t v = (w << 5) + vb[k];
                     uint32_t lab = p[k];
@@ -1383,7 +1608,9 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                         parent[v] = lab;
                     }
                     add |= (lab == g) ? (1u << vb[k]) : 0u;
+                    if (lab != g) ng[k] = make_uint2(v, lab);
                 }
+                if (build) list_append<8>(ngl_o, ngl_c, lc.ngl_sub, ngl_v, ng);
             }
             if (add) gbits[w] |= add;
         }
@@ -1422,6 +1649,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
 #pragma unroll
             for (int k = 0; k < 4; ++k) gp[k] = need[k] ? parent[p[k]] : p[k];
             uint32_t nib = 0, seen = 0;
+            uint2 ng[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const uint32_t v = base + k;
@@ -1432,8 +1660,10 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                 }
                 nib |= (lab == g && lab != kInvalid) ? (1u << k) : 0u;
                 seen |= (p[k] != kInvalid) ? (1u << k) : 0u;
+                ng[k] = make_uint2((p[k] != kInvalid && lab != g) ? v : kInvalid, lab);
                 if (samp_out && v < n && is_sample(v, sb)) samp_out[v >> sb] = lab;   // kInvalid: unseen
             }
+            if (build) list_append<4>(ngl_o, ngl_c, lc.ngl_sub, ngl_v, ng);
             uint32_t word = nib << (4 * (lane & 7));
             word |= __shfl_xor(word, 1, 64);
             word |= __shfl_xor(word, 2, 64);
