@@ -69,6 +69,7 @@ struct gs_cc {
     uint32_t* cbits = nullptr;           // ring folds: first touches claimed under the giant root
     uint32_t* hkbits[2] = {nullptr, nullptr}; // roots hooked before any giant exists, by close parity
     bool hkbits_ok = true;               // every fold since the last close marked its hooked roots
+    bool hkg_ok = true;                  // ... with a giant too (k_fold hb_giant; the ring does not)
     uint32_t* dbits = nullptr;           // delta emission: vertices a close may have relabelled since the last delta
     // list-mode closes (cc_kernels.hpp ListCtl): control words, the NGL (seen vertices outside the
     // giant) and the touch log, each double-buffered by close parity
@@ -300,6 +301,7 @@ struct DebugEnv {
     int small_ept = kSmallEpt;                      // GSGPU_SMALL_EPT: ...take this many edges per thread
     uint64_t young_first_min = kYoungFirstMinWg;    // GSGPU_YOUNG_FIRST_MIN: workgroup floor of the first young launch
     bool list_close = true;                         // GSGPU_LIST_CLOSE=0: no list-mode closes (A/B)
+    bool hb_giant = true;                           // GSGPU_HB_GIANT=0: k_fold marks hooked roots only before a giant (A/B)
     DebugEnv() {
         const char* e = getenv("GSGPU_FOLD_STATS");
         fold_stats = e && atoi(e) != 0;
@@ -318,6 +320,8 @@ struct DebugEnv {
         if (e && *e) small_ept = atoi(e) == 1 ? 1 : (atoi(e) == 2 ? 2 : 4);
         e = getenv("GSGPU_LIST_CLOSE");
         if (e && *e) list_close = atoi(e) != 0;
+        e = getenv("GSGPU_HB_GIANT");
+        if (e && *e) hb_giant = atoi(e) != 0;
 
     }
 };
@@ -360,8 +364,16 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
     // hooked roots marked (while no giant exists, k_fold) by mature SoA launches only: in the young
     // forest the marks would cost an atomic per hook for a close whose grandparent reads hit L2
     // anyway (an RMAT window 1's non-roots hang under a few hub roots)
-    if (!young && !AOS && h->hkbits[0]) f.hbits = h->hkbits[h->closes & 1];
-    else h->hkbits_ok = false;
+    if (!young && !AOS && h->hkbits[0]) {
+        f.hbits = h->hkbits[h->closes & 1];
+        // with a giant too where the close's grandparent reads miss L2 (ids >= 2^22): config 4's
+        // closes 90.7 -> 85.2 us per window; at config 2 (2^20 ids, 8 us closes) the marks cost more
+        // than they save (profiles/r04_hbg_ab.txt)
+        f.hb_giant = (dbg().hb_giant && h->cap >= (1u << 22)) ? 1u : 0u;
+        if (!f.hb_giant) h->hkg_ok = false;
+    } else {
+        h->hkbits_ok = false;
+    }
     // a big young launch (>= capacity/16 edges, i.e. window 1 of the headline) leaves the seen
     // bitmap to the close that follows it — a full pass in any case while the forest is this
     // young — and saves one device-scope atomic per new vertex (window 1: ~6.4M)
@@ -457,6 +469,7 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     f.cbits = kUseCbits ? h->cbits : nullptr;
     if (h->hkbits[0]) f.hbits = h->hkbits[h->closes & 1];
     else h->hkbits_ok = false;
+    h->hkg_ok = false;                   // (the ring fold marks hooked roots only before a giant)
     h->ilist_ok = false;
     KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_RING : h->fold_timer, n);
     const bool st = h->dstats != nullptr;
@@ -709,9 +722,11 @@ int compress_impl(gs_cc_t* h) {
         uint32_t* hb_next = h->hkbits[0] ? h->hkbits[h->closes & 1] : nullptr;
         klaunch(k_compress, dim3(grid), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
                 h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot,
-                (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits, samp_in, samp_out, hb_in, hb_next, lc);
+                (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits, samp_in, samp_out, hb_in, hb_next,
+                (uint32_t)(hb_in && h->hkg_ok), lc);
         h->sbits_stale = false;
         h->hkbits_ok = true;
+        h->hkg_ok = true;
     }
     GS_HIP(hipGetLastError());
     h->compressed = true;
@@ -1101,6 +1116,7 @@ int gs_cc_reset(gs_cc_t* h) {
     GS_HIP(hipMemsetAsync(h->cbits, 0, mark_bytes(h->cap), h->stream));
     for (auto* hb : h->hkbits) if (hb) GS_HIP(hipMemsetAsync(hb, 0, mark_bytes(h->cap), h->stream));
     h->hkbits_ok = true;
+    h->hkg_ok = true;
     if (h->lctl) GS_HIP(hipMemsetAsync(h->lctl, 0, ListCtl::kWords * sizeof(uint32_t), h->stream));
     h->ilist_ok = true;
     h->ilist_folds = 0;

@@ -296,7 +296,8 @@ struct FoldArgs {
     unsigned long long* work = nullptr;   // k_fold: dynamic chunk counter (young forest), or null
     unsigned long long* mark_len = nullptr;   // MARK: the hook log's length word (mark = the log)
     uint32_t* cbits = nullptr;   // ring folds: vertices claimed straight under the giant root (k_compress)
-    uint32_t* hbits = nullptr;   // hooked-root bitmap, used by the kernel only while no giant exists
+    uint32_t* hbits = nullptr;   // hooked-root bitmap: marked while no giant exists, or always if hb_giant
+    uint32_t hb_giant = 0;       // k_fold: mark hooked roots with a giant too (the next close tests the marks)
     // logging fold (k_fold, one edge per thread, one pass): the touch-log slot of this launch's
     // wave 0; in the kernel, tlog is the wave's own slot and tcnt its entry count in LDS
     uint32_t* tlog = nullptr;
@@ -796,7 +797,7 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
     // bitmap from parent[] — first touches skip their seen-bit atomic (Erdos-Renyi windows before the
     // giant forms: ~1 M memory-side atomics per 2^20-edge window)
     if (!filt) f.sbits = nullptr;
-    else f.hbits = nullptr;                          // (hooked roots are marked only before a giant)
+    else if (!f.hb_giant) f.hbits = nullptr;         // (hooked roots marked before a giant, or if asked)
     // logging fold (ListCtl): this wave's touch-log slot
     __shared__ uint32_t s_tcnt[kFoldThreads / 64];
     const uint32_t wave = threadIdx.x >> 6;
@@ -1451,7 +1452,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                                                   uint32_t* __restrict__ cbits, uint32_t* __restrict__ dbits,
                                                   const uint32_t* __restrict__ samp_in, uint32_t* __restrict__ samp_out,
                                                   const uint32_t* __restrict__ hb_in, uint32_t* __restrict__ hb_next,
-                                                  ListClose lc) {
+                                                  uint32_t hb_giant, ListClose lc) {
     __shared__ uint32_t s_g, s_inc, s_clear;
     __shared__ PickLds L;
     // no giant known (none picked yet, or a re-pick found none): the mode of the labels the last
@@ -1571,8 +1572,12 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
         }
     } else if (s_inc) {                              // one bitmap word (32 vertices) per thread
         const uint32_t nwords = (uint32_t)((n + 31) >> 5);
+        // hooked-root marks of every fold since the last close (hb_giant): a straggler's parent that
+        // is unmarked is still a root, no grandparent read (as in the full pass below)
+        const bool usehb = hb_in != nullptr && hb_giant;
         for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += gridDim.x * blockDim.x) {
             uint32_t cand = sbits[w] & ~gbits[w];
+            if (hb_next) hb_next[w] = 0u;            // the next window's marks start empty
             // vertices claimed under the giant root since the last close: already labelled g
             uint32_t add = cbits ? cbits[w] : 0u;
             if (add) cbits[w] = 0u;
@@ -1591,11 +1596,18 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                 }
 #pragma unroll
                 for (int k = 0; k < 8; ++k) p[k] = (k < m) ? parent[(w << 5) + vb[k]] : 0u;
+                bool need[8];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const uint32_t v = (w << 5) + vb[k];
-                    gp[k] = (k < m && p[k] != v) ? parent[p[k]] : p[k];
+                for (int k = 0; k < 8; ++k) need[k] = k < m && p[k] != (w << 5) + vb[k];
+                if (usehb) {
+                    uint32_t hw[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) hw[k] = need[k] ? hb_in[p[k] >> 5] : 0u;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) need[k] = need[k] && ((hw[k] >> (p[k] & 31)) & 1u);
                 }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) gp[k] = need[k] ? parent[p[k]] : p[k];
                 uint2 ng[8];
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
@@ -1624,7 +1636,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
         // before the giant forms) becomes a bit test in a V/8-byte bitmap that stays in L2. Every
         // parent word written since the last close is a root at the time of writing (a hook's lo, a
         // claim's gR, a halving's grandparent), so "unmarked" is exact.
-        const bool usehb = hb_in != nullptr && in[1] == kInvalid;
+        const bool usehb = hb_in != nullptr && (in[1] == kInvalid || hb_giant);
         for (uint64_t blk = (uint64_t)blockIdx.x * 1024; blk < n; blk += (uint64_t)gridDim.x * 1024) {
             const uint32_t base = (uint32_t)blk + threadIdx.x * 4;
             uint32_t p[4];
