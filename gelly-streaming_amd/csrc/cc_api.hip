@@ -80,6 +80,7 @@ struct gs_cc {
     bool ilist_ok = true;                // every fold since the last close logged its first touches
     uint32_t ilist_folds = 0;            // logged folds since the last close
     uint32_t ilist_slots = 0;            // touch-log slots they took (one per wave)
+    bool list_prev = false;              // the last close built an NGL (list_next)
     uint32_t* elab = nullptr;            // delta emission: the labels last emitted (kInvalid: never)
     uint32_t* derr = nullptr;            // derr[0] deferred device error flags; derr[1..5] giant state
     uint32_t* psamp = nullptr;           // 2 x kPickSamples labels a full-pass close recorded (k_compress)
@@ -720,10 +721,21 @@ int compress_impl(gs_cc_t* h) {
         // (the close about to run is number closes - 1 now: it reads the marks of its parity)
         const uint32_t* hb_in = (h->hkbits[0] && h->hkbits_ok) ? h->hkbits[(h->closes - 1) & 1] : nullptr;
         uint32_t* hb_next = h->hkbits[0] ? h->hkbits[h->closes & 1] : nullptr;
-        klaunch(k_compress, dim3(grid), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
-                h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot,
-                (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits, samp_in, samp_out, hb_in, hb_next,
-                (uint32_t)(hb_in && h->hkg_ok), lc);
+        // the list variant when the last close built an NGL (this one may be a list close) or this
+        // one builds one
+        const bool lists = lc.ctl && (h->list_prev || lc.list_next);
+        if (!lists) lc.list_next = 0;        // (the variant without lists builds no NGL: LVALID 0)
+        h->list_prev = lc.list_next != 0;
+        if (lists)
+            klaunch(k_compress<true>, dim3(grid), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
+                    h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot,
+                    (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits, samp_in, samp_out, hb_in, hb_next,
+                    (uint32_t)(hb_in && h->hkg_ok), lc);
+        else
+            klaunch(k_compress<false>, dim3(grid), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
+                    h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot,
+                    (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits, samp_in, samp_out, hb_in, hb_next,
+                    (uint32_t)(hb_in && h->hkg_ok), lc);
         h->sbits_stale = false;
         h->hkbits_ok = true;
         h->hkg_ok = true;
@@ -981,7 +993,7 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
         (void)hipGetLastError();
         return bail(fail(GS_ERR_NOMEM, "hooked-root bitmaps allocation failed"));
     }
-    if (!sparse) {
+    if (!sparse && !getenv("GSGPU_NO_LISTS")) {
         // NGL: up to capacity/64 vertices outside the giant (more: bitmap closes); touch log:
         // kTlogSlots slots per interval
         h->ngl_sub = (uint32_t)std::min<uint64_t>(4096, std::max<uint64_t>(64, (uint64_t)h->cap / 64 / kListSub));
@@ -1117,6 +1129,7 @@ int gs_cc_reset(gs_cc_t* h) {
     for (auto* hb : h->hkbits) if (hb) GS_HIP(hipMemsetAsync(hb, 0, mark_bytes(h->cap), h->stream));
     h->hkbits_ok = true;
     h->hkg_ok = true;
+    h->list_prev = false;
     if (h->lctl) GS_HIP(hipMemsetAsync(h->lctl, 0, ListCtl::kWords * sizeof(uint32_t), h->stream));
     h->ilist_ok = true;
     h->ilist_folds = 0;

@@ -1445,6 +1445,11 @@ struct ListClose {
     uint32_t list_next = 0;              // build the NGL: the next interval's folds are expected to log
 };
 
+// LISTS: list closes and NGL appends (ListCtl) compiled in; the host launches the variant without
+// them when neither this close nor the last one deals with lists (the ring fold's windows: the
+// extra code cost one wave per SIMD of occupancy and ~50 % on the headline's full passes). Both
+// variants keep the control words (LVALID of the next interval, the zeroing).
+template <bool LISTS>
 __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent, uint32_t n,
                                                   uint32_t* __restrict__ gbits, uint32_t* __restrict__ sbits,
                                                   const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
@@ -1490,7 +1495,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
         // 0: full pass, 1: bitmap-incremental, 2: list (ListCtl: a complete NGL, and every fold of
         // the interval logged its first touches)
         if (lc.ctl) {
-            if (s_inc && c_lv && !c_lo && !lc.unlogged) s_inc = 2u;
+            if (LISTS && s_inc && c_lv && !c_lo && !lc.unlogged) s_inc = 2u;
             if (blockIdx.x == 0) {
                 lc.ctl[ListCtl::LVALID(lc.n3)] = (s_g != kInvalid && lc.list_next) ? 1u : 0u;
                 lc.ctl[ListCtl::LOVF(lc.z3)] = 0u;
@@ -1503,7 +1508,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
     __syncthreads();
     const uint32_t g = s_g;
     // this close writes the next NGL (seen vertices outside the giant) into sub-list blockIdx % kListSub
-    const bool build = lc.ctl && lc.list_next && g != kInvalid;
+    const bool build = LISTS && lc.ctl && lc.list_next && g != kInvalid;
     uint2* ngl_o = build ? lc.ngl_out + (size_t)sub * lc.ngl_sub : nullptr;
     uint32_t* ngl_c = build ? lc.ctl + ListCtl::NC(lc.n3) + sub : nullptr;
     uint32_t* ngl_v = build ? lc.ctl + ListCtl::LOVF(lc.n3) : nullptr;
@@ -1515,7 +1520,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
         }
     }
     const int lane = threadIdx.x & 63;
-    if (s_inc == 2u) {
+    if (LISTS && s_inc == 2u) {
         // list close: the last NGL (sub-list `sub` by the workgroups with that index mod kListSub)
         // and the interval's touch-log slots (one per wave, strided over the grid's waves). Their
         // labels may change (a hooked root); every other seen vertex is a giant member labelled g.
@@ -1577,7 +1582,9 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
         const bool usehb = hb_in != nullptr && hb_giant;
         for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += gridDim.x * blockDim.x) {
             uint32_t cand = sbits[w] & ~gbits[w];
-            if (hb_next) hb_next[w] = 0u;            // the next window's marks start empty
+            // the next window's marks start empty (only where they are read: stale marks would only
+            // cost grandparent reads, and zeroing is an 8 MiB write per close at 2^26 ids)
+            if (hb_giant && hb_next) hb_next[w] = 0u;
             // vertices claimed under the giant root since the last close: already labelled g
             uint32_t add = cbits ? cbits[w] : 0u;
             if (add) cbits[w] = 0u;
@@ -1622,7 +1629,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                     add |= (lab == g) ? (1u << vb[k]) : 0u;
                     if (lab != g) ng[k] = make_uint2(v, lab);
                 }
-                if (build) list_append<8>(ngl_o, ngl_c, lc.ngl_sub, ngl_v, ng);
+                if (LISTS && build) list_append<8>(ngl_o, ngl_c, lc.ngl_sub, ngl_v, ng);
             }
             if (add) gbits[w] |= add;
         }
@@ -1675,7 +1682,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                 ng[k] = make_uint2((p[k] != kInvalid && lab != g) ? v : kInvalid, lab);
                 if (samp_out && v < n && is_sample(v, sb)) samp_out[v >> sb] = lab;   // kInvalid: unseen
             }
-            if (build) list_append<4>(ngl_o, ngl_c, lc.ngl_sub, ngl_v, ng);
+            if (LISTS && build) list_append<4>(ngl_o, ngl_c, lc.ngl_sub, ngl_v, ng);
             uint32_t word = nib << (4 * (lane & 7));
             word |= __shfl_xor(word, 1, 64);
             word |= __shfl_xor(word, 2, 64);
