@@ -69,7 +69,6 @@ struct gs_cc {
     uint32_t* cbits = nullptr;           // ring folds: first touches claimed under the giant root
     uint32_t* hkbits[2] = {nullptr, nullptr}; // roots hooked before any giant exists, by close parity
     bool hkbits_ok = true;               // every fold since the last close marked its hooked roots
-    bool hkg_ok = true;                  // ... with a giant too (k_fold hb_giant; the ring does not)
     uint32_t* dbits = nullptr;           // delta emission: vertices a close may have relabelled since the last delta
     // list-mode closes (cc_kernels.hpp ListCtl): control words, the NGL (seen vertices outside the
     // giant) and the touch log, each double-buffered by close parity
@@ -81,6 +80,7 @@ struct gs_cc {
     uint32_t ilist_folds = 0;            // logged folds since the last close
     uint32_t ilist_slots = 0;            // touch-log slots they took (one per wave)
     bool list_prev = false;              // the last close built an NGL (list_next)
+    bool list_kernel = false;            // the last close ran k_compress_list (its control words are current)
     uint32_t* elab = nullptr;            // delta emission: the labels last emitted (kInvalid: never)
     uint32_t* derr = nullptr;            // derr[0] deferred device error flags; derr[1..5] giant state
     uint32_t* psamp = nullptr;           // 2 x kPickSamples labels a full-pass close recorded (k_compress)
@@ -302,7 +302,6 @@ struct DebugEnv {
     int small_ept = kSmallEpt;                      // GSGPU_SMALL_EPT: ...take this many edges per thread
     uint64_t young_first_min = kYoungFirstMinWg;    // GSGPU_YOUNG_FIRST_MIN: workgroup floor of the first young launch
     bool list_close = true;                         // GSGPU_LIST_CLOSE=0: no list-mode closes (A/B)
-    bool hb_giant = true;                           // GSGPU_HB_GIANT=0: k_fold marks hooked roots only before a giant (A/B)
     DebugEnv() {
         const char* e = getenv("GSGPU_FOLD_STATS");
         fold_stats = e && atoi(e) != 0;
@@ -321,8 +320,6 @@ struct DebugEnv {
         if (e && *e) small_ept = atoi(e) == 1 ? 1 : (atoi(e) == 2 ? 2 : 4);
         e = getenv("GSGPU_LIST_CLOSE");
         if (e && *e) list_close = atoi(e) != 0;
-        e = getenv("GSGPU_HB_GIANT");
-        if (e && *e) hb_giant = atoi(e) != 0;
 
     }
 };
@@ -365,16 +362,8 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
     // hooked roots marked (while no giant exists, k_fold) by mature SoA launches only: in the young
     // forest the marks would cost an atomic per hook for a close whose grandparent reads hit L2
     // anyway (an RMAT window 1's non-roots hang under a few hub roots)
-    if (!young && !AOS && h->hkbits[0]) {
-        f.hbits = h->hkbits[h->closes & 1];
-        // with a giant too where the close's grandparent reads miss L2 (ids >= 2^22): config 4's
-        // closes 90.7 -> 85.2 us per window; at config 2 (2^20 ids, 8 us closes) the marks cost more
-        // than they save (profiles/r04_hbg_ab.txt)
-        f.hb_giant = (dbg().hb_giant && h->cap >= (1u << 22)) ? 1u : 0u;
-        if (!f.hb_giant) h->hkg_ok = false;
-    } else {
-        h->hkbits_ok = false;
-    }
+    if (!young && !AOS && h->hkbits[0]) f.hbits = h->hkbits[h->closes & 1];
+    else h->hkbits_ok = false;
     // a big young launch (>= capacity/16 edges, i.e. window 1 of the headline) leaves the seen
     // bitmap to the close that follows it — a full pass in any case while the forest is this
     // young — and saves one device-scope atomic per new vertex (window 1: ~6.4M)
@@ -470,7 +459,6 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     f.cbits = kUseCbits ? h->cbits : nullptr;
     if (h->hkbits[0]) f.hbits = h->hkbits[h->closes & 1];
     else h->hkbits_ok = false;
-    h->hkg_ok = false;                   // (the ring fold marks hooked roots only before a giant)
     h->ilist_ok = false;
     KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_RING : h->fold_timer, n);
     const bool st = h->dstats != nullptr;
@@ -721,24 +709,24 @@ int compress_impl(gs_cc_t* h) {
         // (the close about to run is number closes - 1 now: it reads the marks of its parity)
         const uint32_t* hb_in = (h->hkbits[0] && h->hkbits_ok) ? h->hkbits[(h->closes - 1) & 1] : nullptr;
         uint32_t* hb_next = h->hkbits[0] ? h->hkbits[h->closes & 1] : nullptr;
-        // the list variant when the last close built an NGL (this one may be a list close) or this
-        // one builds one
+        // k_compress_list while lists are in use: the last close built an NGL (this one may be a list
+        // close) or this one builds one. Its control words are stale after plain closes: cleared
+        // (LVALID 0, counts 0) when it starts again
         const bool lists = lc.ctl && (h->list_prev || lc.list_next);
-        if (!lists) lc.list_next = 0;        // (the variant without lists builds no NGL: LVALID 0)
         h->list_prev = lc.list_next != 0;
-        if (lists)
-            klaunch(k_compress<true>, dim3(grid), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
+        if (lists) {
+            if (!h->list_kernel) GS_HIP(hipMemsetAsync(h->lctl, 0, ListCtl::kWords * sizeof(uint32_t), h->stream));
+            klaunch(k_compress_list, dim3(grid), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
                     h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot,
-                    (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits, samp_in, samp_out, hb_in, hb_next,
-                    (uint32_t)(hb_in && h->hkg_ok), lc);
-        else
-            klaunch(k_compress<false>, dim3(grid), dim3(256), h->stream, pick ? nullptr : t.start(), t.stop(),
-                    h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5, h->hot,
-                    (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits, samp_in, samp_out, hb_in, hb_next,
-                    (uint32_t)(hb_in && h->hkg_ok), lc);
+                    (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits, samp_in, samp_out, hb_in, hb_next, lc);
+        } else {
+            klaunch(k_compress, dim3(grid_for(h->cap, 1024, kCompressGrid)), dim3(256), h->stream, pick ? nullptr : t.start(),
+                    t.stop(), h->parent, h->cap, h->gbits, h->sbits, (const uint32_t*)in, giant_state(h), h->derr + 5,
+                    h->hot, (int)h->sbits_stale, kUseCbits ? h->cbits : nullptr, h->dbits, samp_in, samp_out, hb_in, hb_next);
+        }
+        h->list_kernel = lists;
         h->sbits_stale = false;
         h->hkbits_ok = true;
-        h->hkg_ok = true;
     }
     GS_HIP(hipGetLastError());
     h->compressed = true;
@@ -993,7 +981,7 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
         (void)hipGetLastError();
         return bail(fail(GS_ERR_NOMEM, "hooked-root bitmaps allocation failed"));
     }
-    if (!sparse && !getenv("GSGPU_NO_LISTS")) {
+    if (!sparse) {
         // NGL: up to capacity/64 vertices outside the giant (more: bitmap closes); touch log:
         // kTlogSlots slots per interval
         h->ngl_sub = (uint32_t)std::min<uint64_t>(4096, std::max<uint64_t>(64, (uint64_t)h->cap / 64 / kListSub));
@@ -1128,8 +1116,8 @@ int gs_cc_reset(gs_cc_t* h) {
     GS_HIP(hipMemsetAsync(h->cbits, 0, mark_bytes(h->cap), h->stream));
     for (auto* hb : h->hkbits) if (hb) GS_HIP(hipMemsetAsync(hb, 0, mark_bytes(h->cap), h->stream));
     h->hkbits_ok = true;
-    h->hkg_ok = true;
     h->list_prev = false;
+    h->list_kernel = false;
     if (h->lctl) GS_HIP(hipMemsetAsync(h->lctl, 0, ListCtl::kWords * sizeof(uint32_t), h->stream));
     h->ilist_ok = true;
     h->ilist_folds = 0;

@@ -296,8 +296,7 @@ struct FoldArgs {
     unsigned long long* work = nullptr;   // k_fold: dynamic chunk counter (young forest), or null
     unsigned long long* mark_len = nullptr;   // MARK: the hook log's length word (mark = the log)
     uint32_t* cbits = nullptr;   // ring folds: vertices claimed straight under the giant root (k_compress)
-    uint32_t* hbits = nullptr;   // hooked-root bitmap: marked while no giant exists, or always if hb_giant
-    uint32_t hb_giant = 0;       // k_fold: mark hooked roots with a giant too (the next close tests the marks)
+    uint32_t* hbits = nullptr;   // hooked-root bitmap, used by the kernel only while no giant exists
     // logging fold (k_fold, one edge per thread, one pass): the touch-log slot of this launch's
     // wave 0; in the kernel, tlog is the wave's own slot and tcnt its entry count in LDS
     uint32_t* tlog = nullptr;
@@ -797,7 +796,7 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
     // bitmap from parent[] — first touches skip their seen-bit atomic (Erdos-Renyi windows before the
     // giant forms: ~1 M memory-side atomics per 2^20-edge window)
     if (!filt) f.sbits = nullptr;
-    else if (!f.hb_giant) f.hbits = nullptr;         // (hooked roots marked before a giant, or if asked)
+    else f.hbits = nullptr;                          // (hooked roots are marked only before a giant)
     // logging fold (ListCtl): this wave's touch-log slot
     __shared__ uint32_t s_tcnt[kFoldThreads / 64];
     const uint32_t wave = threadIdx.x >> 6;
@@ -1445,19 +1444,170 @@ struct ListClose {
     uint32_t list_next = 0;              // build the NGL: the next interval's folds are expected to log
 };
 
-// LISTS: list closes and NGL appends (ListCtl) compiled in; the host launches the variant without
-// them when neither this close nor the last one deals with lists (the ring fold's windows: the
-// extra code cost one wave per SIMD of occupancy and ~50 % on the headline's full passes). Both
-// variants keep the control words (LVALID of the next interval, the zeroing).
-template <bool LISTS>
 __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent, uint32_t n,
                                                   uint32_t* __restrict__ gbits, uint32_t* __restrict__ sbits,
                                                   const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                   uint32_t* __restrict__ owner, uint2* __restrict__ hot, int rebuild_seen,
                                                   uint32_t* __restrict__ cbits, uint32_t* __restrict__ dbits,
                                                   const uint32_t* __restrict__ samp_in, uint32_t* __restrict__ samp_out,
+                                                  const uint32_t* __restrict__ hb_in, uint32_t* __restrict__ hb_next) {
+    __shared__ uint32_t s_g, s_inc, s_clear;
+    __shared__ PickLds L;
+    // no giant known (none picked yet, or a re-pick found none): the mode of the labels the last
+    // full pass recorded at the sample positions, the same in every workgroup (a giant that forms
+    // mid-stream, e.g. an Erdos-Renyi stream past average degree 1, gets its filter at the next
+    // close instead of at the next host-side pick)
+    uint32_t g_samp = kInvalid;
+    if (samp_in && in[0] == kInvalid) g_samp = mode_of_samples(samp_in, L);      // uniform
+    if (threadIdx.x == 0) {
+        const uint32_t g0 = in[0] != kInvalid ? in[0] : g_samp;
+        const uint32_t g = (g0 == kInvalid) ? kInvalid : find_root_ro(parent, g0);
+        s_g = g;
+        s_inc = (g != kInvalid && g == in[1] && !rebuild_seen) ? 1u : 0u;
+        s_clear = 0;
+        if (blockIdx.x == 0) {
+            if (g != kInvalid) {
+                const uint32_t o = *owner;
+                s_clear = (o == kInvalid || find_root_ro(parent, o) != g) ? 1u : 0u;
+                *owner = g;
+            }
+            out[0] = g;
+            out[1] = g;
+        }
+    }
+    __syncthreads();
+    const uint32_t g = s_g;
+    if (s_clear && hot) {                            // workgroup 0 only: the hot set belonged to another component
+        for (uint32_t i = threadIdx.x; i < kHotBuckets; i += blockDim.x) hot[i] = make_uint2(0u, 0u);
+        if (threadIdx.x == 0) {
+            owner[1] = kHotAdmitLaunches;            // refill: the admission budget
+            owner[2] = 0;                            // the warm set belonged to it too (rebuilt later)
+        }
+    }
+    const int lane = threadIdx.x & 63;
+    if (s_inc) {                                     // one bitmap word (32 vertices) per thread
+        const uint32_t nwords = (uint32_t)((n + 31) >> 5);
+        for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += gridDim.x * blockDim.x) {
+            uint32_t cand = sbits[w] & ~gbits[w];
+            // vertices claimed under the giant root since the last close: already labelled g
+            uint32_t add = cbits ? cbits[w] : 0u;
+            if (add) cbits[w] = 0u;
+            // delta emission: every vertex this close may relabel (or that is new) is dirty
+            if (dbits && (cand | add)) dbits[w] |= cand | add;
+            // up to 8 stragglers at a time, their parent and grandparent reads issued back to
+            // back (one at a time: a young Erdos-Renyi window's close, ~32 stragglers per word,
+            // spent 121 us per 2^24 ids in dependent loads)
+            while (cand) {
+                uint32_t vb[8], p[8], gp[8];
+                int m = 0;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    vb[k] = cand ? (uint32_t)(__ffs(cand) - 1) : 32u;
+                    if (cand) { cand &= cand - 1; ++m; }
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) p[k] = (k < m) ? parent[(w << 5) + vb[k]] : 0u;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t v = (w << 5) + vb[k];
+                    gp[k] = (k < m && p[k] != v) ? parent[p[k]] : p[k];
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    if (k >= m) continue;
+                    const uint32_t v = (w << 5) + vb[k];
+                    uint32_t lab = p[k];
+                    if (p[k] != v && gp[k] != p[k]) {
+                        lab = find_root_ro(parent, gp[k]);
+                        parent[v] = lab;
+                    }
+                    add |= (lab == g) ? (1u << vb[k]) : 0u;
+                }
+            }
+            if (add) gbits[w] |= add;
+        }
+    } else {
+        const uint32_t sb = samp_shift(n);
+        // Hooked-root bitmap (hb_in, non-null only when every fold since the last close marked the
+        // roots it hooked, i.e. none had a giant to filter with, so this close cannot be incremental):
+        // a vertex's parent p that was a root at the last close (every seen vertex pointed to one)
+        // and is unmarked is still a root, so its grandparent read (a random 4-B read of parent[]
+        // per seen vertex: HBM / Infinity-Cache bound, ~170 us per close of an Erdos-Renyi window
+        // before the giant forms) becomes a bit test in a V/8-byte bitmap that stays in L2. Every
+        // parent word written since the last close is a root at the time of writing (a hook's lo, a
+        // claim's gR, a halving's grandparent), so "unmarked" is exact.
+        const bool usehb = hb_in != nullptr && in[1] == kInvalid;
+        for (uint64_t blk = (uint64_t)blockIdx.x * 1024; blk < n; blk += (uint64_t)gridDim.x * 1024) {
+            const uint32_t base = (uint32_t)blk + threadIdx.x * 4;
+            uint32_t p[4];
+            if ((uint64_t)base + 4 <= n) {
+                const uint4 q = *reinterpret_cast<const uint4*>(parent + base);
+                p[0] = q.x; p[1] = q.y; p[2] = q.z; p[3] = q.w;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) p[k] = ((uint64_t)base + k < n) ? parent[base + k] : kInvalid;
+            }
+            bool need[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) need[k] = p[k] != kInvalid && p[k] != base + k;
+            if (usehb) {
+                uint32_t hw[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) hw[k] = need[k] ? hb_in[p[k] >> 5] : 0u;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) need[k] = need[k] && ((hw[k] >> (p[k] & 31)) & 1u);
+            }
+            uint32_t gp[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) gp[k] = need[k] ? parent[p[k]] : p[k];
+            uint32_t nib = 0, seen = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t v = base + k;
+                uint32_t lab = p[k];
+                if (p[k] != kInvalid && p[k] != v && gp[k] != p[k]) {   // depth >= 2: walk, store the root
+                    lab = find_root_ro(parent, gp[k]);
+                    parent[v] = lab;
+                }
+                nib |= (lab == g && lab != kInvalid) ? (1u << k) : 0u;
+                seen |= (p[k] != kInvalid) ? (1u << k) : 0u;
+                if (samp_out && v < n && is_sample(v, sb)) samp_out[v >> sb] = lab;   // kInvalid: unseen
+            }
+            uint32_t word = nib << (4 * (lane & 7));
+            word |= __shfl_xor(word, 1, 64);
+            word |= __shfl_xor(word, 2, 64);
+            word |= __shfl_xor(word, 4, 64);
+            if ((lane & 7) == 0 && base < n) gbits[base >> 5] = word;
+            {                                        // the seen bitmap, exact again after every full pass
+                uint32_t sw = seen << (4 * (lane & 7));
+                sw |= __shfl_xor(sw, 1, 64);
+                sw |= __shfl_xor(sw, 2, 64);
+                sw |= __shfl_xor(sw, 4, 64);
+                if ((lane & 7) == 0 && base < n) {
+                    sbits[base >> 5] = sw;
+                    if (cbits) cbits[base >> 5] = 0u;    // this pass labelled the claimed vertices too
+                    if (dbits) dbits[base >> 5] = sw;    // a full pass may relabel any seen vertex
+                    if (hb_next) hb_next[base >> 5] = 0u;   // the next window's hooked-root marks start empty
+                }
+            }
+        }
+    }
+}
+
+
+// k_compress_list: k_compress plus the list machinery (ListCtl): the list close, and NGL appends in
+// the full and bitmap passes. A separate kernel: compiled into k_compress, that code cost one wave
+// per SIMD of occupancy and slowed the headline's closes by ~40 % even where no list was used
+// (profiles/r04_bisect). The host launches it only while lists are in use (the last close built an
+// NGL or this one builds one), and clears the control words when it starts using it again.
+__global__ __launch_bounds__(256) void k_compress_list(uint32_t* __restrict__ parent, uint32_t n,
+                                                  uint32_t* __restrict__ gbits, uint32_t* __restrict__ sbits,
+                                                  const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                  uint32_t* __restrict__ owner, uint2* __restrict__ hot, int rebuild_seen,
+                                                  uint32_t* __restrict__ cbits, uint32_t* __restrict__ dbits,
+                                                  const uint32_t* __restrict__ samp_in, uint32_t* __restrict__ samp_out,
                                                   const uint32_t* __restrict__ hb_in, uint32_t* __restrict__ hb_next,
-                                                  uint32_t hb_giant, ListClose lc) {
+                                                  ListClose lc) {
     __shared__ uint32_t s_g, s_inc, s_clear;
     __shared__ PickLds L;
     // no giant known (none picked yet, or a re-pick found none): the mode of the labels the last
@@ -1495,7 +1645,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
         // 0: full pass, 1: bitmap-incremental, 2: list (ListCtl: a complete NGL, and every fold of
         // the interval logged its first touches)
         if (lc.ctl) {
-            if (LISTS && s_inc && c_lv && !c_lo && !lc.unlogged) s_inc = 2u;
+            if (s_inc && c_lv && !c_lo && !lc.unlogged) s_inc = 2u;
             if (blockIdx.x == 0) {
                 lc.ctl[ListCtl::LVALID(lc.n3)] = (s_g != kInvalid && lc.list_next) ? 1u : 0u;
                 lc.ctl[ListCtl::LOVF(lc.z3)] = 0u;
@@ -1508,7 +1658,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
     __syncthreads();
     const uint32_t g = s_g;
     // this close writes the next NGL (seen vertices outside the giant) into sub-list blockIdx % kListSub
-    const bool build = LISTS && lc.ctl && lc.list_next && g != kInvalid;
+    const bool build = lc.ctl && lc.list_next && g != kInvalid;
     uint2* ngl_o = build ? lc.ngl_out + (size_t)sub * lc.ngl_sub : nullptr;
     uint32_t* ngl_c = build ? lc.ctl + ListCtl::NC(lc.n3) + sub : nullptr;
     uint32_t* ngl_v = build ? lc.ctl + ListCtl::LOVF(lc.n3) : nullptr;
@@ -1520,7 +1670,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
         }
     }
     const int lane = threadIdx.x & 63;
-    if (LISTS && s_inc == 2u) {
+    if (s_inc == 2u) {
         // list close: the last NGL (sub-list `sub` by the workgroups with that index mod kListSub)
         // and the interval's touch-log slots (one per wave, strided over the grid's waves). Their
         // labels may change (a hooked root); every other seen vertex is a giant member labelled g.
@@ -1577,14 +1727,8 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
         }
     } else if (s_inc) {                              // one bitmap word (32 vertices) per thread
         const uint32_t nwords = (uint32_t)((n + 31) >> 5);
-        // hooked-root marks of every fold since the last close (hb_giant): a straggler's parent that
-        // is unmarked is still a root, no grandparent read (as in the full pass below)
-        const bool usehb = hb_in != nullptr && hb_giant;
         for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += gridDim.x * blockDim.x) {
             uint32_t cand = sbits[w] & ~gbits[w];
-            // the next window's marks start empty (only where they are read: stale marks would only
-            // cost grandparent reads, and zeroing is an 8 MiB write per close at 2^26 ids)
-            if (hb_giant && hb_next) hb_next[w] = 0u;
             // vertices claimed under the giant root since the last close: already labelled g
             uint32_t add = cbits ? cbits[w] : 0u;
             if (add) cbits[w] = 0u;
@@ -1603,18 +1747,11 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                 }
 #pragma unroll
                 for (int k = 0; k < 8; ++k) p[k] = (k < m) ? parent[(w << 5) + vb[k]] : 0u;
-                bool need[8];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) need[k] = k < m && p[k] != (w << 5) + vb[k];
-                if (usehb) {
-                    uint32_t hw[8];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) hw[k] = need[k] ? hb_in[p[k] >> 5] : 0u;
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) need[k] = need[k] && ((hw[k] >> (p[k] & 31)) & 1u);
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t v = (w << 5) + vb[k];
+                    gp[k] = (k < m && p[k] != v) ? parent[p[k]] : p[k];
                 }
-#pragma unroll
-                for (int k = 0; k < 8; ++k) gp[k] = need[k] ? parent[p[k]] : p[k];
                 uint2 ng[8];
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
@@ -1629,7 +1766,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                     add |= (lab == g) ? (1u << vb[k]) : 0u;
                     if (lab != g) ng[k] = make_uint2(v, lab);
                 }
-                if (LISTS && build) list_append<8>(ngl_o, ngl_c, lc.ngl_sub, ngl_v, ng);
+                if (build) list_append<8>(ngl_o, ngl_c, lc.ngl_sub, ngl_v, ng);
             }
             if (add) gbits[w] |= add;
         }
@@ -1643,7 +1780,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
         // before the giant forms) becomes a bit test in a V/8-byte bitmap that stays in L2. Every
         // parent word written since the last close is a root at the time of writing (a hook's lo, a
         // claim's gR, a halving's grandparent), so "unmarked" is exact.
-        const bool usehb = hb_in != nullptr && (in[1] == kInvalid || hb_giant);
+        const bool usehb = hb_in != nullptr && in[1] == kInvalid;
         for (uint64_t blk = (uint64_t)blockIdx.x * 1024; blk < n; blk += (uint64_t)gridDim.x * 1024) {
             const uint32_t base = (uint32_t)blk + threadIdx.x * 4;
             uint32_t p[4];
@@ -1682,7 +1819,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                 ng[k] = make_uint2((p[k] != kInvalid && lab != g) ? v : kInvalid, lab);
                 if (samp_out && v < n && is_sample(v, sb)) samp_out[v >> sb] = lab;   // kInvalid: unseen
             }
-            if (LISTS && build) list_append<4>(ngl_o, ngl_c, lc.ngl_sub, ngl_v, ng);
+            if (build) list_append<4>(ngl_o, ngl_c, lc.ngl_sub, ngl_v, ng);
             uint32_t word = nib << (4 * (lane & 7));
             word |= __shfl_xor(word, 1, 64);
             word |= __shfl_xor(word, 2, 64);
