@@ -600,14 +600,17 @@ int launch_fold_any(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool a
 // host-buffer folds: edges per staging chunk (one window of the headline workload)
 constexpr uint64_t kStagingEdges = 1ull << 24;
 
-int fold_impl(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, uint32_t id_bits) {
+// dev_known: 1 = the caller has checked that both buffers are device memory (gs_cc_fold_windows,
+// once per call: two pointer-attribute queries per window are ~2-4 us of host time, the order of
+// a small window's GPU time), -1 = query here
+int fold_impl(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool aos, uint32_t id_bits, int dev_known = -1) {
     GS_TRY(check(h));
     if (n == 0) return GS_OK;
     if (!a || (!aos && !b)) return fail(GS_ERR_INVALID, "fold: null edge buffer");
     DeviceGuard g(h->device);
     if (h->sparse && id_bits != 64) return fail(GS_ERR_UNSUPPORTED, "fold: a sparse-id summary takes 64-bit ids");
     const size_t esz = id_bits / 8;
-    const bool dev = is_device_pointer(a) && (aos || is_device_pointer(b));
+    const bool dev = dev_known >= 0 ? dev_known != 0 : (is_device_pointer(a) && (aos || is_device_pointer(b)));
     h->compressed = false;
     h->minkey_valid = false;
     if (dev) {
@@ -1269,10 +1272,11 @@ int gs_cc_close_window(gs_cc_t* h) {
 static int fold_windows_loop(gs_cc_t* h, gs_comm_t* comm, int mode, const char* a, const char* b, uint64_t n,
                              uint64_t window_edges, uint64_t* windows_out) {
     const size_t esz = h->cfg.id_bits / 8;
+    const int dev = (n && is_device_pointer(a) && is_device_pointer(b)) ? 1 : 0;
     uint64_t w = 0;
     for (uint64_t off = 0; off < n; off += window_edges, ++w) {
         const uint64_t m = std::min(window_edges, n - off);
-        GS_TRY(fold_impl(h, a + off * esz, b + off * esz, m, false, h->cfg.id_bits));   // (no settle: above)
+        GS_TRY(fold_impl(h, a + off * esz, b + off * esz, m, false, h->cfg.id_bits, dev));   // (no settle: above)
         GS_TRY(comm ? gs_cc_merge_window(h, comm, mode) : gs_cc_close_window(h));
         if (windows_out) *windows_out = w + 1;
     }
