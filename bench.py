@@ -17,7 +17,8 @@ One step = one whole pass over the stream from an empty summary (reset included)
 
 Other lines (not the headline): --workload c2 | c4 | c5 | c3_single (the whole stream as one
 window), --id-bits 64 (the reference's Long ids), --host-input (edges in pinned host memory: the
-PCIe-inclusive rate of gs_cc_fold's staged path).
+PCIe-inclusive rate of gs_cc_fold's staged path); --workload parse | bip: SURVEY.md 8(f)'s
+edge-file ingestion and BipartitenessCheck (bench_rows.py).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under torch.distributed.run.
 Rank 0 prints one JSON line.
@@ -48,6 +49,8 @@ METRIC = "streaming CC edges/sec (RMAT-26) at 1/2/4/8 MI355X + % of HBM roofline
 WORKLOADS = {  # name: (generator, scale or n, edge factor, window log2, seed)
     "c3": ("rmat", 26, 16, 24, 1), "c3_single": ("rmat", 26, 16, 30, 1),
     "c2": ("rmat", 20, 16, 20, 1), "c4": ("er", 24, 1, 20, 2), "c5": ("rmat", 24, 16, 16, 3),
+    # SURVEY.md 8(f) rows (bench_rows.py): edge-file ingestion of 2^24 lines; BipartitenessCheck
+    "parse": ("parse", 24, 1, 24, 1), "bip": ("bip", 22, 16, 20, 1),
 }
 
 
@@ -59,7 +62,9 @@ def parse():
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS),
                     help="c3 (default, the headline): RMAT-26 EF16, 2^24-edge windows; c3_single: the same "
                          "stream as one window; c2: RMAT-20 EF16, 2^20-edge windows; c4: Erdos-Renyi n=m=2^24, "
-                         "2^20-edge windows; c5: RMAT-24 EF16, 2^16-edge windows + per-window emission latency")
+                         "2^20-edge windows; c5: RMAT-24 EF16, 2^16-edge windows + per-window emission latency; "
+                         "parse: edge-file ingestion (gs_parse_edges) of an RMAT-24 stream's text, 2^24 lines; "
+                         "bip: BipartitenessCheck (gs_bip_*) on a bipartite RMAT-22 EF16 stream, 2^20-edge windows")
     ap.add_argument("--scale", type=int, default=None, help="override the workload's RMAT scale")
     ap.add_argument("--edge-factor", type=int, default=None)
     ap.add_argument("--window-log2", type=int, default=None, help="global window = 2^this edges")
@@ -131,6 +136,10 @@ def main():
     sys.stdout.flush()
     out = os.fdopen(os.dup(1), "w", buffering=1)
     os.dup2(2, 1)
+    if a.kind in ("parse", "bip"):                # SURVEY.md 8(f) rows, one GPU
+        import bench_rows
+        (bench_rows.run_parse if a.kind == "parse" else bench_rows.run_bip)(a, out)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

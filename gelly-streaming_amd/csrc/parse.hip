@@ -7,11 +7,16 @@
 // which parseLong rejects), trailing whitespace is dropped by split(), fields past the second are
 // ignored, a field is an optional '+'/'-' and decimal digits within the int64 range, and any other
 // line fails the job. This file restates those rules for every line in parallel:
-//   k_nl_count   per 4 KiB chunk: number of '\n'
-//   k_nl_scan    exclusive scan of the chunk counts (one workgroup)
-//   k_nl_place   line end offsets
-//   k_parse      one thread per line: two fields -> src[i], dst[i]; a bad line records its index
-//                (atomicMin) and the host reports the first one.
+//   k_nl_count      per 4 KiB chunk: number of '\n' (16-B loads)
+//   k_nl_scan       exclusive scan of the chunk counts (one workgroup) = the first line of each chunk
+//   k_parse_chunk   per 4 KiB chunk again: each thread's 16 bytes, a workgroup scan of their '\n'
+//                   counts, and every line that STARTS in those bytes parsed by that thread: its index
+//                   is the chunk's first line + the '\n's before it, so no line-offset array is
+//                   written or read (the round-3 version wrote and re-read 8 B per line: 0.54 ms of
+//                   its 1.77 ms per 2^24 lines); a bad line records its index (atomicMin) and the
+//                   host reports the first one.
+// Scratch (chunk counts and offsets, the bad-line word, a device copy of host text) is kept per
+// thread and device and grown, not allocated per call.
 #include <algorithm>
 #include <vector>
 
@@ -21,11 +26,26 @@ namespace gsgpu {
 
 constexpr int kChunk = 4096;                 // bytes per workgroup (256 threads x 16 B)
 
+// the '\n' bytes of a thread's 16 bytes at base (one 16-B load when the whole block is in the text)
+__device__ __forceinline__ uint32_t nl_mask16(const char* __restrict__ t, uint64_t n, uint64_t base) {
+    uint32_t m = 0;
+    if (base + 16 <= n) {
+        const uint4 q = *reinterpret_cast<const uint4*>(t + base);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) m |= (((w[j] >> (8 * k)) & 0xFFu) == '\n' ? 1u : 0u) << (4 * j + k);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) m |= (base + k < n && t[base + k] == '\n' ? 1u : 0u) << k;
+    }
+    return m;
+}
+
 __global__ __launch_bounds__(256) void k_nl_count(const char* __restrict__ t, uint64_t n, uint32_t* __restrict__ cnt) {
     const uint64_t base = (uint64_t)blockIdx.x * kChunk + threadIdx.x * 16;
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) c += (base + k < n && t[base + k] == '\n');
+    uint32_t c = (uint32_t)__popc(nl_mask16(t, n, base));
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
     __shared__ uint32_t ws[4];
@@ -34,48 +54,31 @@ __global__ __launch_bounds__(256) void k_nl_count(const char* __restrict__ t, ui
     if (threadIdx.x == 0) cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
+// exclusive scan of the chunk counts in one 1024-thread workgroup: each thread a contiguous run of
+// counts, a shuffle scan of the runs' sums (a serial pass over 1024 partials by one thread cost
+// ~100 us per 2^24 lines)
 __global__ __launch_bounds__(1024) void k_nl_scan(const uint32_t* __restrict__ cnt, uint64_t* __restrict__ off, uint32_t nb) {
-    __shared__ unsigned long long part[1024];
+    __shared__ unsigned long long wsum[16];
     const uint32_t per = (nb + blockDim.x - 1) / blockDim.x;
-    const uint32_t lo = threadIdx.x * per, hi = min(lo + per, nb);
+    const uint32_t lo = min(threadIdx.x * per, nb), hi = min(lo + per, nb);
     unsigned long long s = 0;
+#pragma unroll 8
     for (uint32_t i = lo; i < hi; ++i) s += cnt[i];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long run = 0;
-        for (uint32_t t = 0; t < blockDim.x; ++t) { const unsigned long long x = part[t]; part[t] = run; run += x; }
-        off[nb] = run;
-    }
-    __syncthreads();
-    unsigned long long run = part[threadIdx.x];
-    for (uint32_t i = lo; i < hi; ++i) { off[i] = run; run += cnt[i]; }
-}
-
-// line ends: ends[k] = byte offset of the k-th '\n'
-__global__ __launch_bounds__(256) void k_nl_place(const char* __restrict__ t, uint64_t n, const uint64_t* __restrict__ off,
-                                                  uint64_t* __restrict__ ends) {
-    const uint64_t base = (uint64_t)blockIdx.x * kChunk + threadIdx.x * 16;
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) c += (base + k < n && t[base + k] == '\n');
-    // exclusive scan of c over the workgroup
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t incl = c;
+    unsigned long long incl = s;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
+        const unsigned long long y = __shfl_up(incl, o, 64);
         if (lane >= o) incl += y;
     }
-    __shared__ uint32_t ws[4];
-    if (lane == 63) ws[wid] = incl;
+    if (lane == 63) wsum[wid] = incl;
     __syncthreads();
-    uint32_t wbase = 0;
-    for (int w = 0; w < wid; ++w) wbase += ws[w];
-    uint64_t pos = off[blockIdx.x] + wbase + incl - c;
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-        if (base + k < n && t[base + k] == '\n') ends[pos++] = base + k;
+    unsigned long long wbase = 0;
+    for (int w = 0; w < wid; ++w) wbase += wsum[w];
+    unsigned long long run = wbase + incl - s;
+    if (threadIdx.x == blockDim.x - 1) off[nb] = wbase + incl;
+#pragma unroll 8
+    for (uint32_t i = lo; i < hi; ++i) { off[i] = run; run += cnt[i]; }
 }
 
 __device__ __forceinline__ bool is_ws(char ch) {          // Java \s: [ \t\n\x0B\f\r]
@@ -101,31 +104,184 @@ __device__ bool parse_long(const char* __restrict__ t, uint64_t a, uint64_t b, i
     return true;
 }
 
+// the line [a, e) (e = its '\n' or the end of the text) -> (x, y); false if the reference rejects it
+__device__ __forceinline__ bool parse_line(const char* __restrict__ t, uint64_t a, uint64_t e, int64_t* x, int64_t* y) {
+    uint64_t b = e;
+    while (b > a && is_ws(t[b - 1])) --b;                       // split() drops trailing empty fields
+    uint64_t s1 = a;
+    while (s1 < b && !is_ws(t[s1])) ++s1;                       // field 0 = [a, s1)
+    uint64_t e2 = s1 + 1;                                       // field 1 starts right after ONE separator
+    while (e2 < b && !is_ws(t[e2])) ++e2;
+    return s1 < b && parse_long(t, a, s1, x) && parse_long(t, s1 + 1, e2, y);
+}
+
 template <typename IdT>
-__global__ __launch_bounds__(256) void k_parse(const char* __restrict__ t, const uint64_t* __restrict__ ends, uint64_t lines,
-                                               IdT* __restrict__ src, IdT* __restrict__ dst,
-                                               unsigned long long* __restrict__ bad_line) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lines; i += stride) {
-        const uint64_t a = i ? ends[i - 1] + 1 : 0;
-        uint64_t b = ends[i];                                   // exclusive ('\n' or end of text)
-        while (b > a && is_ws(t[b - 1])) --b;                   // split() drops trailing empty fields
-        uint64_t s1 = a;
-        while (s1 < b && !is_ws(t[s1])) ++s1;                   // field 0 = [a, s1)
-        uint64_t e2 = s1 + 1;                                   // field 1 starts right after ONE separator
-        while (e2 < b && !is_ws(t[e2])) ++e2;
+__device__ __forceinline__ void parse_store(const char* __restrict__ t, uint64_t n, uint64_t a, uint64_t i,
+                                            IdT* __restrict__ src, IdT* __restrict__ dst,
+                                            unsigned long long* __restrict__ bad_line) {
+    uint64_t e = a;
+    while (e < n && t[e] != '\n') ++e;
+    int64_t x = 0, y = 0;
+    const bool ok = parse_line(t, a, e, &x, &y) &&
+                    (sizeof(IdT) == 8 || ((uint64_t)x <= 0xFFFFFFFEull && (uint64_t)y <= 0xFFFFFFFEull));
+    if (!ok) { atomicMin(bad_line, (unsigned long long)i); return; }
+    src[i] = static_cast<IdT>(x);
+    dst[i] = static_cast<IdT>(y);
+}
+
+__device__ __forceinline__ uint4 load16(const char* __restrict__ t, uint64_t n, uint64_t base) {
+    if (base + 16 <= n) return *reinterpret_cast<const uint4*>(t + base);
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (base + k < n) w[k >> 2] |= (uint32_t)(uint8_t)t[base + k] << (8 * (k & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Field scanner of one line from a 48-byte window of the LDS copy (the line starts at window byte r,
+// which is text byte base + r; bytes at or past text byte n end the line). Java's rules (file header):
+// field 0 = optional sign + digits up to ONE whitespace, field 1 = optional sign + digits up to
+// whitespace / end of line, anything after field 1 ignored; every other shape is rejected, as are
+// values outside int64. Returns 1 = parsed, 0 = rejected, 2 = the line does not end inside the
+// window (the caller parses it from memory).
+enum { kF0Start, kF0Sign, kF0Dig, kSep, kF1Sign, kF1Dig, kDone, kBad };
+// overflow without a division: v * 10 + d > limit (INT64_MAX, or 2^63 for a '-' field) exactly when
+// v > limit / 10 (the same for both) or v == limit / 10 and d > limit % 10 (7, or 8)
+constexpr uint64_t kLim10 = 922337203685477580ull;
+__device__ __forceinline__ bool acc_digit(uint64_t& v, uint64_t d, bool neg) {
+    if (v > kLim10 || (v == kLim10 && d > (neg ? 8u : 7u))) return false;
+    v = v * 10 + d;
+    return true;
+}
+__device__ __forceinline__ int scan_window(const uint8_t* w, int r, uint64_t base, uint64_t n, int64_t* x, int64_t* y) {
+    int st = kF0Start;
+    bool neg0 = false, neg1 = false;
+    uint64_t v0 = 0, v1 = 0;
+    // a 4-byte LDS word per step (one read per 4 bytes instead of per byte)
+    for (int j = r >> 2; j < 12 && st < kDone; ++j) {
+        const uint32_t word = reinterpret_cast<const uint32_t*>(w)[j];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int p = 4 * j + b;
+            if (p < r || st >= kDone) continue;
+            const uint32_t c = (base + p < n) ? ((word >> (8 * b)) & 0xFFu) : (uint32_t)'\n';
+            const bool dig = c >= '0' && c <= '9';
+            const bool ws = c == ' ' || c == '\t' || c == '\n' || c == 0x0B || c == '\f' || c == '\r';
+            const bool sign = c == '+' || c == '-';
+            const uint64_t d = c - '0';
+            switch (st) {
+            case kF0Start: st = dig ? kF0Dig : sign ? kF0Sign : kBad; neg0 = c == '-'; v0 = dig ? d : 0; break;
+            case kF0Sign: st = dig ? kF0Dig : kBad; v0 = d; break;
+            case kF0Dig:
+                if (dig) {
+                    if (!acc_digit(v0, d, neg0)) st = kBad;
+                } else {
+                    st = (ws && c != '\n') ? kSep : kBad;      // "123\n": no field 1
+                }
+                break;
+            case kSep: st = dig ? kF1Dig : sign ? kF1Sign : kBad; neg1 = c == '-'; v1 = dig ? d : 0; break;
+            case kF1Sign: st = dig ? kF1Dig : kBad; v1 = d; break;
+            case kF1Dig:
+                if (dig) {
+                    if (!acc_digit(v1, d, neg1)) st = kBad;
+                } else {
+                    st = ws ? kDone : kBad;
+                }
+                break;
+            }
+        }
+    }
+    if (st == kBad) return 0;
+    if (st != kDone) return 2;
+    *x = neg0 ? (int64_t)(0 - v0) : (int64_t)v0;
+    *y = neg1 ? (int64_t)(0 - v1) : (int64_t)v1;
+    return 1;
+}
+
+// One 4 KiB chunk per workgroup, 16 bytes per thread, staged in LDS with the 32 bytes after the
+// chunk: a thread parses every line that STARTS in its 16 bytes (after each '\n' there, and line 0
+// at byte 0) from a 48-byte window of that LDS copy (a line longer than the window is parsed from
+// memory); line index = the chunk's first line (off, the scan of k_nl_count) + the '\n's before it.
+template <typename IdT>
+__global__ __launch_bounds__(256) void k_parse_chunk(const char* __restrict__ t, uint64_t n, const uint64_t* __restrict__ off,
+                                                     IdT* __restrict__ src, IdT* __restrict__ dst,
+                                                     unsigned long long* __restrict__ bad_line) {
+    __shared__ uint4 s_text[kChunk / 16 + 2];
+    const uint64_t cbase = (uint64_t)blockIdx.x * kChunk;
+    const uint64_t base = cbase + threadIdx.x * 16;
+    const uint4 q = load16(t, n, base);
+    s_text[threadIdx.x] = q;
+    if (threadIdx.x < 2) s_text[kChunk / 16 + threadIdx.x] = load16(t, n, cbase + kChunk + threadIdx.x * 16);
+    uint32_t m = 0;
+    {
+        const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                m |= ((((qw[j] >> (8 * k)) & 0xFFu) == '\n' && base + 4 * j + k < n) ? 1u : 0u) << (4 * j + k);
+    }
+    const uint32_t c = (uint32_t)__popc(m);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    __shared__ uint32_t ws[4];
+    if (lane == 63) ws[wid] = incl;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (int w = 0; w < wid; ++w) wbase += ws[w];
+    uint64_t i = off[blockIdx.x] + wbase + incl - c;           // '\n's before this thread's bytes
+    const uint8_t* win = reinterpret_cast<const uint8_t*>(s_text) + threadIdx.x * 16;
+    auto one = [&](int r, uint64_t li) {
         int64_t x = 0, y = 0;
-        const bool ok = s1 < b && parse_long(t, a, s1, &x) && parse_long(t, s1 + 1, e2, &y) &&
-                        (sizeof(IdT) == 8 || ((uint64_t)x <= 0xFFFFFFFEull && (uint64_t)y <= 0xFFFFFFFEull));
-        if (!ok) { atomicMin(bad_line, (unsigned long long)i); continue; }
-        src[i] = static_cast<IdT>(x);
-        dst[i] = static_cast<IdT>(y);
+        const int k = scan_window(win, r, base, n, &x, &y);
+        if (k == 2) { parse_store<IdT>(t, n, base + r, li, src, dst, bad_line); return; }
+        const bool ok = k == 1 && (sizeof(IdT) == 8 || ((uint64_t)x <= 0xFFFFFFFEull && (uint64_t)y <= 0xFFFFFFFEull));
+        if (!ok) { atomicMin(bad_line, (unsigned long long)li); return; }
+        src[li] = static_cast<IdT>(x);
+        dst[li] = static_cast<IdT>(y);
+    };
+    if (base == 0) one(0, 0);                                  // line 0
+    while (m) {
+        const int k = __ffs(m) - 1;
+        m &= m - 1;
+        ++i;                                                    // the line after this '\n'
+        if (base + (uint64_t)k + 1 < n) one(k + 1, i);
     }
 }
 
 }  // namespace gsgpu
 
 using namespace gsgpu;
+
+namespace {
+// per thread and device scratch, grown and kept (a parse call allocates nothing in steady use)
+struct ParseScratch {
+    char* text = nullptr;                // device copy of host (or misaligned) text
+    size_t text_cap = 0;
+    uint32_t* cnt = nullptr;
+    uint64_t* off = nullptr;
+    size_t chunks_cap = 0;
+    unsigned long long* bad = nullptr;
+    unsigned long long* hbad = nullptr;  // pinned: [bad line, '\n' count]
+};
+constexpr int kMaxParseDevices = 64;
+thread_local ParseScratch t_scratch[kMaxParseDevices];
+
+int grow(void** p, size_t* cap, size_t want) {
+    if (*cap >= want) return GS_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, want) != hipSuccess) { (void)hipGetLastError(); return fail(GS_ERR_NOMEM, "gs_parse_edges: scratch of %zu bytes", want); }
+    *cap = want;
+    return GS_OK;
+}
+}  // namespace
 
 extern "C" int gs_parse_edges(const char* text, uint64_t n_bytes, uint32_t id_bits, void* src, void* dst,
                               uint64_t cap, uint64_t* n_edges, int device, void* stream) {
@@ -134,85 +290,84 @@ extern "C" int gs_parse_edges(const char* text, uint64_t n_bytes, uint32_t id_bi
     if (id_bits != 32 && id_bits != 64) return fail(GS_ERR_INVALID, "gs_parse_edges: id_bits must be 32 or 64");
     if (n_bytes == 0) return GS_OK;
     if (!text) return fail(GS_ERR_INVALID, "gs_parse_edges: null text");
+    if (device < 0 || device >= kMaxParseDevices) return fail(GS_ERR_INVALID, "gs_parse_edges: device %d", device);
     DeviceGuard g(device);
     if (!g.ok) return fail(GS_ERR_HIP, "gs_parse_edges: hipSetDevice(%d) failed", device);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    ParseScratch& sc = t_scratch[device];
     const size_t esz = id_bits / 8;
     const uint32_t nb = (uint32_t)((n_bytes + kChunk - 1) / kChunk);
-    // scratch: text copy (if host), chunk counts, offsets, bad-line word, line ends (sized after the count)
-    char* dtext = nullptr;
-    uint32_t* cnt = nullptr;
-    uint64_t* off = nullptr;
-    unsigned long long* bad = nullptr;
-    uint64_t* ends = nullptr;
-    void* dsrc = nullptr;
-    void* ddst = nullptr;
-    int rc = GS_OK;
-    auto cleanup = [&]() {
-        if (dtext && dtext != text) (void)hipFree(dtext);
-        if (cnt) (void)hipFree(cnt);
-        if (off) (void)hipFree(off);
-        if (bad) (void)hipFree(bad);
-        if (ends) (void)hipFree(ends);
-        if (dsrc && dsrc != src) (void)hipFree(dsrc);
-        if (ddst && ddst != dst) (void)hipFree(ddst);
-    };
-#define GS_PARSE_HIP(expr)                                                                            \
-    do {                                                                                              \
-        hipError_t e_ = (expr);                                                                       \
-        if (e_ != hipSuccess) { rc = fail(GS_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); cleanup(); return rc; } \
-    } while (0)
-    if (is_device_pointer(text)) {
-        dtext = const_cast<char*>(text);
-    } else {
-        GS_PARSE_HIP(hipMalloc(&dtext, n_bytes));
-        GS_PARSE_HIP(hipMemcpyAsync(dtext, text, n_bytes, hipMemcpyHostToDevice, s));
+    // the kernels read the text in 16-B loads: host or misaligned device text goes through the
+    // scratch copy
+    const char* dtext = text;
+    if (!is_device_pointer(text) || (reinterpret_cast<uintptr_t>(text) & 15)) {
+        size_t c = sc.text_cap;
+        GS_TRY(grow(reinterpret_cast<void**>(&sc.text), &c, n_bytes));
+        sc.text_cap = c;
+        GS_HIP(hipMemcpyAsync(sc.text, text, n_bytes, hipMemcpyDefault, s));
+        dtext = sc.text;
     }
-    GS_PARSE_HIP(hipMalloc(&cnt, (size_t)nb * 4));
-    GS_PARSE_HIP(hipMalloc(&off, ((size_t)nb + 1) * 8));
-    GS_PARSE_HIP(hipMalloc(&bad, 8));
-    GS_PARSE_HIP(hipMemsetAsync(bad, 0xFF, 8, s));
-    hipLaunchKernelGGL(k_nl_count, dim3(nb), dim3(256), 0, s, dtext, n_bytes, cnt);
-    hipLaunchKernelGGL(k_nl_scan, dim3(1), dim3(1024), 0, s, cnt, off, nb);
-    GS_PARSE_HIP(hipGetLastError());
-    uint64_t nl = 0;
-    GS_PARSE_HIP(hipMemcpyAsync(&nl, off + nb, 8, hipMemcpyDeviceToHost, s));
+    if (sc.chunks_cap < (size_t)nb + 1) {
+        size_t c1 = sc.chunks_cap ? sc.chunks_cap * 4 : 0, c2 = sc.chunks_cap ? (sc.chunks_cap + 1) * 8 : 0;
+        GS_TRY(grow(reinterpret_cast<void**>(&sc.cnt), &c1, ((size_t)nb + 1) * 4));
+        GS_TRY(grow(reinterpret_cast<void**>(&sc.off), &c2, ((size_t)nb + 2) * 8));
+        sc.chunks_cap = (size_t)nb + 1;
+    }
+    if (!sc.bad) {
+        size_t c = 0;
+        GS_TRY(grow(reinterpret_cast<void**>(&sc.bad), &c, 8));
+        if (hipHostMalloc(&sc.hbad, 2 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(GS_ERR_NOMEM, "gs_parse_edges: pinned scratch");
+        }
+    }
+    GS_HIP(hipMemsetAsync(sc.bad, 0xFF, 8, s));
+    hipLaunchKernelGGL(k_nl_count, dim3(nb), dim3(256), 0, s, dtext, n_bytes, sc.cnt);
+    hipLaunchKernelGGL(k_nl_scan, dim3(1), dim3(1024), 0, s, sc.cnt, sc.off, nb);
+    GS_HIP(hipGetLastError());
     char last = '\n';
-    GS_PARSE_HIP(hipMemcpyAsync(&last, dtext + n_bytes - 1, 1, hipMemcpyDeviceToHost, s));
-    GS_PARSE_HIP(hipStreamSynchronize(s));
+    GS_HIP(hipMemcpyAsync(&sc.hbad[1], sc.off + nb, 8, hipMemcpyDeviceToHost, s));
+    GS_HIP(hipMemcpyAsync(&last, dtext + n_bytes - 1, 1, hipMemcpyDeviceToHost, s));
+    GS_HIP(hipStreamSynchronize(s));
+    const uint64_t nl = sc.hbad[1];
     const uint64_t lines = nl + (last != '\n');             // a last line without '\n' still counts
-    GS_PARSE_HIP(hipMalloc(&ends, (size_t)std::max<uint64_t>(lines, 1) * 8));
-    hipLaunchKernelGGL(k_nl_place, dim3(nb), dim3(256), 0, s, dtext, n_bytes, off, ends);
-    if (last != '\n') GS_PARSE_HIP(hipMemcpyAsync(ends + nl, &n_bytes, 8, hipMemcpyHostToDevice, s));
-    const bool dev_out = is_device_pointer(src) && is_device_pointer(dst);
     if (lines > cap) {
         *n_edges = lines;
-        cleanup();
         return fail(GS_ERR_CAPACITY, "gs_parse_edges: %llu lines, capacity %llu", (unsigned long long)lines,
                     (unsigned long long)cap);
     }
-    if (dev_out) {
-        dsrc = src;
-        ddst = dst;
-    } else {
-        GS_PARSE_HIP(hipMalloc(&dsrc, (size_t)std::max<uint64_t>(lines, 1) * esz));
-        GS_PARSE_HIP(hipMalloc(&ddst, (size_t)std::max<uint64_t>(lines, 1) * esz));
+    const bool dev_out = is_device_pointer(src) && is_device_pointer(dst);
+    void* dsrc = src;
+    void* ddst = dst;
+    if (!dev_out) {                                          // host outputs: staged per call
+        if (hipMalloc(&dsrc, (size_t)std::max<uint64_t>(lines, 1) * esz) != hipSuccess ||
+            hipMalloc(&ddst, (size_t)std::max<uint64_t>(lines, 1) * esz) != hipSuccess) {
+            (void)hipGetLastError();
+            if (dsrc != src) (void)hipFree(dsrc);
+            return fail(GS_ERR_NOMEM, "gs_parse_edges: output staging");
+        }
     }
-    const unsigned grid = (unsigned)std::min<uint64_t>((lines + 255) / 256 + 1, 16384);
     if (id_bits == 32)
-        hipLaunchKernelGGL(k_parse<uint32_t>, dim3(grid), dim3(256), 0, s, dtext, ends, lines, (uint32_t*)dsrc, (uint32_t*)ddst, bad);
+        hipLaunchKernelGGL(k_parse_chunk<uint32_t>, dim3(nb), dim3(256), 0, s, dtext, n_bytes, sc.off, (uint32_t*)dsrc,
+                           (uint32_t*)ddst, sc.bad);
     else
-        hipLaunchKernelGGL(k_parse<int64_t>, dim3(grid), dim3(256), 0, s, dtext, ends, lines, (int64_t*)dsrc, (int64_t*)ddst, bad);
-    GS_PARSE_HIP(hipGetLastError());
-    unsigned long long first_bad = 0;
-    GS_PARSE_HIP(hipMemcpyAsync(&first_bad, bad, 8, hipMemcpyDeviceToHost, s));
-    if (!dev_out && lines) {
-        GS_PARSE_HIP(hipMemcpyAsync(src, dsrc, lines * esz, hipMemcpyDeviceToHost, s));
-        GS_PARSE_HIP(hipMemcpyAsync(dst, ddst, lines * esz, hipMemcpyDeviceToHost, s));
+        hipLaunchKernelGGL(k_parse_chunk<int64_t>, dim3(nb), dim3(256), 0, s, dtext, n_bytes, sc.off, (int64_t*)dsrc,
+                           (int64_t*)ddst, sc.bad);
+    int rc = GS_OK;
+    if (hipGetLastError() != hipSuccess) rc = fail(GS_ERR_HIP, "gs_parse_edges: k_parse_chunk launch failed");
+    if (rc == GS_OK && hipMemcpyAsync(&sc.hbad[0], sc.bad, 8, hipMemcpyDeviceToHost, s) != hipSuccess)
+        rc = fail(GS_ERR_HIP, "gs_parse_edges: copy of the bad-line word failed");
+    if (rc == GS_OK && !dev_out && lines &&
+        (hipMemcpyAsync(src, dsrc, lines * esz, hipMemcpyDeviceToHost, s) != hipSuccess ||
+         hipMemcpyAsync(dst, ddst, lines * esz, hipMemcpyDeviceToHost, s) != hipSuccess))
+        rc = fail(GS_ERR_HIP, "gs_parse_edges: copy of the outputs failed");
+    if (hipStreamSynchronize(s) != hipSuccess && rc == GS_OK) rc = fail(GS_ERR_HIP, "gs_parse_edges: stream sync failed");
+    if (!dev_out) {
+        (void)hipFree(dsrc);
+        (void)hipFree(ddst);
     }
-    GS_PARSE_HIP(hipStreamSynchronize(s));
-#undef GS_PARSE_HIP
-    cleanup();
+    if (rc != GS_OK) return rc;
+    const unsigned long long first_bad = sc.hbad[0];
     if (first_bad != ~0ull) {
         *n_edges = first_bad;
         return fail(GS_ERR_INVALID, "gs_parse_edges: line %llu is not \"<long><whitespace><long>\" "

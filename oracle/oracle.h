@@ -124,7 +124,12 @@ void gso_gen_rmat(int64_t* src, int64_t* dst, uint64_t first, uint64_t n, int sc
 /* Erdős–Rényi G(n, m)-style: uniform endpoints in [0, nv). */
 void gso_gen_er(int64_t* src, int64_t* dst, uint64_t first, uint64_t n, uint64_t nv, uint64_t seed);
 
+/* Edge-file input (ConnectedComponentsExample.java:108-119, parse.c): lines parsed (<= cap are
+ * written), or -(index of the first line the reference rejects) - 1. */
+int64_t gso_parse_edges(const char* text, uint64_t n_bytes, int64_t* src, int64_t* dst, uint64_t cap);
+
 #ifdef __cplusplus
 }
 #endif
+
 #endif

@@ -239,7 +239,22 @@ class COracle:
         L.gso_gen_er.argtypes = [vp, vp, u64, u64, u64, u64]
         L.gso_splitmix64.argtypes = [u64]; L.gso_splitmix64.restype = u64
         L.gso_pair_mix.argtypes = [u64, u64]; L.gso_pair_mix.restype = u64
+        L.gso_parse_edges.argtypes = [ctypes.c_char_p, u64, vp, vp, u64]; L.gso_parse_edges.restype = i64
         self.L = L
+
+    # ---- edge-file input (parse.c) ----
+    def parse_edges(self, text: bytes):
+        """(src, dst, seconds) as int64 arrays, or (bad line index, None, seconds)."""
+        import time
+        cap = text.count(b"\n") + 1
+        src = np.empty(cap, dtype=np.int64)
+        dst = np.empty(cap, dtype=np.int64)
+        t0 = time.perf_counter()
+        r = int(self.L.gso_parse_edges(text, len(text), _p(src), _p(dst), cap))
+        secs = time.perf_counter() - t0
+        if r < 0:
+            return -r - 1, None, secs
+        return src[:r], dst[:r], secs
 
     # ---- generators ----
     def gen_rmat(self, first: int, n: int, scale: int, seed: int, scramble: bool = True,

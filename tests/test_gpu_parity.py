@@ -762,3 +762,48 @@ def test_parse_edges_large_random_and_fold(oracle):
     ps, pd = parse_edges(text, id_bits=32)
     np.testing.assert_array_equal(ps, s)
     np.testing.assert_array_equal(pd, d)
+
+
+def test_parse_edges_long_lines_extremes_and_device_text(torch_cuda):
+    """Lines longer than the kernel's 48-byte window (parsed from memory), int64 extremes and
+    leading zeros, 4 KiB chunk boundaries at every offset, and device text at a misaligned
+    address (copied to aligned scratch) against the Java rules."""
+    import ctypes
+    from gsgpu._abi import call
+    from gsgpu.edgefile import parse_edges
+    torch = torch_cuda
+    rng = np.random.default_rng(7)
+    lines = []
+    for i in range(20000):
+        k = i % 7
+        if k == 0:
+            lines.append(b"%d %d" % (rng.integers(0, 1 << 62), -int(rng.integers(0, 1 << 62))))
+        elif k == 1:
+            lines.append(b"-9223372036854775808 9223372036854775807 trailing fields here")
+        elif k == 2:
+            lines.append(b"000000000000000000000000000042 +0000000000000000000000000007\t\t")
+        elif k == 3:
+            lines.append(b"%d\t%d" % (i, i + 1) + b" " * int(rng.integers(0, 40)))
+        else:
+            lines.append(b"%d %d" % (rng.integers(0, 1000), rng.integers(0, 1000)))
+    text = b"\n".join(lines) + b"\n"
+    want = _java_parse(text)
+    got = parse_edges(text, id_bits=64)
+    np.testing.assert_array_equal(got[0], want[0])
+    np.testing.assert_array_equal(got[1], want[1])
+    buf = torch.zeros(len(text) + 3, dtype=torch.uint8, device="cuda")
+    buf[3:] = torch.frombuffer(bytearray(text), dtype=torch.uint8).cuda()
+    n = len(want[0])
+    ps = torch.empty(n, dtype=torch.int64, device="cuda")
+    pd = torch.empty(n, dtype=torch.int64, device="cuda")
+    cnt = ctypes.c_uint64()
+    torch.cuda.synchronize()
+    call("gs_parse_edges", ctypes.c_void_p(buf.data_ptr() + 3), len(text), 64, ctypes.c_void_p(ps.data_ptr()),
+         ctypes.c_void_p(pd.data_ptr()), n, ctypes.byref(cnt), 0, None)
+    assert cnt.value == n
+    np.testing.assert_array_equal(ps.cpu().numpy(), want[0])
+    np.testing.assert_array_equal(pd.cpu().numpy(), want[1])
+    bad = text + b"1 99999999999999999999\n5 6\n"
+    assert _java_parse(bad) == n
+    with pytest.raises(GsError):
+        parse_edges(bad, id_bits=64)

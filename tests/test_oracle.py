@@ -259,3 +259,52 @@ def test_c5_fixture_first_windows_live(oracle):
     assert [int(x) for x in r["checksums"]] == [int(x) for x in fx["checksums"][:k]]
     assert [int(x) for x in r["counts"][:, 0]] == fx["vertices"][:k]
     assert [int(x) for x in r["counts"][:, 1]] == fx["components"][:k]
+
+
+# ---------------- edge-file input (oracle/parse.c) vs the Java rules ----------------
+def _java_split_parse(text: bytes):
+    """ConnectedComponentsExample.java:108-119 with Python's re: line.split("\\\\s") (trailing
+    empties dropped), Long.parseLong of fields 0 and 1; (src, dst) or the first bad line index."""
+    import re
+    lines = text.decode().split("\n")
+    if lines and lines[-1] == "":
+        lines = lines[:-1]
+    src, dst = [], []
+    for i, ln in enumerate(lines):
+        f = re.split(r"[ \t\n\x0b\f\r]", ln)
+        while f and f[-1] == "":
+            f.pop()
+        ok = len(f) >= 2 and all(re.fullmatch(r"[+-]?[0-9]+", x) for x in f[:2])
+        if ok:
+            a, b = int(f[0]), int(f[1])
+            ok = -(1 << 63) <= a < (1 << 63) and -(1 << 63) <= b < (1 << 63)
+        if not ok:
+            return i
+        src.append(a)
+        dst.append(b)
+    return np.array(src, dtype=np.int64), np.array(dst, dtype=np.int64)
+
+
+def test_oracle_parse_edges_valid_forms(oracle):
+    text = (b"1 2\n3\t4\n5 6 extra fields\n+7 -8\r\n9 10  \n-9223372036854775808 9223372036854775807\n" +
+            b"".join(b"%d %d\n" % (i, i * 7 % 1000) for i in range(5000)) + b"11 12")
+    want = _java_split_parse(text)
+    s, d, _ = oracle.parse_edges(text)
+    np.testing.assert_array_equal(s, want[0])
+    np.testing.assert_array_equal(d, want[1])
+
+
+@pytest.mark.parametrize("bad", [b"1  2\n", b"\n", b" 1 2\n", b"1x 2\n", b"1\n", b"1 99999999999999999999\n",
+                                 b"1 9223372036854775808\n", b"- 3\n", b"   \n"])
+def test_oracle_parse_edges_rejects_what_java_rejects(oracle, bad):
+    text = b"5 6\n7 8\n" + bad + b"9 10\n"
+    assert _java_split_parse(text) == 2
+    assert oracle.parse_edges(text)[0] == 2
+
+
+def test_oracle_parse_edges_random(oracle):
+    s, d = oracle.gen_rmat(0, 20000, 20, 5)
+    text = "".join("%d %d\n" % (a, b) for a, b in zip(s.tolist(), d.tolist())).encode()
+    ps, pd, _ = oracle.parse_edges(text)
+    np.testing.assert_array_equal(ps, s)
+    np.testing.assert_array_equal(pd, d)
