@@ -8,7 +8,7 @@
 // ignored, a field is an optional '+'/'-' and decimal digits within the int64 range, and any other
 // line fails the job. This file restates those rules for every line in parallel:
 //   k_nl_count      per 4 KiB chunk: number of '\n' (16-B loads)
-//   k_nl_scan       exclusive scan of the chunk counts (one workgroup) = the first line of each chunk
+//   k_nl_scan_*     exclusive scan of the chunk counts (two levels) = the first line of each chunk
 //   k_parse_chunk   per 4 KiB chunk again: each thread's 16 bytes, a workgroup scan of their '\n'
 //                   counts, and every line that STARTS in those bytes parsed by that thread: its index
 //                   is the chunk's first line + the '\n's before it, so no line-offset array is
@@ -54,18 +54,15 @@ __global__ __launch_bounds__(256) void k_nl_count(const char* __restrict__ t, ui
     if (threadIdx.x == 0) cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-// exclusive scan of the chunk counts in one 1024-thread workgroup: each thread a contiguous run of
-// counts, a shuffle scan of the runs' sums (a serial pass over 1024 partials by one thread cost
-// ~100 us per 2^24 lines)
-__global__ __launch_bounds__(1024) void k_nl_scan(const uint32_t* __restrict__ cnt, uint64_t* __restrict__ off, uint32_t nb) {
-    __shared__ unsigned long long wsum[16];
-    const uint32_t per = (nb + blockDim.x - 1) / blockDim.x;
-    const uint32_t lo = min(threadIdx.x * per, nb), hi = min(lo + per, nb);
-    unsigned long long s = 0;
-#pragma unroll 8
-    for (uint32_t i = lo; i < hi; ++i) s += cnt[i];
+// exclusive scan of the chunk counts in two levels: k_nl_scan_local scans 1024 chunks per
+// workgroup (one chunk per thread) into off[] and writes each group's total; k_nl_scan_top scans
+// the group totals (one workgroup) into gpre[] and writes the line count off[nb]; k_parse_chunk
+// adds its group's gpre. (One 1024-thread workgroup scanning every count cost 45 us per 2^24 lines.)
+constexpr int kScanGroup = 1024;
+__device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long x, unsigned long long* wsum,
+                                                              unsigned long long* total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    unsigned long long incl = s;
+    unsigned long long incl = x;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const unsigned long long y = __shfl_up(incl, o, 64);
@@ -73,12 +70,40 @@ __global__ __launch_bounds__(1024) void k_nl_scan(const uint32_t* __restrict__ c
     }
     if (lane == 63) wsum[wid] = incl;
     __syncthreads();
-    unsigned long long wbase = 0;
-    for (int w = 0; w < wid; ++w) wbase += wsum[w];
-    unsigned long long run = wbase + incl - s;
-    if (threadIdx.x == blockDim.x - 1) off[nb] = wbase + incl;
-#pragma unroll 8
-    for (uint32_t i = lo; i < hi; ++i) { off[i] = run; run += cnt[i]; }
+    unsigned long long wbase = 0, all = 0;
+    const int nw = (int)(blockDim.x >> 6);
+    for (int w = 0; w < nw; ++w) {
+        if (w < wid) wbase += wsum[w];
+        all += wsum[w];
+    }
+    *total = all;
+    return wbase + incl - x;
+}
+
+__global__ __launch_bounds__(kScanGroup) void k_nl_scan_local(const uint32_t* __restrict__ cnt, uint64_t* __restrict__ off,
+                                                               unsigned long long* __restrict__ gsum, uint32_t nb) {
+    __shared__ unsigned long long wsum[kScanGroup / 64];
+    const uint32_t c = blockIdx.x * kScanGroup + threadIdx.x;
+    unsigned long long total = 0;
+    const unsigned long long ex = block_excl_scan(c < nb ? cnt[c] : 0u, wsum, &total);
+    if (c < nb) off[c] = ex;
+    if (threadIdx.x == 0) gsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kScanGroup) void k_nl_scan_top(const unsigned long long* __restrict__ gsum,
+                                                             unsigned long long* __restrict__ gpre, uint32_t ng,
+                                                             uint64_t* __restrict__ off, uint32_t nb) {
+    __shared__ unsigned long long wsum[kScanGroup / 64];
+    unsigned long long run = 0;
+    for (uint32_t b0 = 0; b0 < ng; b0 += kScanGroup) {          // uniform
+        const uint32_t g = b0 + threadIdx.x;
+        unsigned long long total = 0;
+        const unsigned long long ex = block_excl_scan(g < ng ? gsum[g] : 0ull, wsum, &total);
+        if (g < ng) gpre[g] = run + ex;
+        run += total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) off[nb] = run;
 }
 
 __device__ __forceinline__ bool is_ws(char ch) {          // Java \s: [ \t\n\x0B\f\r]
@@ -142,9 +167,9 @@ __device__ __forceinline__ uint4 load16(const char* __restrict__ t, uint64_t n, 
 // which is text byte base + r; bytes at or past text byte n end the line). Java's rules (file header):
 // field 0 = optional sign + digits up to ONE whitespace, field 1 = optional sign + digits up to
 // whitespace / end of line, anything after field 1 ignored; every other shape is rejected, as are
-// values outside int64. Returns 1 = parsed, 0 = rejected, 2 = the line does not end inside the
-// window (the caller parses it from memory).
-enum { kF0Start, kF0Sign, kF0Dig, kSep, kF1Sign, kF1Dig, kDone, kBad };
+// values outside int64. Phase by phase (a loop per digit run, one LDS byte per step: a byte-wise
+// state machine over all six states cost ~1,200 instructions per wave-line). Returns 1 = parsed,
+// 0 = rejected, 2 = the line runs past the window (the caller parses it from memory).
 // overflow without a division: v * 10 + d > limit (INT64_MAX, or 2^63 for a '-' field) exactly when
 // v > limit / 10 (the same for both) or v == limit / 10 and d > limit % 10 (7, or 8)
 constexpr uint64_t kLim10 = 922337203685477580ull;
@@ -153,49 +178,46 @@ __device__ __forceinline__ bool acc_digit(uint64_t& v, uint64_t d, bool neg) {
     v = v * 10 + d;
     return true;
 }
-__device__ __forceinline__ int scan_window(const uint8_t* w, int r, uint64_t base, uint64_t n, int64_t* x, int64_t* y) {
-    int st = kF0Start;
-    bool neg0 = false, neg1 = false;
-    uint64_t v0 = 0, v1 = 0;
-    // a 4-byte LDS word per step (one read per 4 bytes instead of per byte)
-    for (int j = r >> 2; j < 12 && st < kDone; ++j) {
-        const uint32_t word = reinterpret_cast<const uint32_t*>(w)[j];
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int p = 4 * j + b;
-            if (p < r || st >= kDone) continue;
-            const uint32_t c = (base + p < n) ? ((word >> (8 * b)) & 0xFFu) : (uint32_t)'\n';
-            const bool dig = c >= '0' && c <= '9';
-            const bool ws = c == ' ' || c == '\t' || c == '\n' || c == 0x0B || c == '\f' || c == '\r';
-            const bool sign = c == '+' || c == '-';
-            const uint64_t d = c - '0';
-            switch (st) {
-            case kF0Start: st = dig ? kF0Dig : sign ? kF0Sign : kBad; neg0 = c == '-'; v0 = dig ? d : 0; break;
-            case kF0Sign: st = dig ? kF0Dig : kBad; v0 = d; break;
-            case kF0Dig:
-                if (dig) {
-                    if (!acc_digit(v0, d, neg0)) st = kBad;
-                } else {
-                    st = (ws && c != '\n') ? kSep : kBad;      // "123\n": no field 1
-                }
-                break;
-            case kSep: st = dig ? kF1Dig : sign ? kF1Sign : kBad; neg1 = c == '-'; v1 = dig ? d : 0; break;
-            case kF1Sign: st = dig ? kF1Dig : kBad; v1 = d; break;
-            case kF1Dig:
-                if (dig) {
-                    if (!acc_digit(v1, d, neg1)) st = kBad;
-                } else {
-                    st = ws ? kDone : kBad;
-                }
-                break;
-            }
-        }
+constexpr uint32_t kPastWindow = 0x100u;
+// the window byte q (an LDS byte read; a one-word cache, an LDS read per 4 bytes, measured slower:
+// 0.47 vs 0.43 ms per 2^24 lines)
+struct WinReader {
+    const uint8_t* w;
+    uint64_t base, n;
+    __device__ __forceinline__ uint32_t at(int q) const {
+        if (q >= 48) return kPastWindow;
+        return base + (uint64_t)q < n ? (uint32_t)w[q] : (uint32_t)'\n';
     }
-    if (st == kBad) return 0;
-    if (st != kDone) return 2;
-    *x = neg0 ? (int64_t)(0 - v0) : (int64_t)v0;
-    *y = neg1 ? (int64_t)(0 - v1) : (int64_t)v1;
+};
+// one field: optional sign and >= 1 digits from window byte *p; on return *p is the byte after the
+// digits and *c that byte. 1 = ok, 0 = rejected, 2 = past the window
+__device__ __forceinline__ int scan_field(WinReader& rd, int* p, uint32_t* c, int64_t* out) {
+    uint32_t ch = rd.at(*p);
+    bool neg = false;
+    if (ch == '+' || ch == '-') { neg = ch == '-'; ch = rd.at(++*p); }
+    if (ch >= kPastWindow) return 2;
+    if (ch - '0' > 9u) return 0;
+    uint64_t v = 0;
+    while (ch - '0' <= 9u) {
+        if (!acc_digit(v, ch - '0', neg)) return 0;
+        ch = rd.at(++*p);
+    }
+    if (ch >= kPastWindow) return 2;
+    *c = ch;
+    *out = neg ? (int64_t)(0 - v) : (int64_t)v;
     return 1;
+}
+__device__ __forceinline__ int scan_window(const uint8_t* w, int r, uint64_t base, uint64_t n, int64_t* x, int64_t* y) {
+    WinReader rd{w, base, n};
+    int p = r;
+    uint32_t c = 0;
+    int k = scan_field(rd, &p, &c, x);
+    if (k != 1) return k;
+    if (!(c == ' ' || c == '\t' || c == 0x0B || c == '\f' || c == '\r')) return 0;   // ONE separator, not '\n'
+    ++p;
+    k = scan_field(rd, &p, &c, y);
+    if (k != 1) return k;
+    return (c == ' ' || c == '\t' || c == '\n' || c == 0x0B || c == '\f' || c == '\r') ? 1 : 0;  // field 1 ends at whitespace
 }
 
 // One 4 KiB chunk per workgroup, 16 bytes per thread, staged in LDS with the 32 bytes after the
@@ -204,6 +226,7 @@ __device__ __forceinline__ int scan_window(const uint8_t* w, int r, uint64_t bas
 // memory); line index = the chunk's first line (off, the scan of k_nl_count) + the '\n's before it.
 template <typename IdT>
 __global__ __launch_bounds__(256) void k_parse_chunk(const char* __restrict__ t, uint64_t n, const uint64_t* __restrict__ off,
+                                                     const unsigned long long* __restrict__ gpre,
                                                      IdT* __restrict__ src, IdT* __restrict__ dst,
                                                      unsigned long long* __restrict__ bad_line) {
     __shared__ uint4 s_text[kChunk / 16 + 2];
@@ -234,7 +257,7 @@ __global__ __launch_bounds__(256) void k_parse_chunk(const char* __restrict__ t,
     __syncthreads();
     uint32_t wbase = 0;
     for (int w = 0; w < wid; ++w) wbase += ws[w];
-    uint64_t i = off[blockIdx.x] + wbase + incl - c;           // '\n's before this thread's bytes
+    uint64_t i = off[blockIdx.x] + gpre[blockIdx.x / kScanGroup] + wbase + incl - c;   // '\n's before this thread's bytes
     const uint8_t* win = reinterpret_cast<const uint8_t*>(s_text) + threadIdx.x * 16;
     auto one = [&](int r, uint64_t li) {
         int64_t x = 0, y = 0;
@@ -268,6 +291,9 @@ struct ParseScratch {
     size_t chunks_cap = 0;
     unsigned long long* bad = nullptr;
     unsigned long long* hbad = nullptr;  // pinned: [bad line, '\n' count]
+    unsigned long long* gsum = nullptr;  // per 1024-chunk group: '\n' total, then its prefix (gpre)
+    unsigned long long* gpre = nullptr;
+    size_t groups_cap = 0;
 };
 constexpr int kMaxParseDevices = 64;
 thread_local ParseScratch t_scratch[kMaxParseDevices];
@@ -313,6 +339,13 @@ extern "C" int gs_parse_edges(const char* text, uint64_t n_bytes, uint32_t id_bi
         GS_TRY(grow(reinterpret_cast<void**>(&sc.off), &c2, ((size_t)nb + 2) * 8));
         sc.chunks_cap = (size_t)nb + 1;
     }
+    const uint32_t ng = (nb + kScanGroup - 1) / kScanGroup;
+    if (sc.groups_cap < ng) {
+        size_t c1 = sc.groups_cap * 8, c2 = sc.groups_cap * 8;
+        GS_TRY(grow(reinterpret_cast<void**>(&sc.gsum), &c1, (size_t)ng * 8));
+        GS_TRY(grow(reinterpret_cast<void**>(&sc.gpre), &c2, (size_t)ng * 8));
+        sc.groups_cap = ng;
+    }
     if (!sc.bad) {
         size_t c = 0;
         GS_TRY(grow(reinterpret_cast<void**>(&sc.bad), &c, 8));
@@ -323,7 +356,9 @@ extern "C" int gs_parse_edges(const char* text, uint64_t n_bytes, uint32_t id_bi
     }
     GS_HIP(hipMemsetAsync(sc.bad, 0xFF, 8, s));
     hipLaunchKernelGGL(k_nl_count, dim3(nb), dim3(256), 0, s, dtext, n_bytes, sc.cnt);
-    hipLaunchKernelGGL(k_nl_scan, dim3(1), dim3(1024), 0, s, sc.cnt, sc.off, nb);
+    hipLaunchKernelGGL(k_nl_scan_local, dim3(ng), dim3(kScanGroup), 0, s, sc.cnt, sc.off, sc.gsum, nb);
+    hipLaunchKernelGGL(k_nl_scan_top, dim3(1), dim3(kScanGroup), 0, s, (const unsigned long long*)sc.gsum, sc.gpre, ng,
+                       sc.off, nb);
     GS_HIP(hipGetLastError());
     char last = '\n';
     GS_HIP(hipMemcpyAsync(&sc.hbad[1], sc.off + nb, 8, hipMemcpyDeviceToHost, s));
@@ -348,11 +383,11 @@ extern "C" int gs_parse_edges(const char* text, uint64_t n_bytes, uint32_t id_bi
         }
     }
     if (id_bits == 32)
-        hipLaunchKernelGGL(k_parse_chunk<uint32_t>, dim3(nb), dim3(256), 0, s, dtext, n_bytes, sc.off, (uint32_t*)dsrc,
-                           (uint32_t*)ddst, sc.bad);
+        hipLaunchKernelGGL(k_parse_chunk<uint32_t>, dim3(nb), dim3(256), 0, s, dtext, n_bytes, sc.off,
+                           (const unsigned long long*)sc.gpre, (uint32_t*)dsrc, (uint32_t*)ddst, sc.bad);
     else
-        hipLaunchKernelGGL(k_parse_chunk<int64_t>, dim3(nb), dim3(256), 0, s, dtext, n_bytes, sc.off, (int64_t*)dsrc,
-                           (int64_t*)ddst, sc.bad);
+        hipLaunchKernelGGL(k_parse_chunk<int64_t>, dim3(nb), dim3(256), 0, s, dtext, n_bytes, sc.off,
+                           (const unsigned long long*)sc.gpre, (int64_t*)dsrc, (int64_t*)ddst, sc.bad);
     int rc = GS_OK;
     if (hipGetLastError() != hipSuccess) rc = fail(GS_ERR_HIP, "gs_parse_edges: k_parse_chunk launch failed");
     if (rc == GS_OK && hipMemcpyAsync(&sc.hbad[0], sc.bad, 8, hipMemcpyDeviceToHost, s) != hipSuccess)
