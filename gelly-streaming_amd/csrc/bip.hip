@@ -22,13 +22,6 @@
 // hook re-finds both roots), path halving is a no-return atomicMin of a packed word (the packed
 // order is the parent order, and the parity to a given ancestor is unique, so any two writers
 // agree on it), a walk treats a word that is not below its index (a stale kInvalid) as a root.
-//
-// Giant filter (as the CC path's gbits, round 4): every close writes, per 32 vertices, a membership
-// word (root == the giant's root) and a parity word (parity relative to that root), for the giant
-// picked by the close before from 1024 sampled roots. An edge whose endpoints are both members is
-// decided from the two parity bits alone: opposite = nothing to do, equal = an odd cycle. Valid
-// until reset however stale, as components only merge (members stay members) and a later root
-// change shifts every member's parity by the same bit.
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -43,7 +36,6 @@ struct BipArgs {
     uint32_t* w;
     uint32_t cap;
     uint32_t* flags;      // flags[0]: bit 0 range error; flags[1]: 1 = odd cycle seen (not bipartite)
-    const uint2* gw = nullptr;   // giant filter: (membership, parity) bits per 32 vertices, or null
 };
 
 // (root, parity of x relative to root) given wx = a read of w[x]
@@ -72,14 +64,6 @@ __device__ __forceinline__ uint32_t bip_make(uint32_t* __restrict__ w, uint32_t 
 
 // require parity(u) ^ parity(v) == rel (1 for an edge)
 __device__ __forceinline__ void bip_union(const BipArgs& a, uint32_t u, uint32_t v, uint32_t rel) {
-    if (a.gw && u != v) {                             // both in the giant: the parity bits decide
-                                                      // (a self-loop only adds its vertex, below)
-        const uint2 gu = a.gw[u >> 5], gv = a.gw[v >> 5];
-        if ((gu.x >> (u & 31)) & (gv.x >> (v & 31)) & 1u) {
-            if ((((gu.y >> (u & 31)) ^ (gv.y >> (v & 31))) & 1u) != rel) atomicOr(&a.flags[1], 1u);
-            return;
-        }
-    }
     uint32_t wu = bip_make(a.w, u);
     if (u == v) return;                               // self-loop: makeSet only
     uint32_t wv = bip_make(a.w, v);
@@ -158,89 +142,21 @@ __global__ __launch_bounds__(256) void k_bip_merge(const uint32_t* __restrict__ 
     }
 }
 
-// Merger emission: full compression (only v's thread writes w[v]; read-only walks), and the giant
-// filter's words for the giant root gst[0] picked by the last close (kInvalid: none; the words are
-// then all zero). A workgroup takes 1024 consecutive vertices per step (4 per thread, 256 apart), so
-// the 32 membership / parity words of those vertices are its own: wave ballots, plain stores. The
-// roots at kBipSamples evenly spaced ids go to samp for k_bip_pick.
-constexpr uint32_t kBipSamples = 1024;
-__global__ __launch_bounds__(256) void k_bip_compress(uint32_t* __restrict__ w, uint32_t n, uint2* __restrict__ gw,
-                                                      const uint32_t* __restrict__ gst, uint32_t* __restrict__ samp) {
-    __shared__ uint32_t s_g;
-    if (threadIdx.x == 0) {
-        uint32_t g = gst ? gst[0] : kInvalid;
-        if (g != kInvalid && g < n) {                 // the picked root's current root (read-only walk)
-            uint32_t wg = w[g];
-            while (wg != kInvalid && (wg >> 1) < g) { g = wg >> 1; wg = w[g]; }
-        } else {
-            g = kInvalid;
+// Merger emission: full compression (only v's thread writes w[v]; read-only walks)
+__global__ __launch_bounds__(256) void k_bip_compress(uint32_t* __restrict__ w, uint32_t n) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += stride) {
+        const uint32_t wv = w[v];
+        if (wv == kInvalid || (wv >> 1) == v) continue;
+        uint32_t cur = wv >> 1, par = wv & 1u, wc = w[cur];
+        while ((wc >> 1) < cur) {
+            par ^= wc & 1u;
+            cur = wc >> 1;
+            wc = w[cur];
         }
-        s_g = g;
+        const uint32_t nw = (cur << 1) | par;
+        if (nw != wv) w[v] = nw;
     }
-    __syncthreads();
-    const uint32_t g = s_g;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t sstride = max(1u, n / kBipSamples);
-    for (uint64_t blk = (uint64_t)blockIdx.x * 1024; blk < n; blk += (uint64_t)gridDim.x * 1024) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint64_t v64 = blk + 256 * k + threadIdx.x;
-            const uint32_t v = (uint32_t)v64;
-            uint32_t root = kInvalid, par = 0;
-            if (v64 < n) {
-                const uint32_t wv = w[v];
-                if (wv != kInvalid) {
-                    root = wv >> 1;
-                    par = wv & 1u;
-                    if (root != v) {
-                        uint32_t cur = root, wc = w[cur];
-                        while ((wc >> 1) < cur) {
-                            par ^= wc & 1u;
-                            cur = wc >> 1;
-                            wc = w[cur];
-                        }
-                        root = cur;
-                        const uint32_t nw = (cur << 1) | par;
-                        if (nw != wv) w[v] = nw;
-                    }
-                }
-                if (samp && v % sstride == 0 && v / sstride < kBipSamples) samp[v / sstride] = root;
-            }
-            if (gw) {
-                const uint64_t mem = __ballot(root == g && g != kInvalid);
-                const uint64_t pb = __ballot(root == g && g != kInvalid && par);
-                const uint64_t word = (blk + 256 * k + 64 * wid) >> 5;     // 2 words per wave
-                if ((lane & 31) == 0 && blk + 256 * k + 64 * wid + lane < n)
-                    gw[word + (lane >> 5)] = make_uint2((uint32_t)(mem >> lane), (uint32_t)(pb >> lane));
-            }
-        }
-    }
-}
-
-// The giant for the next close's filter words: the most frequent root among the samples, if it holds
-// at least 1/16 of them (else none). One workgroup, an LDS hash count.
-__global__ __launch_bounds__(1024) void k_bip_pick(const uint32_t* __restrict__ samp, uint32_t* __restrict__ gst) {
-    constexpr int kSlots = 2048;
-    __shared__ uint32_t key[kSlots], cnt[kSlots];
-    __shared__ unsigned long long best;
-    for (int i = threadIdx.x; i < kSlots; i += blockDim.x) { key[i] = kInvalid; cnt[i] = 0; }
-    if (threadIdx.x == 0) best = 0;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < kBipSamples; i += blockDim.x) {
-        const uint32_t r = samp[i];
-        if (r == kInvalid) continue;
-        uint32_t h = (r * 0x9E3779B1u) >> 21;          // 11 bits
-        for (;;) {
-            const uint32_t old = atomicCAS(&key[h], kInvalid, r);
-            if (old == kInvalid || old == r) { atomicAdd(&cnt[h], 1u); break; }
-            h = (h + 1) & (kSlots - 1);
-        }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kSlots; i += blockDim.x)
-        if (cnt[i]) atomicMax(&best, ((unsigned long long)cnt[i] << 32) | key[i]);
-    __syncthreads();
-    if (threadIdx.x == 0) gst[0] = (best >> 32) >= kBipSamples / 16 ? (uint32_t)best : kInvalid;
 }
 
 // n_vertices, n_components, checksum over (v, key << 1 | sign) of every vertex in the summary
@@ -361,19 +277,11 @@ struct gs_bip {
     size_t stage_bytes = 0;
     uint64_t edges_since_reset = 0;
     bool compressed = true;
-    uint2* gw = nullptr;                       // giant filter words (membership, parity) per 32 vertices
-    uint32_t* gst = nullptr;                   // [0] the giant root the next close builds them for
-    uint32_t* samp = nullptr;                  // kBipSamples sampled roots of the last close
-    bool gw_valid = false;                     // a close has written gw since reset
 };
 
 namespace {
 
-BipArgs bargs(gs_bip_t* h) {
-    BipArgs a{h->w, h->cap, h->flags};
-    a.gw = h->gw_valid ? h->gw : nullptr;
-    return a;
-}
+BipArgs bargs(gs_bip_t* h) { return BipArgs{h->w, h->cap, h->flags}; }
 
 int bcheck(gs_bip_t* h) { return h ? GS_OK : fail(GS_ERR_INVALID, "null handle"); }
 
@@ -400,11 +308,8 @@ int bsync(gs_bip_t* h, int* bipartite) {
 
 int bcompress(gs_bip_t* h) {
     if (h->compressed) return GS_OK;
-    hipLaunchKernelGGL(k_bip_compress, dim3(bgrid(h->cap, 1024, 4096)), dim3(256), 0, h->stream, h->w, h->cap, h->gw,
-                       (const uint32_t*)h->gst, h->samp);
-    hipLaunchKernelGGL(k_bip_pick, dim3(1), dim3(1024), 0, h->stream, (const uint32_t*)h->samp, h->gst);
+    hipLaunchKernelGGL(k_bip_compress, dim3(bgrid(h->cap, 256, 16384)), dim3(256), 0, h->stream, h->w, h->cap);
     GS_HIP(hipGetLastError());
-    h->gw_valid = true;
     h->compressed = true;
     return GS_OK;
 }
@@ -494,8 +399,6 @@ int gs_bip_create(gs_bip_t** out, uint64_t vertex_capacity, uint32_t id_bits, in
     if (hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess) return bail(fail(GS_ERR_HIP, "hipStreamCreate failed"));
     h->stream = h->own;
     if (hipMalloc(&h->w, (size_t)h->cap * 4) != hipSuccess || hipMalloc(&h->flags, 16) != hipSuccess ||
-        hipMalloc(&h->gw, ((size_t)h->cap + 31) / 32 * sizeof(uint2)) != hipSuccess ||
-        hipMalloc(&h->gst, 128) != hipSuccess || hipMalloc(&h->samp, kBipSamples * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&h->dscr, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&h->hscr, 8 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
@@ -513,7 +416,7 @@ int gs_bip_destroy(gs_bip_t* h) {
     DeviceGuard g(h->device);
     if (h->own) (void)hipStreamSynchronize(h->own);
     if (h->stream && h->stream != h->own) (void)hipStreamSynchronize(h->stream);
-    for (void* p : {(void*)h->w, (void*)h->flags, (void*)h->dscr, h->tmp, h->stage, (void*)h->gw, (void*)h->gst, (void*)h->samp})
+    for (void* p : {(void*)h->w, (void*)h->flags, (void*)h->dscr, h->tmp, h->stage})
         if (p) (void)hipFree(p);
     if (h->hscr) (void)hipHostFree(h->hscr);
     if (h->own) (void)hipStreamDestroy(h->own);
@@ -526,10 +429,8 @@ int gs_bip_reset(gs_bip_t* h) {
     DeviceGuard g(h->device);
     GS_HIP(hipMemsetAsync(h->w, 0xFF, (size_t)h->cap * 4, h->stream));
     GS_HIP(hipMemsetAsync(h->flags, 0, 16, h->stream));
-    GS_HIP(hipMemsetAsync(h->gst, 0xFF, 128, h->stream));     // no giant: the next close builds empty words
     h->edges_since_reset = 0;
     h->compressed = true;
-    h->gw_valid = false;
     return GS_OK;
 }
 
