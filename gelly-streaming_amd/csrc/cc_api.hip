@@ -302,6 +302,7 @@ struct DebugEnv {
     int small_ept = kSmallEpt;                      // GSGPU_SMALL_EPT: ...take this many edges per thread
     uint64_t young_first_min = kYoungFirstMinWg;    // GSGPU_YOUNG_FIRST_MIN: workgroup floor of the first young launch
     bool list_close = true;                         // GSGPU_LIST_CLOSE=0: no list-mode closes (A/B)
+    bool small_claim = true;                        // GSGPU_SMALL_CLAIM=0: small k_fold launches without claims (A/B)
     DebugEnv() {
         const char* e = getenv("GSGPU_FOLD_STATS");
         fold_stats = e && atoi(e) != 0;
@@ -320,6 +321,8 @@ struct DebugEnv {
         if (e && *e) small_ept = atoi(e) == 1 ? 1 : (atoi(e) == 2 ? 2 : 4);
         e = getenv("GSGPU_LIST_CLOSE");
         if (e && *e) list_close = atoi(e) != 0;
+        e = getenv("GSGPU_SMALL_CLAIM");
+        if (e && *e) small_claim = atoi(e) != 0;
 
     }
 };
@@ -374,6 +377,7 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
     // one-edge-per-thread mature SoA folds log their first touches (touch-log slots) for a list-mode
     // close; any other fold makes the next close a bitmap or full one
     const uint32_t waves = grid * (kFoldThreads / 64);
+    const uint32_t claim = (!young && ept == 1 && dbg().small_claim) ? 1u : 0u;
     if (h->lctl && !young && !AOS && !h->dbits && dbg().list_close && ept == 1 && !persist &&
         (uint64_t)grid * kFoldThreads >= n && h->ilist_slots + waves <= kTlogSlots) {
         f.tlog = h->tlog[h->closes & 1] + (size_t)h->ilist_slots * kSlotWords;
@@ -391,7 +395,7 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
     KTimer t(h, h->fold_timer, n);
 #define GS_LAUNCH_FOLD(MARKV, VECV, EPTV, STV)                                                                       \
     klaunch((k_fold<IdT, AOS, MARKV, VECV, EPTV, STV>), dim3(grid), dim3(kFoldThreads), h->stream, t.start(), t.stop(), \
-            (const IdT*)a, (const IdT*)b, f)
+            (const IdT*)a, (const IdT*)b, f, claim)
     if (h->dstats) { if (h->mark) GS_LAUNCH_FOLD(true, false, 4, true); else GS_LAUNCH_FOLD(false, false, 4, true); }
     else if (ept == kYoungEpt) { if (h->mark) GS_LAUNCH_FOLD(true, false, kYoungEpt, false); else GS_LAUNCH_FOLD(false, false, kYoungEpt, false); }
     else if (ept == 1) { if (h->mark) GS_LAUNCH_FOLD(true, false, 1, false); else GS_LAUNCH_FOLD(false, false, 1, false); }

@@ -710,11 +710,67 @@ __device__ __forceinline__ void union_group_g(const FoldArgs& f, const uint32_t 
     }
 }
 
+// union_group_g for k_fold's small mature folds (f.claim): the same claims and gR stand-ins, plus
+// the touch log of a logging fold (first touches, claims included). A separate copy so that the
+// ring fold's code is not touched.
+template <bool MARK, bool STATS, int EPT>
+__device__ __forceinline__ void union_group_gl(const FoldArgs& f, const uint32_t (&u)[EPT], const uint32_t (&v)[EPT],
+                                               const bool (&ok)[EPT], const uint32_t (&gflag)[EPT], uint32_t gR,
+                                               FoldStats& st) {
+    uint32_t pu[EPT], pv[EPT];
+    bool claimed[EPT];
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        const bool cu = ok[k] && gflag[k] == 2u && u[k] > gR;      // v in the giant, u outside
+        const bool cv = ok[k] && gflag[k] == 1u && v[k] > gR;      // u in the giant, v outside
+        pu[k] = !ok[k] ? 0u : (gflag[k] & 1u) ? gR : cu ? atomicCAS(&f.parent[u[k]], kInvalid, gR) : f.parent[u[k]];
+        pv[k] = !ok[k] ? 0u : (gflag[k] & 2u) ? gR : cv ? atomicCAS(&f.parent[v[k]], kInvalid, gR) : f.parent[v[k]];
+        claimed[k] = (cu && pu[k] == kInvalid) || (cv && pv[k] == kInvalid);
+    }
+    uint32_t m[EPT];
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        if (claimed[k]) {
+            const uint32_t x = (gflag[k] == 2u) ? u[k] : v[k];
+            set_seen(f.sbits, x);                    // (a first touch: the seen bit, and the log)
+            if (STATS) { ++st.inits; ++st.hooks; }
+        }
+    }
+    if (f.tlog) {
+        NewV nl[EPT];
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            if (claimed[k]) {
+                nl[k].a = (gflag[k] == 2u) ? u[k] : v[k];
+                m[k] = MARK ? nl[k].a : kInvalid;
+            } else {
+                m[k] = ok[k] ? union_edge<MARK, STATS>(f.parent, f.sbits, u[k], v[k], pu[k], pv[k], &st, f.halve != 0,
+                                                       f.hbits, &nl[k]) : kInvalid;
+            }
+        }
+        uint32_t t[2 * EPT];
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            t[2 * k] = nl[k].a;
+            t[2 * k + 1] = nl[k].b;
+        }
+        slot_append<2 * EPT>(f.tlog, f.tcnt, t);
+    } else {
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            if (claimed[k]) m[k] = MARK ? ((gflag[k] == 2u) ? u[k] : v[k]) : kInvalid;
+            else m[k] = ok[k] ? union_edge<MARK, STATS>(f.parent, f.sbits, u[k], v[k], pu[k], pv[k], &st, f.halve != 0, f.hbits)
+                              : kInvalid;
+        }
+    }
+    if (MARK) log_append<EPT>(f.mark, f.mark_len, m);
+}
+
 // Filter, parent gathers and unions of one thread's EPT edges (ids already range-checked;
 // ok[k] false = nothing to do for edge k).
 template <bool MARK, bool STATS, int EPT>
 __device__ __forceinline__ void fold_group(const FoldArgs& f, bool filt, uint32_t (&u)[EPT], uint32_t (&v)[EPT],
-                                           bool (&ok)[EPT], FoldStats& st) {
+                                           bool (&ok)[EPT], FoldStats& st, uint32_t claim_gR) {
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
         if (!ok[k]) { u[k] = 0; v[k] = 0; }
@@ -723,7 +779,8 @@ __device__ __forceinline__ void fold_group(const FoldArgs& f, bool filt, uint32_
     if (STATS) for (int k = 0; k < EPT; ++k) nvalid += ok[k];
     uint32_t gflag[EPT];
     if (filt) filter_group<STATS, EPT, false>(f, u, v, ok, nullptr, HotArgs{nullptr, 0, nullptr}, false, false, ~0ull, gflag);
-    union_group<MARK, STATS, EPT>(f, u, v, ok, st);
+    if (EPT == 1 && filt && claim_gR != kInvalid) union_group_gl<MARK, STATS, EPT>(f, u, v, ok, gflag, claim_gR, st);
+    else union_group<MARK, STATS, EPT>(f, u, v, ok, st);
     if (STATS) {
         for (int k = 0; k < EPT; ++k) nfilt += ok[k];
         atomicAdd(&f.stats[0], (unsigned long long)nvalid);
@@ -734,7 +791,7 @@ __device__ __forceinline__ void fold_group(const FoldArgs& f, bool filt, uint32_
 // One thread's EPT edges starting at edge g * EPT: load, range-check, filter, union.
 template <typename IdT, bool AOS, bool MARK, bool VEC, int EPT, bool STATS>
 __device__ __forceinline__ void fold_edges_at(const IdT* __restrict__ a, const IdT* __restrict__ b, const FoldArgs& f,
-                                              bool filt, uint64_t g, FoldStats& st) {
+                                              bool filt, uint64_t g, FoldStats& st, uint32_t claim_gR) {
     const uint64_t n = f.n;
     const uint64_t e0 = g * EPT;
     uint32_t u[EPT], v[EPT];
@@ -776,7 +833,7 @@ __device__ __forceinline__ void fold_edges_at(const IdT* __restrict__ a, const I
         }
     }
     if (bad) atomicOr(f.rc.err, 1u);
-    fold_group<MARK, STATS, EPT>(f, filt, u, v, ok, st);
+    fold_group<MARK, STATS, EPT>(f, filt, u, v, ok, st, claim_gR);
 }
 
 // UpdateCC over a batch. Each thread takes EPT consecutive edges per pass: endpoint reads are
@@ -788,7 +845,7 @@ __device__ __forceinline__ void fold_edges_at(const IdT* __restrict__ a, const I
 // flight at any time (what bounds the hub contention) without a launch boundary per chunk.
 template <typename IdT, bool AOS, bool MARK, bool VEC, int EPT = kEdgesPerThread, bool STATS = false>
 __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a, const IdT* __restrict__ b,
-                                                       FoldArgs f) {
+                                                       FoldArgs f, uint32_t claim) {
     const uint64_t n = f.n;
     const bool filt = *f.giant != kInvalid;          // wave-uniform
     // no giant yet: the close after this launch is a full pass (k_compress: the slot this launch
@@ -797,6 +854,9 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
     // giant forms: ~1 M memory-side atomics per 2^20-edge window)
     if (!filt) f.sbits = nullptr;
     else f.hbits = nullptr;                          // (hooked roots are marked only before a giant)
+    // small mature folds (claim): survivors next to the giant claim under the root gbits were built
+    // for, as in the ring fold (ids < 2^31)
+    const uint32_t claim_gR = (claim && filt && f.rc.cap <= 0x80000000u) ? f.giant[1] : kInvalid;
     // logging fold (ListCtl): this wave's touch-log slot
     __shared__ uint32_t s_tcnt[kFoldThreads / 64];
     const uint32_t wave = threadIdx.x >> 6;
@@ -816,12 +876,12 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
             __syncthreads();
             if (base >= groups) break;
             const uint64_t g = base + threadIdx.x;
-            if (g < groups) fold_edges_at<IdT, AOS, MARK, VEC, EPT, STATS>(a, b, f, filt, g, st);
+            if (g < groups) fold_edges_at<IdT, AOS, MARK, VEC, EPT, STATS>(a, b, f, filt, g, st, claim_gR);
         }
     } else {
         const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
         for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += stride)
-            fold_edges_at<IdT, AOS, MARK, VEC, EPT, STATS>(a, b, f, filt, g, st);
+            fold_edges_at<IdT, AOS, MARK, VEC, EPT, STATS>(a, b, f, filt, g, st, claim_gR);
     }
     if (f.tlog && (threadIdx.x & 63) == 0) f.tlog[0] = s_tcnt[wave];   // every slot's count, 0 included
     if (STATS) {
