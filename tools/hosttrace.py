@@ -5,7 +5,8 @@ kernels of the run's last stretch, splits every gap between consecutive kernels 
   dispatch  : the call returned before that (the GPU-side launch latency of a dependent kernel).
 Also sums the host's blocking calls (event / stream synchronisation) over the same stretch.
 
-usage: python tools/hosttrace.py <rocprofv3 output dir> [kernels to analyse, default 6000]
+usage: python tools/hosttrace.py <rocprofv3 output dir> [kernels to analyse, default 6000 | first:last]
+(first:last = a slice of the kernels sorted by start time, e.g. one timed step)
 """
 import csv
 import glob
@@ -31,14 +32,18 @@ def short(name):
 
 def main():
     d = sys.argv[1]
-    last = int(sys.argv[2]) if len(sys.argv) > 2 else 6000
+    sel = sys.argv[2] if len(sys.argv) > 2 else "6000"
     ks = rows(os.path.join(d, "**", "*kernel_trace.csv"))
     api = rows(os.path.join(d, "**", "*hip_api_trace.csv"))
     by_corr = {}
     for r in api:
         by_corr[int(r["Correlation_Id"])] = r
     ks.sort(key=lambda r: int(r["Start_Timestamp"]))
-    ks = ks[-last:]
+    if ":" in sel:
+        lo, hi = (int(x) for x in sel.split(":"))
+        ks = ks[lo:hi]
+    else:
+        ks = ks[-int(sel):]
     t_lo, t_hi = int(ks[0]["Start_Timestamp"]), int(ks[-1]["End_Timestamp"])
     busy = sum(int(k["End_Timestamp"]) - int(k["Start_Timestamp"]) for k in ks)
     late = defaultdict(lambda: [0, 0])          # kernel name -> [ns the GPU waited for the host, count]
