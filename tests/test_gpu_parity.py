@@ -807,3 +807,72 @@ def test_parse_edges_long_lines_extremes_and_device_text(torch_cuda):
     assert _java_parse(bad) == n
     with pytest.raises(GsError):
         parse_edges(bad, id_bits=64)
+
+
+def _dev_parse(torch, text, id_bits=64, cap=None):
+    """gs_parse_edges with device text and device outputs (the one-pass look-back kernel)."""
+    import ctypes
+    from gsgpu._abi import call
+    buf = torch.frombuffer(bytearray(text), dtype=torch.uint8).cuda()
+    cap = (text.count(b"\n") + 1) if cap is None else cap
+    dt = torch.int64 if id_bits == 64 else torch.int32
+    ps = torch.full((max(cap, 1),), -7, dtype=dt, device="cuda")
+    pd = torch.full((max(cap, 1),), -7, dtype=dt, device="cuda")
+    cnt = ctypes.c_uint64()
+    torch.cuda.synchronize()
+    call("gs_parse_edges", ctypes.c_void_p(buf.data_ptr()), len(text), id_bits, ctypes.c_void_p(ps.data_ptr()),
+         ctypes.c_void_p(pd.data_ptr()), cap, ctypes.byref(cnt), 0, None)
+    n = cnt.value
+    return n, ps[:n].cpu().numpy().astype(np.int64), pd[:n].cpu().numpy().astype(np.int64)
+
+
+def test_parse_edges_one_pass_device_outputs(torch_cuda):
+    """The one-pass parse (chunk first lines by decoupled look-back, device outputs) against the
+    Java rules: valid forms, every rejected form at a chunk boundary, texts of 1 B to a few chunks at
+    every length class (no trailing '\\n', exactly 4096 B, one line per chunk), int32 outputs, the
+    capacity error, and ~20K chunks of RMAT text (a long look-back chain) equal to the host-output
+    (two-pass) path."""
+    from gsgpu.edgefile import parse_edges
+    torch = torch_cuda
+    text = b"1 2\n3\t4\n5 6 extra fields\n+7 -8\r\n9 10  \n" + b"".join(b"%d %d\n" % (i, i * 7 % 1000) for i in range(5000)) + b"11 12"
+    want = _java_parse(text)
+    n, s, d = _dev_parse(torch, text)
+    assert n == len(want[0])
+    np.testing.assert_array_equal(s, want[0])
+    np.testing.assert_array_equal(d, want[1])
+    for bad in (b"1  2\n", b"\n", b" 1 2\n", b"1x 2\n", b"1\n", b"1 99999999999999999999\n"):
+        head = b"".join(b"%d %d\n" % (i, i) for i in range(600))        # the bad line past chunk 0
+        t = head + bad + b"9 10\n"
+        assert _java_parse(t) == 600
+        with pytest.raises(GsError) as ei:
+            _dev_parse(torch, t)
+        assert ei.value.code == _abi.GS_ERR_INVALID and "line 601" in str(ei.value)
+    for t in (b"5 6", b"5 6\n", b"123456789 987654321", b"1 2\n" * 1024, b"1 2\n" * 1023 + b"12 3",
+              b"7 8" + b" " * 4093, (b"4 5" + b" " * 4092 + b"\n") * 3, b"1 2\n" * 3000 + b"3 4"):
+        want = _java_parse(t)
+        n, s, d = _dev_parse(torch, t)
+        assert n == len(want[0]), len(t)
+        np.testing.assert_array_equal(s, want[0])
+        np.testing.assert_array_equal(d, want[1])
+    t = b"".join(b"%d %d\n" % (i, 4000000000 - i) for i in range(9000))
+    n, s, d = _dev_parse(torch, t, id_bits=32)
+    assert n == 9000
+    np.testing.assert_array_equal(s, np.arange(9000))
+    np.testing.assert_array_equal(d & 0xFFFFFFFF, 4000000000 - np.arange(9000))
+    with pytest.raises(GsError) as ei:
+        _dev_parse(torch, t, cap=8999)
+    assert ei.value.code == _abi.GS_ERR_CAPACITY
+    rng = np.random.default_rng(5)
+    a = rng.integers(0, 1 << 24, 1 << 22)
+    b = rng.integers(0, 1 << 24, 1 << 22)
+    big = ("\n".join("%d %d" % (x, y) for x, y in zip(a.tolist(), b.tolist())) + "\n").encode()
+    n, s, d = _dev_parse(torch, big)
+    assert n == len(a)
+    np.testing.assert_array_equal(s, a)
+    np.testing.assert_array_equal(d, b)
+    part = big[: big.rfind(b"\n", 0, 1 << 20) + 1] + b"77 88"
+    hs, hd = parse_edges(part, id_bits=64)
+    n2, s2, d2 = _dev_parse(torch, part)
+    assert n2 == len(hs)
+    np.testing.assert_array_equal(s2, hs)
+    np.testing.assert_array_equal(d2, hd)

@@ -7,7 +7,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py \
-  tests/test_gpu_rows.py -k "parse" > "$OUT/pytest.log" 2>&1
+  tests/test_gpu_rows.py -k "parse" -v > "$OUT/pytest.log" 2>&1
 rc=$?; tail -1 "$OUT/pytest.log"; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" "$OUT/pytest.log" | head -20; exit 3; }
 BASE=$GRAFT_REPO_ROOT/gelly-streaming_amd/gsgpu/lib/exp/libgsgpu_base.so
 for i in 1 2 3; do
