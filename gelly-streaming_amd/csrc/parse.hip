@@ -7,16 +7,14 @@
 // which parseLong rejects), trailing whitespace is dropped by split(), fields past the second are
 // ignored, a field is an optional '+'/'-' and decimal digits within the int64 range, and any other
 // line fails the job. This file restates those rules for every line in parallel:
-//   k_parse_chunk   per 4 KiB chunk: each thread's 16 bytes, a workgroup scan of their '\n'
-//                   counts, the chunk's first line from a decoupled look-back over the chunks' status
-//                   words (device outputs: one pass over the text), and every line that STARTS in
-//                   those bytes parsed by that thread: its index is the chunk's first line + the
-//                   '\n's before it, so no line-offset array is
+//   k_nl_count      per 4 KiB chunk: number of '\n' (16-B loads)
+//   k_nl_scan_*     exclusive scan of the chunk counts (two levels) = the first line of each chunk
+//   k_parse_chunk   per 4 KiB chunk again: each thread's 16 bytes, a workgroup scan of their '\n'
+//                   counts, and every line that STARTS in those bytes parsed by that thread: its index
+//                   is the chunk's first line + the '\n's before it, so no line-offset array is
 //                   written or read (the round-3 version wrote and re-read 8 B per line: 0.54 ms of
 //                   its 1.77 ms per 2^24 lines); a bad line records its index (atomicMin) and the
 //                   host reports the first one.
-//   k_nl_count + k_nl_scan_*   host outputs only (staged at the line count, so it is needed first):
-//                   '\n' per chunk and their exclusive scan (two levels) = each chunk's first line
 // Scratch (chunk counts and offsets, the bad-line word, a device copy of host text) is kept per
 // thread and device and grown, not allocated per call.
 #include <algorithm>
@@ -238,43 +236,17 @@ __device__ __forceinline__ int scan_window(const uint8_t* w, int r, uint64_t bas
     return (c == ' ' || c == '\t' || c == '\n' || c == 0x0B || c == '\f' || c == '\r') ? 1 : 0;  // field 1 ends at whitespace
 }
 
-// Chunk status words of the one-pass parse (decoupled look-back): bits 62-63 = 0 not yet published,
-// 1 = the chunk's own '\n' count (aggregate), 2 = its inclusive prefix; bits 0-61 the value.
-constexpr uint64_t kStAgg = 1ull << 62, kStPre = 2ull << 62, kStVal = (1ull << 62) - 1;
-__device__ __forceinline__ void st_publish(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t st_read(const uint64_t* p) {
-    return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // One 4 KiB chunk per workgroup, 16 bytes per thread, staged in LDS with the 32 bytes after the
 // chunk: a thread parses every line that STARTS in its 16 bytes (after each '\n' there, and line 0
 // at byte 0) from a 48-byte window of that LDS copy (a line longer than the window is parsed from
-// memory); line index = the chunk's first line + the '\n's before it. The chunk's first line:
-//   kOnePass = false: off + gpre, the scan of k_nl_count (two passes over the text);
-//   kOnePass = true:  chunks in ticket order (an atomicAdd per workgroup, so every lower chunk is
-//                     already running), each publishes its own count, then wave 0 looks back 64
-//                     chunks at a time, summing counts up to the nearest inclusive prefix, and
-//                     publishes its own (one pass over the text; a chunk never waits on a chunk that
-//                     has not published its count, and every chunk publishes it before waiting).
-//                     Lines at or past cap are not written (the host reports the capacity error).
-template <typename IdT, bool kOnePass>
+// memory); line index = the chunk's first line (off, the scan of k_nl_count) + the '\n's before it.
+template <typename IdT>
 __global__ __launch_bounds__(256) void k_parse_chunk(const char* __restrict__ t, uint64_t n, const uint64_t* __restrict__ off,
                                                      const unsigned long long* __restrict__ gpre,
-                                                     uint64_t* __restrict__ status, uint32_t* __restrict__ ticket,
-                                                     uint64_t cap, IdT* __restrict__ src, IdT* __restrict__ dst,
+                                                     IdT* __restrict__ src, IdT* __restrict__ dst,
                                                      unsigned long long* __restrict__ bad_line) {
     __shared__ uint4 s_text[kChunk / 16 + 2];
-    __shared__ uint32_t s_chunk;
-    __shared__ uint64_t s_first;
-    uint32_t chunk = blockIdx.x;
-    if (kOnePass) {
-        if (threadIdx.x == 0) s_chunk = atomicAdd(ticket, 1u);
-        __syncthreads();
-        chunk = s_chunk;
-    }
-    const uint64_t cbase = (uint64_t)chunk * kChunk;
+    const uint64_t cbase = (uint64_t)blockIdx.x * kChunk;
     const uint64_t base = cbase + threadIdx.x * 16;
     const uint4 q = load16(t, n, base);
     s_text[threadIdx.x] = q;
@@ -301,42 +273,10 @@ __global__ __launch_bounds__(256) void k_parse_chunk(const char* __restrict__ t,
     __syncthreads();
     uint32_t wbase = 0;
     for (int w = 0; w < wid; ++w) wbase += ws[w];
-    uint64_t first;
-    if (kOnePass) {
-        if (wid == 0) {
-            const uint64_t total = (uint64_t)ws[0] + ws[1] + ws[2] + ws[3];
-            uint64_t ex = 0;
-            if (chunk == 0) {
-                if (lane == 0) st_publish(status, kStPre | total);
-            } else {
-                if (lane == 0) st_publish(status + chunk, kStAgg | total);
-                for (int64_t end = chunk;; end -= 64) {               // predecessors end-1-lane
-                    const int64_t j = end - 1 - lane;
-                    uint64_t v = kStPre;                                // before chunk 0: a zero prefix
-                    if (j >= 0)
-                        do { v = st_read(status + j); } while (v < kStAgg);
-                    const unsigned long long pm = __ballot(v >= kStPre);
-                    const int stop = pm ? __ffsll((long long)pm) - 1 : 64;  // nearest prefix
-                    uint64_t add = lane <= stop ? (v & kStVal) : 0;
-#pragma unroll
-                    for (int o = 32; o > 0; o >>= 1) add += __shfl_xor(add, o, 64);
-                    ex += add;
-                    if (pm) break;
-                }
-                if (lane == 0) st_publish(status + chunk, kStPre | (ex + total));
-            }
-            if (lane == 0) s_first = ex;
-        }
-        __syncthreads();
-        first = s_first;
-    } else {
-        first = off[chunk] + gpre[chunk / kScanGroup];
-    }
-    uint64_t i = first + wbase + incl - c;                      // '\n's before this thread's bytes
+    uint64_t i = off[blockIdx.x] + gpre[blockIdx.x / kScanGroup] + wbase + incl - c;   // '\n's before this thread's bytes
     const uint8_t* win = reinterpret_cast<const uint8_t*>(s_text) + threadIdx.x * 16;
     const bool in = base + 48 <= n;
     auto one = [&](int r, uint64_t li) {
-        if (kOnePass && li >= cap) return;
         int64_t x = 0, y = 0;
         const int k = in ? scan_window<true>(win, r, base, n, &x, &y) : scan_window<false>(win, r, base, n, &x, &y);
         if (k == 2) { parse_store<IdT>(t, n, base + r, li, src, dst, bad_line); return; }
@@ -432,76 +372,53 @@ extern "C" int gs_parse_edges(const char* text, uint64_t n_bytes, uint32_t id_bi
         }
     }
     GS_HIP(hipMemsetAsync(sc.bad, 0xFF, 8, s));
-    const bool dev_out = is_device_pointer(src) && is_device_pointer(dst);
+    hipLaunchKernelGGL(k_nl_count, dim3(nb), dim3(256), 0, s, dtext, n_bytes, sc.cnt);
+    hipLaunchKernelGGL(k_nl_scan_local, dim3(ng), dim3(kScanGroup), 0, s, sc.cnt, sc.off, sc.gsum, nb);
+    hipLaunchKernelGGL(k_nl_scan_top, dim3(1), dim3(kScanGroup), 0, s, (const unsigned long long*)sc.gsum, sc.gpre, ng,
+                       sc.off, nb);
+    GS_HIP(hipGetLastError());
     char last = '\n';
-    uint64_t lines = 0;
-    int rc = GS_OK;
-    if (dev_out) {
-        // one pass (k_parse_chunk<., true>): the chunk status words and the ticket (off[nb + 1])
-        // start at zero; the last chunk's inclusive prefix is the '\n' count
-        GS_HIP(hipMemsetAsync(sc.off, 0, ((size_t)nb + 2) * 8, s));
-        uint32_t* ticket = reinterpret_cast<uint32_t*>(sc.off + nb + 1);
-        if (id_bits == 32)
-            hipLaunchKernelGGL((k_parse_chunk<uint32_t, true>), dim3(nb), dim3(256), 0, s, dtext, n_bytes, nullptr, nullptr,
-                               sc.off, ticket, cap, (uint32_t*)src, (uint32_t*)dst, sc.bad);
-        else
-            hipLaunchKernelGGL((k_parse_chunk<int64_t, true>), dim3(nb), dim3(256), 0, s, dtext, n_bytes, nullptr, nullptr,
-                               sc.off, ticket, cap, (int64_t*)src, (int64_t*)dst, sc.bad);
-        GS_HIP(hipGetLastError());
-        GS_HIP(hipMemcpyAsync(&sc.hbad[1], sc.off + nb - 1, 8, hipMemcpyDeviceToHost, s));
-        GS_HIP(hipMemcpyAsync(&last, dtext + n_bytes - 1, 1, hipMemcpyDeviceToHost, s));
-        GS_HIP(hipMemcpyAsync(&sc.hbad[0], sc.bad, 8, hipMemcpyDeviceToHost, s));
-        GS_HIP(hipStreamSynchronize(s));
-        lines = (sc.hbad[1] & kStVal) + (last != '\n');       // a last line without '\n' still counts
-        if (lines > cap) {
-            *n_edges = lines;
-            return fail(GS_ERR_CAPACITY, "gs_parse_edges: %llu lines, capacity %llu", (unsigned long long)lines,
-                        (unsigned long long)cap);
-        }
-    } else {
-        // host outputs: count first (they are staged at the line count), then parse
-        hipLaunchKernelGGL(k_nl_count, dim3(nb), dim3(256), 0, s, dtext, n_bytes, sc.cnt);
-        hipLaunchKernelGGL(k_nl_scan_local, dim3(ng), dim3(kScanGroup), 0, s, sc.cnt, sc.off, sc.gsum, nb);
-        hipLaunchKernelGGL(k_nl_scan_top, dim3(1), dim3(kScanGroup), 0, s, (const unsigned long long*)sc.gsum, sc.gpre, ng,
-                           sc.off, nb);
-        GS_HIP(hipGetLastError());
-        GS_HIP(hipMemcpyAsync(&sc.hbad[1], sc.off + nb, 8, hipMemcpyDeviceToHost, s));
-        GS_HIP(hipMemcpyAsync(&last, dtext + n_bytes - 1, 1, hipMemcpyDeviceToHost, s));
-        GS_HIP(hipStreamSynchronize(s));
-        lines = sc.hbad[1] + (last != '\n');                  // a last line without '\n' still counts
-        if (lines > cap) {
-            *n_edges = lines;
-            return fail(GS_ERR_CAPACITY, "gs_parse_edges: %llu lines, capacity %llu", (unsigned long long)lines,
-                        (unsigned long long)cap);
-        }
-        void* dsrc = nullptr;
-        void* ddst = nullptr;
+    GS_HIP(hipMemcpyAsync(&sc.hbad[1], sc.off + nb, 8, hipMemcpyDeviceToHost, s));
+    GS_HIP(hipMemcpyAsync(&last, dtext + n_bytes - 1, 1, hipMemcpyDeviceToHost, s));
+    GS_HIP(hipStreamSynchronize(s));
+    const uint64_t nl = sc.hbad[1];
+    const uint64_t lines = nl + (last != '\n');             // a last line without '\n' still counts
+    if (lines > cap) {
+        *n_edges = lines;
+        return fail(GS_ERR_CAPACITY, "gs_parse_edges: %llu lines, capacity %llu", (unsigned long long)lines,
+                    (unsigned long long)cap);
+    }
+    const bool dev_out = is_device_pointer(src) && is_device_pointer(dst);
+    void* dsrc = src;
+    void* ddst = dst;
+    if (!dev_out) {                                          // host outputs: staged per call
         if (hipMalloc(&dsrc, (size_t)std::max<uint64_t>(lines, 1) * esz) != hipSuccess ||
             hipMalloc(&ddst, (size_t)std::max<uint64_t>(lines, 1) * esz) != hipSuccess) {
             (void)hipGetLastError();
-            if (dsrc) (void)hipFree(dsrc);
+            if (dsrc != src) (void)hipFree(dsrc);
             return fail(GS_ERR_NOMEM, "gs_parse_edges: output staging");
         }
-        if (id_bits == 32)
-            hipLaunchKernelGGL((k_parse_chunk<uint32_t, false>), dim3(nb), dim3(256), 0, s, dtext, n_bytes, sc.off,
-                               (const unsigned long long*)sc.gpre, nullptr, nullptr, ~0ull, (uint32_t*)dsrc, (uint32_t*)ddst,
-                               sc.bad);
-        else
-            hipLaunchKernelGGL((k_parse_chunk<int64_t, false>), dim3(nb), dim3(256), 0, s, dtext, n_bytes, sc.off,
-                               (const unsigned long long*)sc.gpre, nullptr, nullptr, ~0ull, (int64_t*)dsrc, (int64_t*)ddst,
-                               sc.bad);
-        if (hipGetLastError() != hipSuccess) rc = fail(GS_ERR_HIP, "gs_parse_edges: k_parse_chunk launch failed");
-        if (rc == GS_OK && hipMemcpyAsync(&sc.hbad[0], sc.bad, 8, hipMemcpyDeviceToHost, s) != hipSuccess)
-            rc = fail(GS_ERR_HIP, "gs_parse_edges: copy of the bad-line word failed");
-        if (rc == GS_OK && lines &&
-            (hipMemcpyAsync(src, dsrc, lines * esz, hipMemcpyDeviceToHost, s) != hipSuccess ||
-             hipMemcpyAsync(dst, ddst, lines * esz, hipMemcpyDeviceToHost, s) != hipSuccess))
-            rc = fail(GS_ERR_HIP, "gs_parse_edges: copy of the outputs failed");
-        if (hipStreamSynchronize(s) != hipSuccess && rc == GS_OK) rc = fail(GS_ERR_HIP, "gs_parse_edges: stream sync failed");
+    }
+    if (id_bits == 32)
+        hipLaunchKernelGGL(k_parse_chunk<uint32_t>, dim3(nb), dim3(256), 0, s, dtext, n_bytes, sc.off,
+                           (const unsigned long long*)sc.gpre, (uint32_t*)dsrc, (uint32_t*)ddst, sc.bad);
+    else
+        hipLaunchKernelGGL(k_parse_chunk<int64_t>, dim3(nb), dim3(256), 0, s, dtext, n_bytes, sc.off,
+                           (const unsigned long long*)sc.gpre, (int64_t*)dsrc, (int64_t*)ddst, sc.bad);
+    int rc = GS_OK;
+    if (hipGetLastError() != hipSuccess) rc = fail(GS_ERR_HIP, "gs_parse_edges: k_parse_chunk launch failed");
+    if (rc == GS_OK && hipMemcpyAsync(&sc.hbad[0], sc.bad, 8, hipMemcpyDeviceToHost, s) != hipSuccess)
+        rc = fail(GS_ERR_HIP, "gs_parse_edges: copy of the bad-line word failed");
+    if (rc == GS_OK && !dev_out && lines &&
+        (hipMemcpyAsync(src, dsrc, lines * esz, hipMemcpyDeviceToHost, s) != hipSuccess ||
+         hipMemcpyAsync(dst, ddst, lines * esz, hipMemcpyDeviceToHost, s) != hipSuccess))
+        rc = fail(GS_ERR_HIP, "gs_parse_edges: copy of the outputs failed");
+    if (hipStreamSynchronize(s) != hipSuccess && rc == GS_OK) rc = fail(GS_ERR_HIP, "gs_parse_edges: stream sync failed");
+    if (!dev_out) {
         (void)hipFree(dsrc);
         (void)hipFree(ddst);
-        if (rc != GS_OK) return rc;
     }
+    if (rc != GS_OK) return rc;
     const unsigned long long first_bad = sc.hbad[0];
     if (first_bad != ~0ull) {
         *n_edges = first_bad;

@@ -810,7 +810,7 @@ def test_parse_edges_long_lines_extremes_and_device_text(torch_cuda):
 
 
 def _dev_parse(torch, text, id_bits=64, cap=None):
-    """gs_parse_edges with device text and device outputs (the one-pass look-back kernel)."""
+    """gs_parse_edges with device text and device outputs (what bench.py's parse line times)."""
     import ctypes
     from gsgpu._abi import call
     buf = torch.frombuffer(bytearray(text), dtype=torch.uint8).cuda()
@@ -826,12 +826,12 @@ def _dev_parse(torch, text, id_bits=64, cap=None):
     return n, ps[:n].cpu().numpy().astype(np.int64), pd[:n].cpu().numpy().astype(np.int64)
 
 
-def test_parse_edges_one_pass_device_outputs(torch_cuda):
-    """The one-pass parse (chunk first lines by decoupled look-back, device outputs) against the
-    Java rules: valid forms, every rejected form at a chunk boundary, texts of 1 B to a few chunks at
-    every length class (no trailing '\\n', exactly 4096 B, one line per chunk), int32 outputs, the
-    capacity error, and ~20K chunks of RMAT text (a long look-back chain) equal to the host-output
-    (two-pass) path."""
+def test_parse_edges_device_outputs(torch_cuda):
+    """Device text and device outputs against the Java rules: valid forms, every rejected form past
+    the first chunk, texts of 1 B to a few chunks at every length class (no trailing '\\n', exactly
+    4096 B, one line per chunk), int32 outputs, the capacity error, and ~20K chunks of random text,
+    equal to the host-output path. (Written for the one-pass look-back parse, which was measured
+    slower and removed: profiles/r04_parse_onepass_ab.txt.)"""
     from gsgpu.edgefile import parse_edges
     torch = torch_cuda
     text = b"1 2\n3\t4\n5 6 extra fields\n+7 -8\r\n9 10  \n" + b"".join(b"%d %d\n" % (i, i * 7 % 1000) for i in range(5000)) + b"11 12"
