@@ -240,11 +240,9 @@ __device__ __forceinline__ int scan_window(const uint8_t* w, int r, uint64_t bas
 // chunk: a thread parses every line that STARTS in its 16 bytes (after each '\n' there, and line 0
 // at byte 0) from a 48-byte window of that LDS copy (a line longer than the window is parsed from
 // memory); line index = the chunk's first line (off, the scan of k_nl_count) + the '\n's before it.
-// Lines at or past cap are not written: device outputs are parsed without waiting for the line
-// count (one host sync per call), and the host reports a capacity error afterwards.
 template <typename IdT>
 __global__ __launch_bounds__(256) void k_parse_chunk(const char* __restrict__ t, uint64_t n, const uint64_t* __restrict__ off,
-                                                     const unsigned long long* __restrict__ gpre, uint64_t cap,
+                                                     const unsigned long long* __restrict__ gpre,
                                                      IdT* __restrict__ src, IdT* __restrict__ dst,
                                                      unsigned long long* __restrict__ bad_line) {
     __shared__ uint4 s_text[kChunk / 16 + 2];
@@ -279,7 +277,6 @@ __global__ __launch_bounds__(256) void k_parse_chunk(const char* __restrict__ t,
     const uint8_t* win = reinterpret_cast<const uint8_t*>(s_text) + threadIdx.x * 16;
     const bool in = base + 48 <= n;
     auto one = [&](int r, uint64_t li) {
-        if (li >= cap) return;                                 // (the host reports the capacity error)
         int64_t x = 0, y = 0;
         const int k = in ? scan_window<true>(win, r, base, n, &x, &y) : scan_window<false>(win, r, base, n, &x, &y);
         if (k == 2) { parse_store<IdT>(t, n, base + r, li, src, dst, bad_line); return; }
@@ -383,22 +380,18 @@ extern "C" int gs_parse_edges(const char* text, uint64_t n_bytes, uint32_t id_bi
     char last = '\n';
     GS_HIP(hipMemcpyAsync(&sc.hbad[1], sc.off + nb, 8, hipMemcpyDeviceToHost, s));
     GS_HIP(hipMemcpyAsync(&last, dtext + n_bytes - 1, 1, hipMemcpyDeviceToHost, s));
-    const bool dev_out = is_device_pointer(src) && is_device_pointer(dst);
-    uint64_t lines = 0;
-    auto count_lines = [&]() -> int {
-        lines = sc.hbad[1] + (last != '\n');                  // a last line without '\n' still counts
-        if (lines <= cap) return GS_OK;
+    GS_HIP(hipStreamSynchronize(s));
+    const uint64_t nl = sc.hbad[1];
+    const uint64_t lines = nl + (last != '\n');             // a last line without '\n' still counts
+    if (lines > cap) {
         *n_edges = lines;
         return fail(GS_ERR_CAPACITY, "gs_parse_edges: %llu lines, capacity %llu", (unsigned long long)lines,
                     (unsigned long long)cap);
-    };
+    }
+    const bool dev_out = is_device_pointer(src) && is_device_pointer(dst);
     void* dsrc = src;
     void* ddst = dst;
-    uint64_t wcap = cap;
-    if (!dev_out) {                                          // host outputs: staged at the line count
-        GS_HIP(hipStreamSynchronize(s));
-        GS_TRY(count_lines());
-        wcap = lines;
+    if (!dev_out) {                                          // host outputs: staged per call
         if (hipMalloc(&dsrc, (size_t)std::max<uint64_t>(lines, 1) * esz) != hipSuccess ||
             hipMalloc(&ddst, (size_t)std::max<uint64_t>(lines, 1) * esz) != hipSuccess) {
             (void)hipGetLastError();
@@ -408,10 +401,10 @@ extern "C" int gs_parse_edges(const char* text, uint64_t n_bytes, uint32_t id_bi
     }
     if (id_bits == 32)
         hipLaunchKernelGGL(k_parse_chunk<uint32_t>, dim3(nb), dim3(256), 0, s, dtext, n_bytes, sc.off,
-                           (const unsigned long long*)sc.gpre, wcap, (uint32_t*)dsrc, (uint32_t*)ddst, sc.bad);
+                           (const unsigned long long*)sc.gpre, (uint32_t*)dsrc, (uint32_t*)ddst, sc.bad);
     else
         hipLaunchKernelGGL(k_parse_chunk<int64_t>, dim3(nb), dim3(256), 0, s, dtext, n_bytes, sc.off,
-                           (const unsigned long long*)sc.gpre, wcap, (int64_t*)dsrc, (int64_t*)ddst, sc.bad);
+                           (const unsigned long long*)sc.gpre, (int64_t*)dsrc, (int64_t*)ddst, sc.bad);
     int rc = GS_OK;
     if (hipGetLastError() != hipSuccess) rc = fail(GS_ERR_HIP, "gs_parse_edges: k_parse_chunk launch failed");
     if (rc == GS_OK && hipMemcpyAsync(&sc.hbad[0], sc.bad, 8, hipMemcpyDeviceToHost, s) != hipSuccess)
@@ -426,7 +419,6 @@ extern "C" int gs_parse_edges(const char* text, uint64_t n_bytes, uint32_t id_bi
         (void)hipFree(ddst);
     }
     if (rc != GS_OK) return rc;
-    if (dev_out) GS_TRY(count_lines());                      // (lines past cap were not written)
     const unsigned long long first_bad = sc.hbad[0];
     if (first_bad != ~0ull) {
         *n_edges = first_bad;
