@@ -12,6 +12,7 @@ struct CcInfo {
     bool sparse;
     bool marking;            // marking currently on (gs_cc_set_marking)
     uint64_t reset_gen;      // gs_cc_reset calls so far: a new stream starts when it changes
+    uint32_t id_bits;        // the handle's id width (gs_cc_config.id_bits)
 };
 int cc_info(gs_cc_t* h, CcInfo* out);
 int cc_export_async(gs_cc_t* h, void* pairs, uint64_t cap, unsigned long long* dcount, uint64_t expect = ~0ull);
@@ -25,4 +26,8 @@ int cc_fold_pairs_any(gs_cc_t* h, const void* pairs, uint64_t n);
 // a pending exchange verification of the handle's last window (comm.hip): cc_settle runs it once
 void cc_set_settle(gs_cc_t* h, int (*fn)(void*), void* ctx);
 int cc_settle(gs_cc_t* h);
+// per-handle state of the streaming text ingestion (parse.hip gs_cc_fold_text / _file): made on
+// first use, kept for the next call, freed by gs_cc_destroy through free_fn
+void* cc_ingest_get(gs_cc_t* h);
+void cc_ingest_set(gs_cc_t* h, void* p, void (*free_fn)(void*));
 }  // namespace gsgpu

@@ -3,9 +3,15 @@
 //
 //   cc_example                                   built-in sample stream (k, k+2), k = 1..100,
 //                                                event time k*100 ms, merge window 1000 ms (:121-139)
-//   cc_example <edges> <merge ms> <print ms>     whitespace-separated "src trg" lines (:108-119);
-//                                                no timestamps in the file, so the merge window is
-//                                                cut by edge count: <merge ms> edges per window
+//   cc_example <edges> <merge ms> <print ms> [capacity]
+//                                                whitespace-separated "src trg" lines (:108-119),
+//                                                streamed from the file through the device
+//                                                (gs_cc_fold_file: chunked pinned H2D, parsed and
+//                                                folded on the device); no timestamps in the file,
+//                                                so the merge window is cut by edge count (<merge ms>
+//                                                edges per window) and the print window by window
+//                                                count (<print ms> windows); any Long ids (a sparse-id
+//                                                summary of at most [capacity] distinct ids, 2^24)
 //
 // Output: like the reference's FlattenSet -> keyBy(vertex) -> timeWindow(print) -> fold(identity)
 // -> print (:61-67): at the end of every print window, one "(vertex,root)" line per vertex with
@@ -29,25 +35,36 @@ int main(int argc, char** argv) {
     long merge_ms = 1000, print_ms = 2000;
     uint64_t window_edges = 0;
     if (argc > 1) {
-        if (argc != 4) {
-            std::cerr << "Usage: cc_example <input edges path> <merge window time (ms)> <print window time (ms)>\n";
+        if (argc != 4 && argc != 5) {
+            std::cerr << "Usage: cc_example <input edges path> <merge window time (ms)> <print window time (ms)> [capacity]\n";
             return 1;
         }
-        std::ifstream in(argv[1], std::ios::binary);
-        if (!in) { std::cerr << "cannot open " << argv[1] << "\n"; return 1; }
-        const std::string text((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
-        // parsed on the device with the reference's split("\\s") + Long.parseLong rules
-        const uint64_t cap = (uint64_t)std::count(text.begin(), text.end(), '\n') + 1;
-        s.src.resize(cap);
-        s.dst.resize(cap);
-        uint64_t n = 0;
-        const int rc = gs_parse_edges(text.data(), text.size(), 64, s.src.data(), s.dst.data(), cap, &n, 0, nullptr);
-        if (rc != GS_OK) { std::cerr << gs_last_error() << "\n"; return 2; }
-        s.src.resize(n);
-        s.dst.resize(n);
         merge_ms = std::atol(argv[2]);
         print_ms = std::atol(argv[3]);
         window_edges = merge_ms > 0 ? (uint64_t)merge_ms : 1;
+        const uint64_t cap = argc == 5 ? std::strtoull(argv[4], nullptr, 0) : (1ull << 24);
+        try {
+            DisjointSet<int64_t> ds(cap, 0, GS_CC_SPARSE_IDS);
+            ConnectedComponents<int64_t> cc(merge_ms, cap, 0, window_edges);
+            std::vector<int64_t> v, l;
+            // print window p = windows [p * print_ms, (p + 1) * print_ms): FlattenSet + IdentityFold
+            // print the emission of its last window, i.e. the summary right after that window closes
+            const uint64_t pw = print_ms > 0 ? (uint64_t)print_ms : 1;
+            bool pending = false;
+            auto flush = [&](DisjointSet<int64_t>& d) {
+                d.pairs(v, l);
+                for (size_t i = 0; i < v.size(); ++i) std::printf("(%lld,%lld)\n", (long long)v[i], (long long)l[i]);
+            };
+            cc.runFile(ds, argv[1], [&](DisjointSet<int64_t>& d, uint64_t w) {
+                pending = true;
+                if ((w + 1) % pw == 0) { flush(d); pending = false; }
+            });
+            if (pending) flush(ds);
+        } catch (const GsError& e) {
+            std::cerr << e.what() << "\n";
+            return 2;
+        }
+        return 0;
     } else {
         std::cout << "Executing ConnectedComponentsExample example with default parameters and built-in default data.\n";
         for (long k = 1; k <= 100; ++k) {

@@ -255,6 +255,23 @@ public:
         }
     }
 
+    // the same operator over an edge FILE streamed through the device (gs_cc_fold_file: chunks of
+    // text read into pinned staging, parsed on the device, folded from device memory; the reference's
+    // readTextFile + split + parseLong, ConnectedComponentsExample.java:108-119): count windows of
+    // window_edges edges (0: the constructor's), emit(summary, w) after window w's close. `summary`
+    // must be a DisjointSet<K> made for the file's ids (GS_CC_SPARSE_IDS for arbitrary longs).
+    void runFile(DisjointSet<K>& summary, const std::string& path,
+                 const std::function<void(DisjointSet<K>&, uint64_t)>& emit, uint64_t window_edges = 0) {
+        struct Ctx { DisjointSet<K>* ds; const std::function<void(DisjointSet<K>&, uint64_t)>* emit; };
+        Ctx ctx{&summary, &emit};
+        const uint64_t W = window_edges ? window_edges : (window_edges_ ? window_edges_ : (uint64_t)std::max(1L, millis_));
+        uint64_t edges = 0, windows = 0;
+        check(gs_cc_fold_file(summary.handle(), path.c_str(), W, 0,
+                              [](void* c, uint64_t w) { Ctx* x = static_cast<Ctx*>(c); (*x->emit)(*x->ds, w); },
+                              &ctx, &edges, &windows),
+              "gs_cc_fold_file");
+    }
+
 private:
     long millis_;
     uint64_t cap_;

@@ -26,7 +26,7 @@ GS_ERR_COMM = -8
 GS_CC_TRACK_MARKS = 1
 GS_CC_SPARSE_IDS = 2
 
-GS_K_FOLD, GS_K_COMPRESS, GS_K_MERGE, GS_K_EXPORT, GS_K_RING = 0, 1, 2, 3, 4
+GS_K_FOLD, GS_K_COMPRESS, GS_K_MERGE, GS_K_EXPORT, GS_K_RING, GS_K_UNION = 0, 1, 2, 3, 4, 6
 GS_MERGE_ALLGATHER, GS_MERGE_GATHER, GS_MERGE_TREE = 0, 1, 2
 GS_TIMING_MASK = 0x100
 
@@ -42,6 +42,7 @@ EXPORTED_SYMBOLS = (
     "gs_cc_emit_delta_async", "gs_cc_emit_wait",
     "gs_cc_checksum", "gs_cc_find", "gs_cc_find_flags", "gs_cc_labels_device", "gs_cc_export_marks",
     "gs_cc_fold_pairs32", "gs_cc_export_marks_async", "gs_cc_set_marking", "gs_cc_timing", "gs_cc_kernel_time", "gs_cc_kernel_units", "gs_gen_rmat", "gs_gen_er", "gs_parse_edges",
+    "gs_cc_fold_text", "gs_cc_fold_file",
     "gs_bip_create", "gs_bip_destroy", "gs_bip_reset", "gs_bip_set_stream", "gs_bip_sync", "gs_bip_fold",
     "gs_bip_fold_pairs", "gs_bip_merge", "gs_bip_close_window", "gs_bip_status", "gs_bip_checksum",
     "gs_bip_emit_pairs",
@@ -140,6 +141,8 @@ def lib() -> ctypes.CDLL:
         "gs_gen_rmat": [vp, vp, u32, u64, u64, i32, u64, u32, u32, u32, i32, vp],
         "gs_gen_er": [vp, vp, u32, u64, u64, u64, u64, vp],
         "gs_parse_edges": [vp, u64, u32, vp, vp, u64, P(u64), i32, vp],
+        "gs_cc_fold_text": [vp, vp, u64, u64, u64, ctypes.CFUNCTYPE(None, vp, u64), vp, P(u64), P(u64)],
+        "gs_cc_fold_file": [vp, ctypes.c_char_p, u64, u64, ctypes.CFUNCTYPE(None, vp, u64), vp, P(u64), P(u64)],
         "gs_bip_create": [P(vp), u64, u32, i32],
         "gs_bip_destroy": [vp],
         "gs_bip_reset": [vp],

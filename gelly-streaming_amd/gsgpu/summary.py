@@ -63,6 +63,10 @@ def _stream_ptr(stream) -> Optional[int]:
     return int(stream.cuda_stream)        # torch.cuda.Stream
 
 
+def _cuda_tensors(objs):
+    return [o for o in objs if _is_torch(o) and o.is_cuda]
+
+
 class DisjointSet:
     """GPU union-find summary (DisjointSet<K>), K = int32 or int64 vertex ids in [0, capacity);
     ``sparse=True`` (64-bit ids only): ANY Java long ids, at most ``vertex_capacity`` distinct."""
@@ -109,6 +113,43 @@ class DisjointSet:
     def set_stream(self, stream) -> None:
         call("gs_cc_set_stream", self.handle, _stream_ptr(stream))
 
+    def _stream(self) -> int:
+        s = ctypes.c_void_p()
+        call("gs_cc_get_stream", self.handle, ctypes.byref(s))
+        return int(s.value or 0)
+
+    def _after_torch(self, *objs) -> None:
+        """Device tensors a call reads were produced in torch's stream order: the handle's stream
+        waits for torch's current stream first (an event, no host wait). Without it a handle on
+        its own stream could read a tensor torch is still writing (e.g. the torch.stack of a
+        fold_pairs input; round 4's list-close diagnostic failed that way)."""
+        ts = _cuda_tensors(objs)
+        if not ts:
+            return
+        import torch
+        cur = torch.cuda.current_stream(ts[0].device)
+        hs = self._stream()
+        if hs == 0 or hs == cur.cuda_stream:         # same stream (or the null stream: ordered anyway)
+            return
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        torch.cuda.ExternalStream(hs, device=ts[0].device).wait_event(ev)
+
+    def _torch_after(self, *objs) -> None:
+        """The reverse: torch's current stream waits for what this handle enqueued into device
+        tensors without a host wait (async exports)."""
+        ts = _cuda_tensors(objs)
+        if not ts:
+            return
+        import torch
+        cur = torch.cuda.current_stream(ts[0].device)
+        hs = self._stream()
+        if hs == 0 or hs == cur.cuda_stream:
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.ExternalStream(hs, device=ts[0].device))
+        cur.wait_event(ev)
+
     def sync(self) -> None:
         call("gs_cc_sync", self.handle)
 
@@ -132,6 +173,7 @@ class DisjointSet:
     def find_batch(self, ids) -> np.ndarray:
         p, keep, n = _buf(ids, self.id_bits, "ids")
         out = np.empty(n, dtype=np.uint32 if self.id_bits == 32 else np.int64)
+        self._after_torch(keep)
         call("gs_cc_find", self.handle, p, out.ctypes.data_as(ctypes.c_void_p), n)
         return out.view(np.int32).astype(np.int64) if self.id_bits == 32 else out
 
@@ -140,6 +182,7 @@ class DisjointSet:
         p, keep, n = _buf(ids, self.id_bits, "ids")
         out = np.empty(n, dtype=np.uint32 if self.id_bits == 32 else np.int64)
         found = np.empty(n, dtype=np.uint8)
+        self._after_torch(keep)
         call("gs_cc_find_flags", self.handle, p, out.ctypes.data_as(ctypes.c_void_p),
              found.ctypes.data_as(ctypes.c_void_p), n)
         lab = out.view(np.int32).astype(np.int64) if self.id_bits == 32 else out
@@ -177,6 +220,7 @@ class DisjointSet:
         pd, kd, m = _buf(dst, self.id_bits, "dst")
         if n != m:
             raise ValueError("src and dst lengths differ (%d, %d)" % (n, m))
+        self._after_torch(ks, kd)
         call("gs_cc_fold", self.handle, ps, pd, n)
 
     def fold_pairs(self, pairs, n: Optional[int] = None, id_bits: Optional[int] = None) -> None:
@@ -186,6 +230,7 @@ class DisjointSet:
         cnt = total // 2 if n is None else int(n)
         if cnt * 2 > total:
             raise ValueError("pairs buffer holds %d pairs, %d requested" % (total // 2, cnt))
+        self._after_torch(keep)
         call("gs_cc_fold_pairs32" if bits == 32 else "gs_cc_fold_pairs", self.handle, p, cnt)
 
     def close_window(self) -> None:
@@ -207,9 +252,57 @@ class DisjointSet:
         if n != m:
             raise ValueError("src and dst lengths differ (%d, %d)" % (n, m))
         w = U64()
+        self._after_torch(ks, kd)
         call("gs_cc_fold_windows", self.handle, comm.handle if comm is not None else None,
              MODES[mode], ps, pd, n, int(window_edges), ctypes.byref(w))
         return int(w.value)
+
+    def fold_text(self, text, window_edges: int, chunk_bytes: int = 0, on_window=None) -> Tuple[int, int]:
+        """gs_cc_fold_text: edge text (ConnectedComponentsExample's file format) streamed into this
+        summary in count windows, each closed; the ids never leave the device. ``text``: bytes /
+        bytearray / numpy uint8 (host), a pinned torch uint8 tensor (DMA straight from it) or a CUDA
+        uint8 tensor. on_window(w): called after window w's close is enqueued (read its emission
+        there). Returns (edges, windows). A rejected line raises GsError (code GS_ERR_INVALID) with
+        ``.edges`` = its 0-based line number (every line before it was folded)."""
+        keep = text
+        if _is_torch(text):
+            p, n = ctypes.c_void_p(text.data_ptr()), text.numel() * text.element_size()
+            self._after_torch(text)
+        elif isinstance(text, (bytes, bytearray, memoryview)):
+            keep = np.frombuffer(text, dtype=np.uint8)
+            p, n = keep.ctypes.data_as(ctypes.c_void_p), keep.size
+        else:
+            keep = np.ascontiguousarray(text, dtype=np.uint8)
+            p, n = keep.ctypes.data_as(ctypes.c_void_p), keep.size
+        return self._fold_stream("gs_cc_fold_text", (p, n), window_edges, chunk_bytes, on_window)
+
+    def fold_file(self, path: str, window_edges: int, chunk_bytes: int = 0, on_window=None) -> Tuple[int, int]:
+        """gs_cc_fold_file: as fold_text, the text read from ``path`` chunk by chunk into pinned
+        staging (the whole file never sits in host memory)."""
+        return self._fold_stream("gs_cc_fold_file", (str(path).encode(),), window_edges, chunk_bytes, on_window)
+
+    _WINDOW_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64)
+
+    def _fold_stream(self, name, src_args, window_edges, chunk_bytes, on_window):
+        errs = []
+
+        def cb(_ctx, w):
+            try:
+                on_window(int(w))
+            except Exception as e:  # an exception cannot cross the C frame: re-raised after the call
+                errs.append(e)
+        fn = self._WINDOW_FN(cb) if on_window is not None else ctypes.cast(None, self._WINDOW_FN)
+        edges, wins = U64(), U64()
+        rc = getattr(_abi.lib(), name)(self.handle, *src_args, int(window_edges), int(chunk_bytes), fn, None,
+                                       ctypes.byref(edges), ctypes.byref(wins))
+        if errs:
+            raise errs[0]
+        if rc != _abi.GS_OK:
+            msg = _abi.lib().gs_last_error()
+            e = _abi.GsError(rc, name, msg.decode() if msg else "")
+            e.edges, e.windows = int(edges.value), int(wins.value)
+            raise e
+        return int(edges.value), int(wins.value)
 
     def stats(self) -> Tuple[int, int]:
         nv, nc = U64(), U64()
@@ -230,6 +323,7 @@ class DisjointSet:
         if out is None:
             out = np.empty(n, dtype=np.int32 if self.id_bits == 32 else np.int64)
         p, keep, m = _buf(out, self.id_bits, "labels")
+        self._after_torch(keep)
         call("gs_cc_emit_dense", self.handle, p, m)
         return out
 
@@ -256,6 +350,7 @@ class DisjointSet:
         pv, kv, cap = _buf(vertices, self.id_bits, "vertices")
         pl, kl, cap2 = _buf(labels, self.id_bits, "labels")
         cnt = U64()
+        self._after_torch(kv, kl)
         call("gs_cc_emit_delta", self.handle, pv, pl, min(cap, cap2), ctypes.byref(cnt))
         return vertices[:cnt.value], labels[:cnt.value]
 
@@ -266,6 +361,7 @@ class DisjointSet:
         pv, kv, cap = _buf(vertices, self.id_bits, "vertices")
         pl, kl, cap2 = _buf(labels, self.id_bits, "labels")
         cnt = U64()
+        self._after_torch(kv, kl)
         call("gs_cc_emit_delta_async", self.handle, pv, pl, min(cap, cap2), ctypes.byref(cnt))
         self._epend.append((vertices, labels, cnt, kv, kl))
 
@@ -310,6 +406,7 @@ class DisjointSet:
         p, keep, total = _buf(out, 64 if self.sparse else 32, "out")
         cap = total // 2 if cap_pairs is None else int(cap_pairs)
         n = U64()
+        self._after_torch(keep)
         call("gs_cc_export_marks", self.handle, p, cap, ctypes.byref(n))
         return int(n.value)
 
@@ -317,7 +414,9 @@ class DisjointSet:
         """export_marks enqueued on the stream; the pair count lands in the device int64 tensor
         ``count`` (one element), no host sync."""
         p, keep, total = _buf(out, 32, "out")
+        self._after_torch(keep, count)
         call("gs_cc_export_marks_async", self.handle, p, total // 2, ctypes.c_void_p(count.data_ptr()))
+        self._torch_after(keep, count)
 
     def set_marking(self, on: bool) -> None:
         """Pause / resume marking (GS_CC_TRACK_MARKS): folds while paused are not exported."""
@@ -340,10 +439,12 @@ class DisjointSet:
         return int(u.value)
 
     def fold_time(self) -> Tuple[float, int]:
-        """(ms, launches) of every UpdateCC launch: k_fold (young / plain) + the steady k_fold_ring."""
+        """(ms, launches) of every UpdateCC launch: k_fold (young / plain) + the steady k_fold_ring
+        (or, in gs_cc_fold_windows, the run-ahead filter k_filter) + k_union."""
         a, na = self.kernel_time(_abi.GS_K_FOLD)
         b, nb = self.kernel_time(_abi.GS_K_RING)
-        return a + b, na + nb
+        c, nc = self.kernel_time(_abi.GS_K_UNION)
+        return a + b + c, na + nb + nc
 
 
 def combine_cc(s1: DisjointSet, s2: DisjointSet) -> DisjointSet:

@@ -215,9 +215,11 @@ int gs_cc_fold_windows(gs_cc_t* h, gs_comm_t* comm, int mode, const void* src, c
 
 /* ---- instrumentation ----
  * kernel ids: 0 fold (young-forest / plain k_fold launches), 1 compress (close_window), 2 merge,
- * 3 export, 4 ring (the steady k_fold_ring launches), 5 reserved (a retired steady-fold variant;
- * always 0); fold time = 0 + 4. */
-enum { GS_K_FOLD = 0, GS_K_COMPRESS = 1, GS_K_MERGE = 2, GS_K_EXPORT = 3, GS_K_RING = 4, GS_K_ROUTE = 5, GS_K_COUNT = 6 };
+ * 3 export, 4 ring (the steady k_fold_ring launches, and gs_cc_fold_windows' run-ahead filter
+ * k_filter), 5 reserved (a retired steady-fold variant; always 0), 6 union (k_union: the ordered
+ * half of a split steady window); fold time = 0 + 4 + 6. */
+enum { GS_K_FOLD = 0, GS_K_COMPRESS = 1, GS_K_MERGE = 2, GS_K_EXPORT = 3, GS_K_RING = 4, GS_K_ROUTE = 5, GS_K_UNION = 6,
+       GS_K_COUNT = 7 };
 /* enable = 0: off; 1: every kernel; GS_TIMING_MASK | (1 << GS_K_x) | ...: only those kernels
  * carry timing events (a timed launch costs ~3 us more dispatch time). Totals reset. */
 enum { GS_TIMING_MASK = 0x100 };
@@ -242,6 +244,30 @@ int gs_gen_er(void* src, void* dst, uint32_t id_bits, uint64_t first, uint64_t n
  * reference would reject -> GS_ERR_INVALID, *n_edges = its 0-based index. */
 int gs_parse_edges(const char* text, uint64_t n_bytes, uint32_t id_bits, void* src, void* dst, uint64_t cap,
                    uint64_t* n_edges, int device, void* hip_stream);
+
+/* ---- streaming edge-file ingestion into a summary (ConnectedComponentsExample.java:108-119 ->
+ * edges.aggregate(new ConnectedComponents<>(mergeWindowTime)), :61) ----
+ * The text (gs_parse_edges' line rules) is consumed in chunks of at most chunk_bytes (0 = 64 MiB),
+ * each cut after its last '
+' (the partial last line carried to the next chunk), copied to the
+ * device through two pinned staging buffers (the host's read / copy of chunk i+1 overlaps the parse
+ * of chunk i and the folds of chunk i-1), parsed on the device into an edge ring, and folded into h
+ * straight from it in count windows of window_edges edges, every window closed (the Merger's
+ * emission; a last partial window is closed too). The ids never return to the host.
+ * gs_cc_fold_text: text in host memory (pinned: DMA straight from it; pageable: through the pinned
+ * staging) or device memory (one chunk). gs_cc_fold_file: read(2) from path into the staging.
+ * h: either id width; GS_CC_SPARSE_IDS summaries take any Long id. *edges_out = edges folded; *windows_out =
+ * windows closed. A line the reference rejects: GS_ERR_INVALID, every line before it folded (its
+ * window left open), *edges_out = its 0-based line number. A line longer than chunk_bytes:
+ * GS_ERR_CAPACITY. Enqueued on h's stream like gs_cc_fold_windows. on_window (may be NULL): called on
+ * the calling thread after window w's close is enqueued (w counts from 0 per call): the Merger's
+ * per-window emission hook (read it with gs_cc_emit_delta / _pairs / gs_cc_checksum there); with a
+ * callback every window is folded and closed on its own (no run-ahead filter across windows). */
+typedef void (*gs_window_fn)(void* ctx, uint64_t window);
+int gs_cc_fold_text(gs_cc_t* h, const char* text, uint64_t n_bytes, uint64_t window_edges, uint64_t chunk_bytes,
+                    gs_window_fn on_window, void* ctx, uint64_t* edges_out, uint64_t* windows_out);
+int gs_cc_fold_file(gs_cc_t* h, const char* path, uint64_t window_edges, uint64_t chunk_bytes,
+                    gs_window_fn on_window, void* ctx, uint64_t* edges_out, uint64_t* windows_out);
 
 /* ---- BipartitenessCheck (library/BipartitenessCheck.java:38-133, summaries/Candidates.java) ----
  * A Candidates summary on the device: union-find with a parity bit per vertex. ids in

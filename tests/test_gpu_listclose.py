@@ -95,3 +95,27 @@ def test_list_close_find_and_emission_between_windows(oracle, torch_cuda):
         if w % 5 == 2:
             ds.pairs()
         assert ds.checksum()[0] == int(want["checksums"][w]), "window %d" % w
+
+
+def test_handle_on_its_own_stream_reads_torch_inputs_in_order(oracle, torch_cuda):
+    """A handle on its own stream (no stream= argument) folding device tensors that torch has just
+    produced on its current stream: gsgpu waits for torch's stream first (summary.py _after_torch).
+    Round 4's list-close diagnostic ran the test above without stream= and failed at a fold_pairs
+    window (w % 11 == 5: the torch.stack had not finished when the library read it)."""
+    torch = torch_cuda
+    scale, n, W = 16, 1 << 19, 4096
+    cap = 1 << scale
+    s, d = oracle.gen_rmat(0, n, scale, 11)
+    want = oracle.run(s, d, W, partitions=4, threads=4, emit=EMIT_CHECKSUM, label_cap=cap)
+    ts = torch.from_numpy(s.astype(np.int32)).cuda()
+    td = torch.from_numpy(d.astype(np.int32)).cuda()
+    ds = DisjointSet(cap, id_bits=32)                # its own stream
+    for w, lo in enumerate(range(0, n, W)):
+        # produced on torch's stream right before the call (a larger torch op in front of it, so
+        # that an unordered read would see a buffer still being written)
+        junk = torch.empty(1 << 24, device="cuda").uniform_()
+        pairs = torch.stack([ts[lo:lo + W], td[lo:lo + W]], dim=1).contiguous().view(-1)
+        ds.fold_pairs(pairs)
+        ds.close_window()
+        del junk
+        assert ds.checksum()[0] == int(want["checksums"][w]), "window %d" % w

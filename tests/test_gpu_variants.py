@@ -85,6 +85,11 @@ VARIANTS = {
     "ring_forced_no_warm": {"GSGPU_FOLD_MODE": "ring"},
     "plain_forced": {"GSGPU_FOLD_MODE": "plain", "GSGPU_RING_MIN_BITS": "20"},
     "young_split_2^18": {"GSGPU_YOUNG_SPLIT": str(1 << 18)},
+    # no list-mode closes: every close after a logging fold is a bitmap or full one (the A/B knob
+    # the round-4 list-close measurements ran against)
+    "list_close_off": {"GSGPU_LIST_CLOSE": "0"},
+    # gs_cc_fold_windows without the run-ahead filter (k_fold_ring per steady window, as round 4)
+    "ring_run_ahead_off": {"GSGPU_RING_MIN_BITS": "20", "GSGPU_RUN_AHEAD": "0"},
 }
 
 
@@ -104,3 +109,18 @@ def test_fold_variants_verified(name):
     out = subprocess.check_output(cmd, env=_env(VARIANTS[name]), timeout=300)
     line = _last_json(out)
     assert line["verify"] == {"edges_consistent": True, "labels_minimal_idempotent": True, "equals_torch_cc": True}
+
+
+@pytest.mark.parametrize("name", ["production", "list_close_off"])
+def test_list_close_switch(name):
+    """tests/test_gpu_listclose.py (list, bitmap and full closes mixed in one stream) and all 4,096
+    windows of config 5 (RMAT-24, 2^16-edge windows: the list close's workload) with list-mode
+    closes on (production) and off (GSGPU_LIST_CLOSE=0), each in a process of its own."""
+    env = _env(VARIANTS[name])
+    subprocess.check_call([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                           os.path.join(HERE, "test_gpu_listclose.py")], env=env, timeout=600, cwd=ROOT)
+    out = subprocess.check_output([sys.executable, os.path.join(HERE, "headline_check.py"), "--fixture", "c5",
+                                   "--fold-windows", "--chunk", "256"] + (["--variant"] if VARIANTS[name] else []),
+                                  env=env, timeout=900)
+    r = _last_json(out)
+    assert r["windows"] == 4096 and r["fixture_windows_equal"] and r["ok"], r

@@ -73,9 +73,34 @@ def run_case(torch, oracle, name, s, d, W, cap, partitions=4):
         if ds.checksum()[0] != int(want["checksums"][w]) and bad is None:
             bad = w
     final_ok = bool(np.array_equal(ds.dense().astype(np.int64), want["final"]))
+    fw_bad = run_fold_windows(ds, ts, td, W, want)
     ds.close()
     return {"case": name, "windows": int(len(want["checksums"])), "first_bad_window": bad, "final_equal": final_ok,
-            "ok": bad is None and final_ok}
+            "fold_windows_first_bad": fw_bad, "ok": bad is None and final_ok and fw_bad is None}
+
+
+def run_fold_windows(ds, ts, td, W, want):
+    """gs_cc_fold_windows (bench.py's timed call; with the ring fold on, the run-ahead filter
+    pipeline of cc_api.hip fold_windows_loop) in calls of 1, 2, 3, 5, 8, ... windows, each call's
+    last window vs the oracle; then the whole stream in one call. Returns the first bad window."""
+    nwin = len(want["checksums"])
+    sizes = [1, 2, 3, 5, 8, 13]
+    ds.reset()
+    w0, i = 0, 0
+    while w0 < nwin:
+        k = min(sizes[i % len(sizes)], nwin - w0)
+        lo, hi = w0 * W, min(ts.numel(), (w0 + k) * W)
+        assert ds.fold_windows(ts[lo:hi], td[lo:hi], W) == k
+        w0 += k
+        i += 1
+        if ds.checksum()[0] != int(want["checksums"][w0 - 1]):
+            return w0 - 1
+    ds.reset()
+    assert ds.fold_windows(ts, td, W) == nwin
+    if ds.checksum()[0] != int(want["checksums"][nwin - 1]) or \
+            not np.array_equal(ds.dense().astype(np.int64), want["final"]):
+        return nwin - 1
+    return None
 
 
 def main():

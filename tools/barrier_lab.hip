@@ -60,6 +60,62 @@ __device__ __forceinline__ void grid_barrier(const Bar& b, unsigned nblocks, uns
     __syncthreads();
 }
 
+// two-level grid barrier (round-5 verdict): workgroup b arrives on the counter of its XCD group
+// (b % 8: the dispatcher places workgroups on the 8 XCDs round-robin), each on a 128-B line of its
+// own; the last arrival of a group arrives on the top counter, whose last arrival bumps the
+// generation. 8 + (blocks / 8) arrivals per counter instead of `blocks` on one. spin: poll without
+// s_sleep.
+struct Bar2 {
+    unsigned* group;   // 8 counters, 32 words apart
+    unsigned* top;     // own line
+    unsigned* gen;     // own line
+    unsigned* err;
+};
+template <bool kSpin>
+__device__ __forceinline__ void grid_barrier2(const Bar2& b, unsigned nblocks, unsigned& g) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned x = blockIdx.x & 7u;
+        const unsigned members = nblocks / 8 + ((nblocks & 7u) > x ? 1u : 0u);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        unsigned* gc = b.group + 32 * x;
+        const unsigned a = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        bool released = false;
+        if (a == members - 1) {
+            __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned groups = nblocks < 8 ? nblocks : 8u;
+            const unsigned t = __hip_atomic_fetch_add(b.top, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            if (t == groups - 1) {
+                __hip_atomic_store(b.top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(b.gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                released = true;
+            }
+        }
+        if (!released) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(b.gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) {
+                if (__hip_atomic_load(b.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;   // a peer timed out
+                if (!kSpin) __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) { atomicOr(b.err, 1u); break; }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        g += 1;
+    }
+    __syncthreads();
+}
+
+template <bool kSpin>
+__global__ void k_barriers2(Bar2 b, unsigned iters, unsigned* __restrict__ a, unsigned n, int store) {
+    unsigned g = 0;
+    if (threadIdx.x == 0) g = __hip_atomic_load(b.gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    for (unsigned it = 0; it < iters; ++it) {
+        if (store && i < n) a[i] = a[i] + it;
+        grid_barrier2<kSpin>(b, gridDim.x, g);
+    }
+}
+
 __global__ void k_barriers(Bar b, unsigned iters, unsigned* __restrict__ a, unsigned n, int store) {
     unsigned g = 0;
     if (threadIdx.x == 0) g = __hip_atomic_load(b.gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
@@ -100,7 +156,11 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e1));
     float ms = 0.f;
     printf("{\"cus\": %d, \"iters\": %u", cus, iters);
-    const unsigned blocks_list[] = {(unsigned)cus, 2u * cus, 4u * cus};
+    unsigned* ctl2 = nullptr;
+    CK(hipMalloc(&ctl2, 4096));
+    CK(hipMemset(ctl2, 0, 4096));
+    Bar2 b2{ctl2, ctl2 + 8 * 32, ctl2 + 9 * 32, ctl + 64};
+    const unsigned blocks_list[] = {32u, 64u, (unsigned)cus, 2u * cus, 4u * cus};
     for (unsigned threads : {256u, 1024u}) {
         for (unsigned blocks : blocks_list) {
             if (threads == 1024 && blocks > (unsigned)cus) continue;
@@ -137,6 +197,21 @@ int main(int argc, char** argv) {
                 CK(hipEventSynchronize(e1));
                 CK(hipEventElapsedTime(&ms, e0, e1));
                 printf(", \"cg%s_us_%ux%u\": %.3f", store ? "_store" : "", blocks, threads, ms * 1e3 / iters);
+                for (int spin = 0; spin < 2; ++spin) {            // the two-level barrier, s_sleep / spin
+                    void* args2[] = {&b2, (void*)&iters, &a, (void*)&n, &store};
+                    const void* k2 = spin ? (const void*)k_barriers2<true> : (const void*)k_barriers2<false>;
+                    CK(hipLaunchCooperativeKernel(k2, dim3(blocks), dim3(threads), args2, 0, s));
+                    CK(hipStreamSynchronize(s));
+                    CK(hipEventRecord(e0, s));
+                    CK(hipLaunchCooperativeKernel(k2, dim3(blocks), dim3(threads), args2, 0, s));
+                    CK(hipEventRecord(e1, s));
+                    CK(hipEventSynchronize(e1));
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    printf(", \"bar2%s%s_us_%ux%u\": %.3f", spin ? "_spin" : "", store ? "_store" : "", blocks, threads,
+                           ms * 1e3 / iters);
+                    CK(hipMemcpy(&e, ctl + 64, 4, hipMemcpyDeviceToHost));
+                    if (e) { printf(", \"spin_cap_hit\": 1}\n"); return 2; }
+                }
             }
         }
     }
