@@ -40,7 +40,7 @@ import torch.distributed as dist  # noqa: E402
 import gsgpu  # noqa: E402
 from gsgpu import gen  # noqa: E402
 from gsgpu._abi import (GS_K_COMPRESS, GS_K_EXPORT, GS_K_FOLD, GS_K_MERGE, GS_K_RING,  # noqa: E402
-                        GS_K_UNION, GS_TIMING_MASK, LIB_PATH, lib_source_sha)
+                        GS_TIMING_MASK, LIB_PATH, lib_source_sha)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "streaming CC edges/sec (RMAT-26) at 1/2/4/8 MI355X + % of HBM roofline"
@@ -51,6 +51,7 @@ WORKLOADS = {  # name: (generator, scale or n, edge factor, window log2, seed)
     "c2": ("rmat", 20, 16, 20, 1), "c4": ("er", 24, 1, 20, 2), "c5": ("rmat", 24, 16, 16, 3),
     # SURVEY.md 8(f) rows (bench_rows.py): edge-file ingestion of 2^24 lines; BipartitenessCheck
     "parse": ("parse", 24, 1, 24, 1), "bip": ("bip", 22, 16, 20, 1),
+    "parse_file": ("parse_file", 20, 16, 20, 1),
 }
 
 
@@ -64,7 +65,9 @@ def parse():
                          "stream as one window; c2: RMAT-20 EF16, 2^20-edge windows; c4: Erdos-Renyi n=m=2^24, "
                          "2^20-edge windows; c5: RMAT-24 EF16, 2^16-edge windows + per-window emission latency; "
                          "parse: edge-file ingestion (gs_parse_edges) of an RMAT-24 stream's text, 2^24 lines; "
-                         "bip: BipartitenessCheck (gs_bip_*) on a bipartite RMAT-22 EF16 stream, 2^20-edge windows")
+                         "bip: BipartitenessCheck (gs_bip_*) on a bipartite RMAT-22 EF16 stream, 2^20-edge windows; "
+                         "parse_file: config 2's stream as text in pinned host memory streamed through gs_cc_fold_text "
+                         "(chunked H2D, device parse, folds + closes per window; PCIe-inclusive)")
     ap.add_argument("--scale", type=int, default=None, help="override the workload's RMAT scale")
     ap.add_argument("--edge-factor", type=int, default=None)
     ap.add_argument("--window-log2", type=int, default=None, help="global window = 2^this edges")
@@ -136,9 +139,9 @@ def main():
     sys.stdout.flush()
     out = os.fdopen(os.dup(1), "w", buffering=1)
     os.dup2(2, 1)
-    if a.kind in ("parse", "bip"):                # SURVEY.md 8(f) rows, one GPU
+    if a.kind in ("parse", "bip", "parse_file"):  # SURVEY.md 8(f) rows, one GPU
         import bench_rows
-        (bench_rows.run_parse if a.kind == "parse" else bench_rows.run_bip)(a, out)
+        {"parse": bench_rows.run_parse, "bip": bench_rows.run_bip, "parse_file": bench_rows.run_parse_file}[a.kind](a, out)
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -217,7 +220,7 @@ def main():
             ds.delta_async(hv[w & 1], hl[w & 1])
             consume(ds.emit_wait(1))
 
-    fold_mask = GS_TIMING_MASK | (1 << GS_K_FOLD) | (1 << GS_K_RING) | (1 << GS_K_UNION) | \
+    fold_mask = GS_TIMING_MASK | (1 << GS_K_FOLD) | (1 << GS_K_RING) | \
         ((1 << GS_K_MERGE) | (1 << GS_K_EXPORT) if world > 1 else 0)
 
     # the plain per-window loop runs inside the library (gs_cc_fold_windows: one ABI call per step
@@ -264,10 +267,6 @@ def main():
     final_sum = ds.checksum() if rank == 0 else None
     young_ms, young_n = ds.kernel_time(GS_K_FOLD)
     ring_ms, ring_n = ds.kernel_time(GS_K_RING)
-    try:
-        union_ms, union_n = ds.kernel_time(GS_K_UNION)
-    except gsgpu.GsError:                             # a library without the split fold (A/B of an old build)
-        union_ms, union_n = 0.0, 0
     young_e, ring_e = (ds.kernel_units(k) for k in (GS_K_FOLD, GS_K_RING))
     merge_ms, _ = ds.kernel_time(GS_K_MERGE)
     export_ms, _ = ds.kernel_time(GS_K_EXPORT)
@@ -326,15 +325,10 @@ def main():
         per_edge_survey = eb + 8 if a.id_bits == 32 else 2 * 16
         total_edges = a.steps * E_rank * world
         folds = nwin                                  # the timed launches: the last step's
-        fold_win_ms = (young_ms + ring_ms + union_ms) / max(folds, 1) or float("nan")
-        # the dominant kernel: the steady fold — k_fold_ring, or in gs_cc_fold_windows the split
-        # steady window k_filter (run ahead on its own stream) + k_union (ordered): bytes per launch
-        # from the edges each timed launch actually folded (a long fold call is cut into launches of
-        # at most 2^24 edges); a split window's time is the SUM of its two launches' durations (no
-        # credit for the overlap)
-        if ring_n and union_n:
-            kernel, avg_ms, n_l, e_l = "k_filter+k_union", ring_ms / ring_n + union_ms / union_n, ring_n, ring_e / ring_n
-        elif ring_n:
+        fold_win_ms = (young_ms + ring_ms) / max(folds, 1) or float("nan")
+        # the dominant kernel: the steady fold k_fold_ring, bytes per launch from the edges each timed
+        # launch actually folded (a long fold call is cut into launches of at most 2^24 edges)
+        if ring_n:
             kernel, avg_ms, n_l, e_l = "k_fold_ring", ring_ms / ring_n, ring_n, ring_e / ring_n
         else:                                        # no steady launches (small ids: plain k_fold)
             kernel, avg_ms, n_l, e_l = "k_fold (every window)", fold_win_ms, folds, W_rank
@@ -396,13 +390,9 @@ def main():
                 "edges_per_launch": e_l,
                 "avg_launch_ms": avg_ms,
                 "launches": n_l,
-                "split": {"filter_avg_ms": ring_ms / ring_n, "union_avg_ms": union_ms / union_n,
-                          "filter_only_achieved": per_edge * e_l / (ring_ms / ring_n * 1e-3) / 1e9}
-                if ring_n and union_n else None,
                 "definition": "dominant kernel: %d B per edge (edge read + 2 parent words, SURVEY.md 8(d); 4-B parent "
                               "words for int64 ids too) x the edges each launch folded / its average launch duration "
-                              "(HIP events on the launch stream, the last step of the timed region); a split steady "
-                              "window (k_filter + k_union) counts the sum of both launches" % per_edge,
+                              "(HIP events on the launch stream, the last step of the timed region)" % per_edge,
                 "fold_all": {"achieved": per_edge * W_rank / (fold_win_ms * 1e-3) / 1e9,
                              "frac": per_edge * W_rank / (fold_win_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                              "ms_per_window": fold_win_ms, "young_launches": young_n,
@@ -417,7 +407,7 @@ def main():
                                        "never moved)" % per_edge},
             },
             "kernels": {
-                "fold_share": (young_ms + ring_ms + union_ms) / (elapsed / a.steps * 1e3),   # timed: the last step's folds
+                "fold_share": (young_ms + ring_ms) / (elapsed / a.steps * 1e3),   # timed: the last step's folds
                 "compress_ms_per_window": comp_ms / max(comp_n, 1),
                 "compress_share": comp_ms / (elapsed / a.steps * 1e3),
             },

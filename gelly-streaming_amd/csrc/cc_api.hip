@@ -128,20 +128,6 @@ struct gs_cc {
     int cus = 0;                         // compute units: k_fold_ring grid
     void* ingest = nullptr;              // streaming text ingestion state (parse.hip), freed by ingest_free
     void (*ingest_free)(void*) = nullptr;
-    // run-ahead filter pipeline of gs_cc_fold_windows (cc_kernels.hpp k_filter / k_union): the
-    // filter of window w+1 runs on fstream while window w is unioned and closed on `stream`
-    struct Pipe {
-        hipStream_t fs = nullptr;
-        hipEvent_t filt[2] = {nullptr, nullptr};     // filter x done (parity x & 1)
-        hipEvent_t close = nullptr;                  // the latest close of the ordered stream
-        uint2* surv[2] = {nullptr, nullptr};         // survivor buffers (parity x & 1)
-        uint32_t* scnt[2] = {nullptr, nullptr};      // survivors per filter workgroup
-        size_t surv_bytes = 0;
-        int pending = -1;                            // parity of a filter whose union is not enqueued yet
-        bool flags_ok = true;                        // ... and whether its giant flags still hold
-        unsigned grid[2] = {0, 0};
-        uint64_t region[2] = {0, 0};
-    } pipe;
     // GS_CC_SPARSE_IDS: id -> slot table; cap (above) = slots = 2^hbits + 1
     bool sparse = false;
     int64_t* keys = nullptr;             // 2^hbits slot keys (INT64_MIN = empty)
@@ -319,8 +305,6 @@ struct DebugEnv {
     uint64_t young_first_min = kYoungFirstMinWg;    // GSGPU_YOUNG_FIRST_MIN: workgroup floor of the first young launch
     bool list_close = true;                         // GSGPU_LIST_CLOSE=0: no list-mode closes (A/B)
     bool small_claim = true;                        // GSGPU_SMALL_CLAIM=0: small k_fold launches without claims (A/B)
-    int run_ahead = 1;                              // GSGPU_RUN_AHEAD=0: gs_cc_fold_windows without the split filter;
-                                                    // 2: split but serialised on the ordered stream (A/B of the overlap)
     DebugEnv() {
         const char* e = getenv("GSGPU_FOLD_STATS");
         fold_stats = e && atoi(e) != 0;
@@ -341,8 +325,6 @@ struct DebugEnv {
         if (e && *e) list_close = atoi(e) != 0;
         e = getenv("GSGPU_SMALL_CLAIM");
         if (e && *e) small_claim = atoi(e) != 0;
-        e = getenv("GSGPU_RUN_AHEAD");
-        if (e && *e) run_ahead = atoi(e);
 
     }
 };
@@ -716,13 +698,6 @@ int compress_impl(gs_cc_t* h) {
                            (h->closes == 0 || h->edges_since_reset - h->pick_edges >= kPickMinEdges);
         const bool pick = force || h->closes < kEarlyPicks;
         if (force) h->pick_edges = h->edges_since_reset;
-        // a forced re-pick may rebuild gbits and the hot set for ANOTHER component: no run-ahead
-        // filter may read them meanwhile (the close waits for the outstanding one), and that
-        // filter's giant flags are dropped (fold_windows_loop, cc_kernels.hpp k_filter)
-        if (force && h->pipe.pending >= 0) {
-            GS_HIP(hipStreamWaitEvent(h->stream, h->pipe.filt[h->pipe.pending & 1], 0));
-            h->pipe.flags_ok = false;
-        }
         ListClose lc;
         unsigned grid = grid_for(h->cap, 1024, kCompressGrid);
         if (h->lctl) {
@@ -1153,16 +1128,6 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->estream) (void)hipStreamDestroy(h->estream);
     if (h->tmp) (void)hipFree(h->tmp);
     if (h->ingest && h->ingest_free) h->ingest_free(h->ingest);
-    if (h->pipe.fs) {
-        (void)hipStreamSynchronize(h->pipe.fs);
-        for (auto e : h->pipe.filt) if (e) (void)hipEventDestroy(e);
-        if (h->pipe.close) (void)hipEventDestroy(h->pipe.close);
-        for (int k = 0; k < 2; ++k) {
-            if (h->pipe.surv[k]) (void)hipFree(h->pipe.surv[k]);
-            if (h->pipe.scnt[k]) (void)hipFree(h->pipe.scnt[k]);
-        }
-        (void)hipStreamDestroy(h->pipe.fs);
-    }
     if (h->own) (void)hipStreamDestroy(h->own);
     delete h;
     return GS_OK;
@@ -1328,163 +1293,19 @@ int gs_cc_close_window(gs_cc_t* h) {
     return compress_impl(h);
 }
 
-// ---- run-ahead filter pipeline (cc_kernels.hpp k_filter / k_union) ----
-// Survivor buffers for windows of up to n edges: per filter workgroup a region of every edge it
-// can read (grid-stride passes x 4096 edges), two buffers (filter x writes x & 1; the union of
-// x - 2 that read it precedes close x - 2, which filter x waits for).
-static int pipe_ensure(gs_cc_t* h, uint64_t n) {
-    gs_cc::Pipe& p = h->pipe;
-    if (!p.fs) {
-        GS_HIP(hipStreamCreateWithFlags(&p.fs, hipStreamNonBlocking));
-        for (auto& e : p.filt) GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        GS_HIP(hipEventCreateWithFlags(&p.close, hipEventDisableTiming));
-    }
-    const uint64_t groups = n / 4;
-    const unsigned grid = grid_for(groups, kHotThreads, (unsigned)std::max(h->cus, 1));
-    const uint64_t stride = (uint64_t)grid * kHotThreads;
-    const uint64_t region = ((groups + stride - 1) / stride) * kHotThreads * 4;
-    const size_t bytes = (size_t)grid * region * sizeof(uint2);
-    if (bytes > p.surv_bytes) {
-        GS_HIP(hipStreamSynchronize(p.fs));
-        GS_HIP(hipStreamSynchronize(h->stream));
-        for (int k = 0; k < 2; ++k) {
-            if (p.surv[k]) (void)hipFree(p.surv[k]);
-            if (p.scnt[k]) (void)hipFree(p.scnt[k]);
-            p.surv[k] = nullptr;
-            p.scnt[k] = nullptr;
-        }
-        p.surv_bytes = 0;
-        for (int k = 0; k < 2; ++k)
-            if (hipMalloc(&p.surv[k], bytes) != hipSuccess || hipMalloc(&p.scnt[k], 4096 * sizeof(uint32_t)) != hipSuccess) {
-                (void)hipGetLastError();
-                return fail(GS_ERR_NOMEM, "fold_windows: survivor buffers of %zu bytes", bytes);
-            }
-        p.surv_bytes = bytes;
-    }
-    return GS_OK;
-}
-
-// The filter of window x (its edges at a, b; n a multiple of 4) on the filter stream, after the
-// ordered stream's latest close: survivors into buffer x & 1.
-extern "C++" template <typename IdT>
-static int pipe_filter(gs_cc_t* h, uint64_t x, const IdT* a, const IdT* b, uint64_t n) {
-    gs_cc::Pipe& p = h->pipe;
-    const int k = (int)(x & 1);
-    ensure_stats(h);
-    if (dbg().run_ahead == 2) GS_HIP(hipEventRecord(p.close, h->stream));   // serialised: after everything
-    GS_HIP(hipStreamWaitEvent(p.fs, p.close, 0));
-    bool build = false;
-    const HotArgs hot = ring_hot_args(h, &build);
-    FoldArgs f{n, h->parent, nullptr, nullptr, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
-    const uint64_t groups = n / 4;
-    const unsigned grid = grid_for(groups, kHotThreads, (unsigned)std::max(h->cus, 1));
-    const uint64_t stride = (uint64_t)grid * kHotThreads;
-    const uint64_t region = ((groups + stride - 1) / stride) * kHotThreads * 4;
-    const SurvArgs sv{p.surv[k], p.scnt[k], region};
-    KTimer t(h, GS_K_RING, n);
-    hipEvent_t stop = build ? nullptr : t.stop();
-    if (h->dstats) klaunch(k_filter<IdT, true>, dim3(grid), dim3(kHotThreads), p.fs, t.start(), stop, a, b, f, hot, sv);
-    else klaunch(k_filter<IdT, false>, dim3(grid), dim3(kHotThreads), p.fs, t.start(), stop, a, b, f, hot, sv);
-    if (build) launch_warm_build(h, t.stop(), p.fs);
-    GS_HIP(hipGetLastError());
-    GS_HIP(hipEventRecord(p.filt[k], p.fs));                  // after the warm build: a union waits for it too
-    p.grid[k] = grid;
-    p.region[k] = region;
-    p.pending = (int)x;
-    p.flags_ok = true;
-    return GS_OK;
-}
-
-constexpr unsigned kUnionSplit = 8;
-// The ordered half of window x: its survivors unioned on h->stream once its filter is done.
-static int pipe_union(gs_cc_t* h, uint64_t x, uint64_t n) {
-    gs_cc::Pipe& p = h->pipe;
-    const int k = (int)(x & 1);
-    GS_HIP(hipStreamWaitEvent(h->stream, p.filt[k], 0));
-    FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
-    f.mark_len = h->mark_ctr;
-    f.cbits = kUseCbits ? h->cbits : nullptr;
-    if (h->hkbits[0]) f.hbits = h->hkbits[h->closes & 1];
-    else h->hkbits_ok = false;
-    h->ilist_ok = false;
-    const SurvArgs sv{p.surv[k], p.scnt[k], p.region[k]};
-    // one survivor per thread where a window has up to ~grid x 2^11 of them (each thread's unions run
-    // one after another: a dependent chain of parent reads and CASes per survivor); the workgroups
-    // past a region's count exit at once
-    const unsigned split = kUnionSplit;
-    const uint32_t flags_ok = p.flags_ok ? 1u : 0u;
-    KTimer t(h, GS_K_UNION, n);
-    const dim3 grid(p.grid[k], split);
-    if (h->mark) {
-        if (h->dstats) klaunch(k_union<true, true>, grid, dim3(kUnionThreads), h->stream, t.start(), t.stop(), f, sv, flags_ok);
-        else klaunch(k_union<true, false>, grid, dim3(kUnionThreads), h->stream, t.start(), t.stop(), f, sv, flags_ok);
-    } else {
-        if (h->dstats) klaunch(k_union<false, true>, grid, dim3(kUnionThreads), h->stream, t.start(), t.stop(), f, sv, flags_ok);
-        else klaunch(k_union<false, false>, grid, dim3(kUnionThreads), h->stream, t.start(), t.stop(), f, sv, flags_ok);
-    }
-    GS_HIP(hipGetLastError());
-    p.pending = -1;
-    return GS_OK;
-}
-
 // The per-window host loop of gs_cc_fold_windows (fold, then close or merge), enqueued on h->stream.
-// Steady windows (past the young forest, where the ring fold would run: dense device SoA ids,
-// 16-B aligned windows of at most kInternalCloseEdges edges) are split: k_filter of window w+1 on
-// the filter stream runs while window w's survivors are unioned (k_union), exchanged and closed on
-// h->stream. The filter of window x waits for the close of window x - 2 only.
+// (Round 5 measured a split of the steady fold here — a read-only giant filter run one window ahead
+// on a stream of its own, the ordered unions after it — and removed it: DESIGN.md §4.)
 static int fold_windows_loop(gs_cc_t* h, gs_comm_t* comm, int mode, const char* a, const char* b, uint64_t n,
                              uint64_t window_edges, uint64_t* windows_out) {
     const size_t esz = h->cfg.id_bits / 8;
     const int dev = (n && is_device_pointer(a) && is_device_pointer(b)) ? 1 : 0;
-    const bool aligned = (((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0) &&
-                         (window_edges * esz) % 16 == 0;
-    const bool pipe_on = dev && aligned && dbg().run_ahead != 0 && !h->sparse && h->hot && use_ring(h) &&
-                         window_edges >= 4 && window_edges <= kInternalCloseEdges;
-    const uint64_t young_limit = h->cap / 4;
-    auto eligible = [&](uint64_t edges_before, uint64_t m) { return pipe_on && edges_before >= young_limit && m >= 4; };
-    auto filter = [&](uint64_t x, uint64_t off, uint64_t m) -> int {
-        if (esz == 4)
-            return pipe_filter<uint32_t>(h, x, reinterpret_cast<const uint32_t*>(a + off * esz),
-                                         reinterpret_cast<const uint32_t*>(b + off * esz), m & ~(uint64_t)3);
-        return pipe_filter<int64_t>(h, x, reinterpret_cast<const int64_t*>(a + off * esz),
-                                    reinterpret_cast<const int64_t*>(b + off * esz), m & ~(uint64_t)3);
-    };
-    if (pipe_on) {
-        GS_TRY(pipe_ensure(h, window_edges));
-        GS_HIP(hipEventRecord(h->pipe.close, h->stream));     // the caller's edges and everything before
-        h->pipe.pending = -1;
-    }
     uint64_t w = 0;
     for (uint64_t off = 0; off < n; off += window_edges, ++w) {
         const uint64_t m = std::min(window_edges, n - off);
-        if (eligible(h->edges_since_reset, m)) {
-            if (h->pipe.pending != (int64_t)w) GS_TRY(filter(w, off, m));   // not filtered ahead
-            const uint64_t m4 = m & ~(uint64_t)3;
-            h->compressed = false;
-            h->minkey_valid = false;
-            GS_TRY(pipe_union(h, w, m4));
-            if (m4 < m) {                                       // a last window's < 4-edge tail
-                if (esz == 4) launch_fold<uint32_t, false>(h, a + (off + m4) * esz, b + (off + m4) * esz, m - m4, false);
-                else launch_fold<int64_t, false>(h, a + (off + m4) * esz, b + (off + m4) * esz, m - m4, false);
-                GS_HIP(hipGetLastError());
-            }
-            h->edges_since_reset += m;
-            // the next window's filter, after the latest close (w - 1's): it runs while this window
-            // is unioned, exchanged and closed
-            if (off + window_edges < n && dbg().run_ahead == 1) {
-                const uint64_t m2 = std::min(window_edges, n - off - window_edges);
-                if (eligible(h->edges_since_reset, m2)) GS_TRY(filter(w + 1, off + window_edges, m2));
-            }
-        } else {
-            GS_TRY(fold_impl(h, a + off * esz, b + off * esz, m, false, h->cfg.id_bits, dev));   // (no settle: above)
-        }
+        GS_TRY(fold_impl(h, a + off * esz, b + off * esz, m, false, h->cfg.id_bits, dev));   // (no settle: above)
         GS_TRY(comm ? gs_cc_merge_window(h, comm, mode) : gs_cc_close_window(h));
-        if (pipe_on) GS_HIP(hipEventRecord(h->pipe.close, h->stream));
         if (windows_out) *windows_out = w + 1;
-    }
-    if (h->pipe.pending >= 0) {                                 // (an error path left a filter unconsumed)
-        GS_HIP(hipStreamWaitEvent(h->stream, h->pipe.filt[h->pipe.pending & 1], 0));
-        h->pipe.pending = -1;
     }
     return GS_OK;
 }
@@ -1921,7 +1742,7 @@ int gs_cc_timing(gs_cc_t* h, int enable) {
     GS_TRY(resolve_timing(h));
     h->timing = enable != 0;
     h->timing_mask = (enable & GS_TIMING_MASK) ? ((uint32_t)enable & 0xFFu) : ~0u;
-    if (h->timing_mask & (1u << GS_K_FOLD)) h->timing_mask |= (1u << GS_K_RING) | (1u << GS_K_UNION);   // "fold" = every launch kind
+    if (h->timing_mask & (1u << GS_K_FOLD)) h->timing_mask |= (1u << GS_K_RING);   // "fold" = every launch kind
     for (int k = 0; k < GS_K_COUNT; ++k) { h->total_ms[k] = 0; h->launches[k] = 0; h->units[k] = 0; }
     return GS_OK;
 }

@@ -1132,170 +1132,6 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
     }
 }
 
-// ---- run-ahead split of the steady fold (gs_cc_fold_windows) ----
-// k_fold_ring does two things per window: the giant FILTER (LDS hot set, warm set, gbits: read-only,
-// ~90 % of its time) and the UNIONS of the survivors (parent gathers, CAS hooks, claims). Only the
-// unions must run in window order between the closes; the filter of window w+1 may run while window
-// w is unioned, exchanged and closed, because what it reads is monotone between giant re-picks:
-// components only merge until reset, so a gbits bit / hot or warm entry, however stale, still says
-// "this vertex is in the giant's component", and an edge with both endpoints there is a no-op for
-// every later emission. k_filter writes the survivors of a window (with the filter's giant flags in
-// bit 31 of each id, as the ring did) into its workgroup's region of a survivor buffer; k_union then
-// unions them on the ordered stream. The host (cc_api.hip fold_windows_loop) keeps the filter one
-// window ahead on a stream of its own, and drains it around a forced giant re-pick — the one close
-// that may rebuild gbits / the hot set for ANOTHER component — whose outstanding filters' giant
-// flags it then drops (the union re-derives those endpoints from parent[]; the filter's drops stay
-// valid: two endpoints in one component stay in one component).
-struct SurvArgs {
-    uint2* out;          // survivors: workgroup b's region at out + b * region
-    uint32_t* cnt;       // survivors per region (the filter's grid)
-    uint64_t region;     // pairs per region (>= the edges a filter workgroup reads)
-};
-
-template <typename IdT, bool STATS>
-__global__ __launch_bounds__(kHotThreads) void k_filter(const IdT* __restrict__ a, const IdT* __restrict__ b,
-                                                        FoldArgs f, HotArgs hot, SurvArgs sv) {
-    __shared__ __attribute__((aligned(16))) uint2 tab[kHotBuckets];
-    __shared__ uint32_t s_pos;
-    const uint64_t n = f.n;
-    const bool filt = *f.giant != kInvalid;          // uniform: the slot of the latest close it waited for
-    if (filt) lds_fill<2 * kHotBuckets>(reinterpret_cast<uint32_t*>(tab), reinterpret_cast<const uint32_t*>(hot.table), 2 * kHotBuckets);
-    // giant flags ride in bit 31 of the survivors' ids (ids < 2^31)
-    const bool flags = filt && f.rc.cap <= 0x80000000u;
-    const uint32_t budget = hot.budget ? *hot.budget : 1u;
-    const uint64_t sample_edges = (hot.periodic || budget) ? hot.sample_edges : 0;
-    const bool warm_ok = filt && hot.warm && *hot.warm_valid != 0;
-    const uint64_t count_edges = (filt && hot.wkeys && hot.warm_valid && *hot.warm_valid == 0) ? hot.count_edges : 0;
-    if (threadIdx.x == 0) s_pos = 0;
-    __syncthreads();
-    if (blockIdx.x == 0 && threadIdx.x == 0 && hot.budget && budget) *hot.budget = budget - 1;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && hot.wkeys)
-        *hot.wctl = (min(count_edges, n / 4 * 4) + 255) / 256 * 256;
-    const int lane = threadIdx.x & 63;
-    uint2* const out = sv.out + (uint64_t)blockIdx.x * sv.region;
-    const uint64_t groups = n / 4;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint64_t nvalid = 0, nkept = 0;
-    for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < groups; g0 += stride) {
-        const uint64_t g = g0 + lane;
-        uint32_t u[4] = {0, 0, 0, 0}, v[4] = {0, 0, 0, 0};
-        bool ok[4] = {false, false, false, false};
-        uint32_t gf[4] = {0u, 0u, 0u, 0u};
-        if (g < groups) {
-            bool oka[4] = {true, true, true, true}, okb[4] = {true, true, true, true};
-            Raw4<IdT> ra, rb;
-            ra.load(a, g);
-            rb.load(b, g);
-            ra.unpack(u, oka, f.rc.cap);
-            rb.unpack(v, okb, f.rc.cap);
-            bool bad = false;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                ok[k] = oka[k] && okb[k];
-                bad |= !ok[k];
-                if (!ok[k]) { u[k] = 0; v[k] = 0; }
-            }
-            if (bad) atomicOr(f.rc.err, 1u);
-        }
-        if (STATS) for (int k = 0; k < 4; ++k) nvalid += ok[k];
-        if (filt) filter_group<STATS, 4, true>(f, u, v, ok, tab, hot, g * 4 < sample_edges, warm_ok,
-                                               g0 * 4 < count_edges ? g0 / 64 : ~0ull, gf);
-        if (!flags) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) gf[k] = 0u;
-        }
-        const uint32_t c = (uint32_t)ok[0] + ok[1] + ok[2] + ok[3];
-        if (STATS) nkept += c;
-        uint32_t incl = c;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += y;
-        }
-        const uint32_t wtot = __shfl(incl, 63, 64);
-        if (wtot == 0) continue;                     // uniform
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&s_pos, wtot);   // LDS: the wave's place in the region
-        uint32_t pos = __shfl(base, 0, 64) + incl - c;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (!ok[k]) continue;
-            out[pos] = make_uint2(u[k] | ((gf[k] & 1u) << 31), v[k] | ((gf[k] >> 1) << 31));
-            ++pos;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) sv.cnt[blockIdx.x] = s_pos;
-    if (STATS) {
-        atomicAdd(&f.stats[0], nvalid);
-        atomicAdd(&f.stats[1], nvalid - nkept);
-    }
-}
-
-// The ordered half: union every survivor of a filtered window (region blockIdx.x of the buffer,
-// split over gridDim.y workgroups: passes blockIdx.y, blockIdx.y + gridDim.y, ...).
-// gR and the seen / hooked-root bitmaps follow the CURRENT giant slot (the close this union precedes
-// reads it), exactly as k_fold_ring's unions do; the survivors' giant flags are used only while
-// flags_ok (no forced giant re-pick since the filter ran) and a giant exists. MARK: the hooked roots
-// of a workgroup go to the hook log in LDS batches, one global atomic per batch.
-constexpr int kUnionThreads = 256;
-constexpr uint32_t kUnionLogBatch = 1024;
-template <bool MARK, bool STATS>
-__global__ __launch_bounds__(kUnionThreads) void k_union(FoldArgs f, SurvArgs sv, uint32_t flags_ok) {
-    __shared__ uint32_t s_log[MARK ? kUnionLogBatch : 1];
-    __shared__ uint32_t s_n;
-    __shared__ unsigned long long s_base;
-    const bool filt = *f.giant != kInvalid;          // uniform
-    if (!filt) f.sbits = nullptr;                    // the next close is a full pass
-    else f.hbits = nullptr;
-    const uint32_t gR = (filt && f.rc.cap <= 0x80000000u) ? f.giant[1] : kInvalid;
-    const bool use_flags = flags_ok && gR != kInvalid;
-    const uint32_t cnt = sv.cnt[blockIdx.x];
-    const uint2* in = sv.out + (uint64_t)blockIdx.x * sv.region;
-    const uint32_t idmask = (f.rc.cap <= 0x80000000u) ? 0x7FFFFFFFu : 0xFFFFFFFFu;
-    if (MARK && threadIdx.x == 0) s_n = 0;
-    if (MARK) __syncthreads();
-    FoldStats st;
-    const int lane = threadIdx.x & 63;
-    const uint64_t lt = (1ull << lane) - 1;
-    const uint32_t step = blockDim.x * gridDim.y;
-    for (uint32_t i0 = blockIdx.y * blockDim.x; i0 < cnt; i0 += step) {      // uniform trip count
-        const uint32_t i = i0 + threadIdx.x;
-        const bool ok1 = i < cnt;
-        const uint2 e = ok1 ? in[i] : make_uint2(0u, 0u);
-        const uint32_t u[1] = {e.x & idmask}, v[1] = {e.y & idmask};
-        const uint32_t gf[1] = {use_flags ? ((e.x >> 31) | ((e.y >> 31) << 1)) : 0u};
-        const bool ok[1] = {ok1};
-        uint32_t mk[1] = {kInvalid};
-        union_group_g<MARK, STATS, 1>(f, u, v, ok, gf, use_flags ? gR : kInvalid, st, mk);
-        if (MARK) {
-            const uint64_t bm = __ballot(mk[0] != kInvalid);
-            uint32_t wpos = 0;
-            if (lane == 0 && bm) wpos = atomicAdd(&s_n, (uint32_t)__popcll(bm));
-            wpos = __shfl(wpos, 0, 64);
-            const uint32_t at = wpos + (uint32_t)__popcll(bm & lt);
-            if (mk[0] != kInvalid && at < kUnionLogBatch) s_log[at] = mk[0];
-            __syncthreads();
-            const uint32_t nb = s_n;
-            // flush when the batch may not hold another full pass (or on the last pass)
-            if (nb + blockDim.x > kUnionLogBatch || i0 + step >= cnt) {
-                if (threadIdx.x == 0) s_base = nb ? atomicAdd(f.mark_len, (unsigned long long)min(nb, kUnionLogBatch)) : 0ull;
-                __syncthreads();
-                for (uint32_t j = threadIdx.x; j < min(nb, kUnionLogBatch); j += blockDim.x) f.mark[s_base + j] = s_log[j];
-                __syncthreads();
-                if (threadIdx.x == 0) s_n = 0;
-                __syncthreads();
-            }
-        }
-    }
-    if (STATS) {
-        atomicAdd(&f.stats[2], (unsigned long long)st.early);
-        atomicAdd(&f.stats[3], (unsigned long long)st.hooks);
-        atomicAdd(&f.stats[4], (unsigned long long)st.casfail);
-        atomicAdd(&f.stats[5], (unsigned long long)st.inits);
-    }
-}
-
 // Warm build without global counters (the count launch's per-endpoint atomicAdd into 2^B 16-bit
 // counters cost ~390 us and four band scans of them ~400 us per RMAT-26 build): the count launch
 // writes its LDS-miss giant endpoints into key slots (512 per wave step, kInvalid where none);
@@ -1675,7 +1511,7 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
                                                   uint32_t* __restrict__ cbits, uint32_t* __restrict__ dbits,
                                                   const uint32_t* __restrict__ samp_in, uint32_t* __restrict__ samp_out,
                                                   const uint32_t* __restrict__ hb_in, uint32_t* __restrict__ hb_next) {
-    __shared__ uint32_t s_g, s_inc, s_clear;
+    __shared__ uint32_t s_g, s_inc, s_clear, s_ren;
     __shared__ PickLds L;
     // no giant known (none picked yet, or a re-pick found none): the mode of the labels the last
     // full pass recorded at the sample positions, the same in every workgroup (a giant that forms
@@ -1688,6 +1524,9 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
         const uint32_t g = (g0 == kInvalid) ? kInvalid : find_root_ro(parent, g0);
         s_g = g;
         s_inc = (g != kInvalid && g == in[1] && !rebuild_seen) ? 1u : 0u;
+        // the giant's root changed (a smaller id joined it) but it is the component gbits were
+        // built for: the full pass labels its members g without walking (s_ren)
+        s_ren = (!s_inc && g != kInvalid && in[1] != kInvalid && find_root_ro(parent, in[1]) == g) ? 1u : 0u;
         s_clear = 0;
         if (blockIdx.x == 0) {
             if (g != kInvalid) {
@@ -1761,6 +1600,11 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
         // parent word written since the last close is a root at the time of writing (a hook's lo, a
         // claim's gR, a halving's grandparent), so "unmarked" is exact.
         const bool usehb = hb_in != nullptr && in[1] == kInvalid;
+        // giant renamed (s_ren): a vertex whose gbits or cbits bit is set is in g's component (the bits
+        // were built for, or claimed under, its old root in[1], now below g; members point at in[1] or
+        // an ancestor of it): its label is g, no walk. (The 8 lanes of a bitmap word read it before
+        // any of them writes it below: one wave, in order.)
+        const bool ren = s_ren != 0;
         for (uint64_t blk = (uint64_t)blockIdx.x * 1024; blk < n; blk += (uint64_t)gridDim.x * 1024) {
             const uint32_t base = (uint32_t)blk + threadIdx.x * 4;
             uint32_t p[4];
@@ -1771,9 +1615,11 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
 #pragma unroll
                 for (int k = 0; k < 4; ++k) p[k] = ((uint64_t)base + k < n) ? parent[base + k] : kInvalid;
             }
+            uint32_t mem = 0;                        // rename: this thread's 4 member bits
+            if (ren && base < n) mem = ((gbits[base >> 5] | (cbits ? cbits[base >> 5] : 0u)) >> (base & 31)) & 15u;
             bool need[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) need[k] = p[k] != kInvalid && p[k] != base + k;
+            for (int k = 0; k < 4; ++k) need[k] = p[k] != kInvalid && p[k] != base + k && !((mem >> k) & 1u);
             if (usehb) {
                 uint32_t hw[4];
 #pragma unroll
@@ -1789,7 +1635,10 @@ __global__ __launch_bounds__(256) void k_compress(uint32_t* __restrict__ parent,
             for (int k = 0; k < 4; ++k) {
                 const uint32_t v = base + k;
                 uint32_t lab = p[k];
-                if (p[k] != kInvalid && p[k] != v && gp[k] != p[k]) {   // depth >= 2: walk, store the root
+                if ((mem >> k) & 1u) {                   // a renamed giant member
+                    lab = g;
+                    if (p[k] != g) parent[v] = g;
+                } else if (p[k] != kInvalid && p[k] != v && gp[k] != p[k]) {   // depth >= 2: walk, store the root
                     lab = find_root_ro(parent, gp[k]);
                     parent[v] = lab;
                 }
@@ -1832,7 +1681,7 @@ __global__ __launch_bounds__(256) void k_compress_list(uint32_t* __restrict__ pa
                                                   const uint32_t* __restrict__ samp_in, uint32_t* __restrict__ samp_out,
                                                   const uint32_t* __restrict__ hb_in, uint32_t* __restrict__ hb_next,
                                                   ListClose lc) {
-    __shared__ uint32_t s_g, s_inc, s_clear;
+    __shared__ uint32_t s_g, s_inc, s_clear, s_ren;
     __shared__ PickLds L;
     // no giant known (none picked yet, or a re-pick found none): the mode of the labels the last
     // full pass recorded at the sample positions, the same in every workgroup (a giant that forms
@@ -1854,6 +1703,9 @@ __global__ __launch_bounds__(256) void k_compress_list(uint32_t* __restrict__ pa
         const uint32_t g = (g0 == kInvalid) ? kInvalid : find_root_ro(parent, g0);
         s_g = g;
         s_inc = (g != kInvalid && g == in[1] && !rebuild_seen) ? 1u : 0u;
+        // the giant's root changed (a smaller id joined it) but it is the component gbits were
+        // built for: the full pass labels its members g without walking (s_ren)
+        s_ren = (!s_inc && g != kInvalid && in[1] != kInvalid && find_root_ro(parent, in[1]) == g) ? 1u : 0u;
         s_clear = 0;
         if (blockIdx.x == 0) {
             if (g != kInvalid) {
@@ -2005,6 +1857,11 @@ __global__ __launch_bounds__(256) void k_compress_list(uint32_t* __restrict__ pa
         // parent word written since the last close is a root at the time of writing (a hook's lo, a
         // claim's gR, a halving's grandparent), so "unmarked" is exact.
         const bool usehb = hb_in != nullptr && in[1] == kInvalid;
+        // giant renamed (s_ren): a vertex whose gbits or cbits bit is set is in g's component (the bits
+        // were built for, or claimed under, its old root in[1], now below g; members point at in[1] or
+        // an ancestor of it): its label is g, no walk. (The 8 lanes of a bitmap word read it before
+        // any of them writes it below: one wave, in order.)
+        const bool ren = s_ren != 0;
         for (uint64_t blk = (uint64_t)blockIdx.x * 1024; blk < n; blk += (uint64_t)gridDim.x * 1024) {
             const uint32_t base = (uint32_t)blk + threadIdx.x * 4;
             uint32_t p[4];
@@ -2015,9 +1872,11 @@ __global__ __launch_bounds__(256) void k_compress_list(uint32_t* __restrict__ pa
 #pragma unroll
                 for (int k = 0; k < 4; ++k) p[k] = ((uint64_t)base + k < n) ? parent[base + k] : kInvalid;
             }
+            uint32_t mem = 0;                        // rename: this thread's 4 member bits
+            if (ren && base < n) mem = ((gbits[base >> 5] | (cbits ? cbits[base >> 5] : 0u)) >> (base & 31)) & 15u;
             bool need[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) need[k] = p[k] != kInvalid && p[k] != base + k;
+            for (int k = 0; k < 4; ++k) need[k] = p[k] != kInvalid && p[k] != base + k && !((mem >> k) & 1u);
             if (usehb) {
                 uint32_t hw[4];
 #pragma unroll
@@ -2034,7 +1893,10 @@ __global__ __launch_bounds__(256) void k_compress_list(uint32_t* __restrict__ pa
             for (int k = 0; k < 4; ++k) {
                 const uint32_t v = base + k;
                 uint32_t lab = p[k];
-                if (p[k] != kInvalid && p[k] != v && gp[k] != p[k]) {   // depth >= 2: walk, store the root
+                if ((mem >> k) & 1u) {                   // a renamed giant member
+                    lab = g;
+                    if (p[k] != g) parent[v] = g;
+                } else if (p[k] != kInvalid && p[k] != v && gp[k] != p[k]) {   // depth >= 2: walk, store the root
                     lab = find_root_ro(parent, gp[k]);
                     parent[v] = lab;
                 }

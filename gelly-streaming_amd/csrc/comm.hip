@@ -797,7 +797,28 @@ int merge_window(gs_cc_t* h, gs_comm_t* c, int mode) {
     if (c->bound && (c->bound != h || c->mode != mode))
         return fail(GS_ERR_INVALID, "gs_cc_merge_window: this communicator serves another handle or mode "
                                     "(one communicator per summary and mode)");
-    if (!c->bound) { c->bound = h; c->mode = mode; c->reset_gen = in.reset_gen; }
+    if (!c->bound) {
+        // every rank sizes its exchange buffers from its own handle, and the speculative slots are
+        // sized from them on the sending and the receiving side alike (next_slot): agree once, when
+        // the communicator is bound, that every rank's capacity and pair width are the same
+        // (every rank sees every word, so all fail together on a mismatch)
+        const int P = c->world;
+        const unsigned long long mine = (unsigned long long)c->cap_pairs << 8 | c->pair_bytes;
+        c->hcnt[P] = mine;                           // (pinned: the copy reads it when it runs)
+        GS_HIP(hipMemcpyAsync(c->dcnt + P, c->hcnt + P, sizeof(mine), hipMemcpyHostToDevice, in.stream));
+        GS_TRY(allgather(c, c->dcnt + P, c->dcnt, sizeof(unsigned long long), in.stream));
+        GS_HIP(hipMemcpyAsync(c->hcnt, c->dcnt, P * sizeof(unsigned long long), hipMemcpyDeviceToHost, in.stream));
+        GS_HIP(hipStreamSynchronize(in.stream));
+        for (int q = 0; q < P; ++q)
+            if (c->hcnt[q] != mine)
+                return fail(GS_ERR_INVALID, "gs_cc_merge_window: rank %d's summary has %llu-pair / %llu-byte exchange "
+                            "buffers, rank %d's %llu / %llu: every rank needs the same vertex capacity and id mode",
+                            q, c->hcnt[q] >> 8, c->hcnt[q] & 0xFF, c->rank, (unsigned long long)c->cap_pairs,
+                            (unsigned long long)c->pair_bytes);
+        c->bound = h;
+        c->mode = mode;
+        c->reset_gen = in.reset_gen;
+    }
     if (mode != GS_MERGE_ALLGATHER) GS_TRY(cc_settle(h));   // (allgather settles after its export)
     if (in.reset_gen != c->reset_gen) {              // the handle was reset: a new stream
         c->reset_gen = in.reset_gen;

@@ -26,7 +26,7 @@ GS_ERR_COMM = -8
 GS_CC_TRACK_MARKS = 1
 GS_CC_SPARSE_IDS = 2
 
-GS_K_FOLD, GS_K_COMPRESS, GS_K_MERGE, GS_K_EXPORT, GS_K_RING, GS_K_UNION = 0, 1, 2, 3, 4, 6
+GS_K_FOLD, GS_K_COMPRESS, GS_K_MERGE, GS_K_EXPORT, GS_K_RING = 0, 1, 2, 3, 4
 GS_MERGE_ALLGATHER, GS_MERGE_GATHER, GS_MERGE_TREE = 0, 1, 2
 GS_TIMING_MASK = 0x100
 

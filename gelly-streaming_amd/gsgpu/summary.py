@@ -439,12 +439,10 @@ class DisjointSet:
         return int(u.value)
 
     def fold_time(self) -> Tuple[float, int]:
-        """(ms, launches) of every UpdateCC launch: k_fold (young / plain) + the steady k_fold_ring
-        (or, in gs_cc_fold_windows, the run-ahead filter k_filter) + k_union."""
+        """(ms, launches) of every UpdateCC launch: k_fold (young / plain) + the steady k_fold_ring."""
         a, na = self.kernel_time(_abi.GS_K_FOLD)
         b, nb = self.kernel_time(_abi.GS_K_RING)
-        c, nc = self.kernel_time(_abi.GS_K_UNION)
-        return a + b + c, na + nb + nc
+        return a + b, na + nb
 
 
 def combine_cc(s1: DisjointSet, s2: DisjointSet) -> DisjointSet:

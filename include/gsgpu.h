@@ -215,11 +215,9 @@ int gs_cc_fold_windows(gs_cc_t* h, gs_comm_t* comm, int mode, const void* src, c
 
 /* ---- instrumentation ----
  * kernel ids: 0 fold (young-forest / plain k_fold launches), 1 compress (close_window), 2 merge,
- * 3 export, 4 ring (the steady k_fold_ring launches, and gs_cc_fold_windows' run-ahead filter
- * k_filter), 5 reserved (a retired steady-fold variant; always 0), 6 union (k_union: the ordered
- * half of a split steady window); fold time = 0 + 4 + 6. */
-enum { GS_K_FOLD = 0, GS_K_COMPRESS = 1, GS_K_MERGE = 2, GS_K_EXPORT = 3, GS_K_RING = 4, GS_K_ROUTE = 5, GS_K_UNION = 6,
-       GS_K_COUNT = 7 };
+ * 3 export, 4 ring (the steady k_fold_ring launches), 5 reserved (a retired steady-fold variant;
+ * always 0); fold time = 0 + 4. */
+enum { GS_K_FOLD = 0, GS_K_COMPRESS = 1, GS_K_MERGE = 2, GS_K_EXPORT = 3, GS_K_RING = 4, GS_K_ROUTE = 5, GS_K_COUNT = 6 };
 /* enable = 0: off; 1: every kernel; GS_TIMING_MASK | (1 << GS_K_x) | ...: only those kernels
  * carry timing events (a timed launch costs ~3 us more dispatch time). Totals reset. */
 enum { GS_TIMING_MASK = 0x100 };

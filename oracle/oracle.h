@@ -107,6 +107,12 @@ int gso_cc_run_counts(const int64_t* init_v, const int64_t* init_l, uint64_t n_i
                       uint64_t* out_checksums, uint64_t* out_counts, int64_t* out_labels, int64_t* final_labels,
                       gso_run_stats* stats);
 
+/* ---------------- BipartitenessCheck (bipartite.c; the semantics the reference's tests pin) ----
+ * The dataflow of gso_cc_run over a parity union-find: *ok = the stream is bipartite; the final
+ * summary's vertex and component counts. */
+int gso_bip_run(const int64_t* src, const int64_t* dst, uint64_t n, uint64_t window_edges, int partitions,
+                int threads, int* ok, uint64_t* n_vertices, uint64_t* n_components, double* seconds);
+
 /* ---------------- incremental canonical emission (emission.c) ---------------- */
 typedef struct gso_track gso_track;
 gso_track* gso_track_new(uint64_t cap);            /* dense ids in [0, cap)                    */

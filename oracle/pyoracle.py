@@ -240,7 +240,20 @@ class COracle:
         L.gso_splitmix64.argtypes = [u64]; L.gso_splitmix64.restype = u64
         L.gso_pair_mix.argtypes = [u64, u64]; L.gso_pair_mix.restype = u64
         L.gso_parse_edges.argtypes = [ctypes.c_char_p, u64, vp, vp, u64]; L.gso_parse_edges.restype = i64
+        L.gso_bip_run.argtypes = [vp, vp, u64, u64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                  ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_double)]
+        L.gso_bip_run.restype = ctypes.c_int
         self.L = L
+
+    # ---- BipartitenessCheck (bipartite.c) ----
+    def bip_run(self, src, dst, window_edges: int, partitions: int = 1, threads: int = 1):
+        """(bipartite, vertices, components, seconds) of the stream through the dataflow."""
+        src = np.ascontiguousarray(src, dtype=np.int64)
+        dst = np.ascontiguousarray(dst, dtype=np.int64)
+        ok, nv, nc, secs = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_double()
+        self.L.gso_bip_run(_p(src), _p(dst), int(src.size), int(window_edges), int(partitions), int(threads),
+                           ctypes.byref(ok), ctypes.byref(nv), ctypes.byref(nc), ctypes.byref(secs))
+        return bool(ok.value), int(nv.value), int(nc.value), float(secs.value)
 
     # ---- edge-file input (parse.c) ----
     def parse_edges(self, text: bytes):

@@ -38,7 +38,7 @@ def fold_sequence(passdir):
     for f in files:
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"].split("(")[0].replace("void ", "")
-            if "k_fold" not in k and "k_filter" not in k and "k_union" not in k:
+            if "k_fold" not in k:
                 continue
             d = int(r.get("Dispatch_Id") or r.get("Correlation_Id"))
             per[d][r["Counter_Name"]] += float(r["Counter_Value"])
@@ -132,14 +132,10 @@ def main():
     except Exception:
         pass
     out["lib_source_sha"] = lib_source_sha()
-    # the steady fold per launch (what bench.py's roofline.traffic / requests report): k_fold_ring,
-    # or the split steady window of gs_cc_fold_windows, k_filter + k_union (per filter launch: the
-    # counters of both kernels summed, launches = filter launches)
+    # the steady fold per launch (what bench.py's roofline.traffic / requests report): k_fold_ring
     ks, name = [k for k in agg if "k_fold_ring" in k], "k_fold_ring"
-    if any("k_filter" in k for k in agg):
-        ks, name = [k for k in agg if "k_filter" in k or "k_union" in k], "k_filter+k_union"
     if ks:
-        nl = max(sum(ncalls.get(k) or 0 for k in ks if "k_union" not in k), 1)
+        nl = max(sum(ncalls.get(k) or 0 for k in ks), 1)
         f_ = sum(agg[k].get("FETCH_SIZE", 0.0) for k in ks) * 1024 / nl
         w_ = sum(agg[k].get("WRITE_SIZE", 0.0) for k in ks) * 1024 / nl
         h_ = sum(agg[k].get("TCC_HIT_sum", 0.0) for k in ks)

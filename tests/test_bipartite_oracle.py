@@ -100,3 +100,30 @@ def test_self_loops_only_add_vertices():
     assert [emission_string(*x) for x in intended_run(np.array([3, 1]), np.array([3, 2]), 0)] == \
         ["(true,{1={1=(1,true), 2=(2,false)}, 3={3=(3,true)}})"]
     assert bfs_bipartition([3, 1], [3, 2])[0]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_c_restatement_equals_intended_semantics(seed):
+    """oracle/bipartite.c (bench.py's BipartitenessCheck cpu_baseline) = intended_run on random
+    bipartite and odd-cycle streams, any partition count."""
+    from pyoracle import coracle
+    rng = np.random.default_rng(seed)
+    n, nv = 3000, 400
+    side = rng.integers(0, 2, nv)
+    a = rng.integers(0, nv, n)
+    b = rng.integers(0, nv, n)
+    keep = (side[a] != side[b]) | (a == b)
+    s, d = a[keep], b[keep]
+    if seed % 2 == 0:                                     # one odd edge somewhere
+        i = int(rng.integers(0, s.size))
+        same = np.nonzero(side == side[s[i]])[0]
+        d[i] = same[same != s[i]][0]
+    s = s * 1000003 - 7                                   # Long ids, negatives included
+    d = d * 1000003 - 7
+    W = 700
+    want = intended_run(s.tolist(), d.tolist(), W)[-1]
+    for P in (1, 3):
+        ok, nvert, ncomp, _ = coracle().bip_run(s, d, W, partitions=P, threads=P)
+        assert ok == want[0]
+        if ok:
+            assert nvert == len(want[1]) and ncomp == len(set(want[1].values()))

@@ -55,12 +55,19 @@ def test_rccl_world1(oracle, mode):
     comm.close()
 
 
-def _run_local(world, mode, s, d, cap, W):
-    """One thread per rank: fold slice r of every window, merge_window; returns per-rank checksums."""
+def _long_ids(x):
+    """A bijection of dense ids onto Java longs spread over the whole range (negatives, >= 2^32)."""
+    x = np.asarray(x, dtype=np.uint64)
+    return ((x * np.uint64(0x9E3779B97F4A7C15)) ^ np.uint64(0x5851F42D4C957F2D)).view(np.int64)
+
+
+def _run_local(world, mode, s, d, cap, W, sparse=False):
+    """One thread per rank: fold slice r of every window, merge_window; returns per-rank checksums.
+    sparse: s, d are arbitrary int64 ids folded into GS_CC_SPARSE_IDS summaries (finals None)."""
     import torch
     comms = Comm.local_group(world, 0)
-    ts = torch.from_numpy(s.astype(np.int32)).cuda()
-    td = torch.from_numpy(d.astype(np.int32)).cuda()
+    ts = torch.from_numpy(s.astype(np.int64 if sparse else np.int32)).cuda()
+    td = torch.from_numpy(d.astype(np.int64 if sparse else np.int32)).cuda()
     torch.cuda.synchronize()
     sums = [[] for _ in range(world)]
     finals = [None] * world
@@ -68,14 +75,14 @@ def _run_local(world, mode, s, d, cap, W):
 
     def rank(r):
         try:
-            ds = DisjointSet(cap, id_bits=32, track_marks=True)
+            ds = DisjointSet(cap, id_bits=64 if sparse else 32, track_marks=True, sparse=sparse)
             for lo in range(0, s.size, W):
                 ln = min(W, s.size - lo)
                 a, b = lo + (ln * r) // world, lo + (ln * (r + 1)) // world
                 ds.fold(ts[a:b], td[a:b])
                 ds.merge_window(comms[r], mode)
                 sums[r].append(ds.checksum()[0])
-            finals[r] = ds.dense().astype(np.int64)
+            finals[r] = None if sparse else ds.dense().astype(np.int64)
             ds.close()
         except Exception as e:          # surfaced by the main thread
             errors.append((r, repr(e)))
@@ -121,9 +128,10 @@ def test_local_group_young_windows_big_deltas(oracle):
         np.testing.assert_array_equal(finals[r], want["final"])
 
 
+@pytest.mark.parametrize("sparse", [False, True])
 @pytest.mark.parametrize("mode", ["allgather", "gather"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_local_group_speculative_slot_overflow(oracle, world, mode):
+def test_local_group_speculative_slot_overflow(oracle, world, mode, sparse):
     """The speculative slots (allgather: one per rank, all-gathered; gather: each sender's own,
     sent to rank 0) are sized from the last window's deltas: a tiny first window (one self-loop)
     then an Erdos-Renyi window whose deltas outgrow the 4K-pair slot — the tail round must carry the
@@ -134,20 +142,25 @@ def test_local_group_speculative_slot_overflow(oracle, world, mode):
     s1 = np.zeros(W, dtype=np.int64)                 # window 1: the self-loop (0, 0), W times
     s2, d2 = oracle.gen_er(0, 3 * W, cap, 4)        # windows 2-4: 3 x 2^17 uniform edges
     s = np.concatenate([s1, s2]); d = np.concatenate([s1, d2])
-    want = oracle.run(s, d, W, partitions=world, emit=EMIT_CHECKSUM, label_cap=cap, want_final=True)
-    sums, finals, info = _run_local(world, mode, s, d, cap, W)
+    if sparse:                                       # (id, root id) int64 pairs: the tail rounds' offsets in
+        s, d = _long_ids(s), _long_ids(d)            # 4-word pairs
+    want = oracle.run(s, d, W, partitions=world, emit=EMIT_CHECKSUM, label_cap=0 if sparse else cap,
+                      want_final=not sparse)
+    sums, finals, info = _run_local(world, mode, s, d, cap, W, sparse=sparse)
     for r in (range(world) if mode == "allgather" else [0]):
         assert sums[r] == [int(x) for x in want["checksums"]], "rank %d" % r
-        np.testing.assert_array_equal(finals[r], want["final"])
+        if not sparse:
+            np.testing.assert_array_equal(finals[r], want["final"])
     if mode == "allgather":
         assert all(i[5] >= 1 for i in info) and len({i[5] for i in info}) == 1, info
     else:
         assert info[0][5] >= 1 and all(i[5] >= 1 for i in info[1:]), info
 
 
+@pytest.mark.parametrize("sparse", [False, True])
 @pytest.mark.parametrize("mode", ["allgather", "gather"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_lazy_verification_overflow_in_a_batch(oracle, world, mode):
+def test_lazy_verification_overflow_in_a_batch(oracle, world, mode, sparse):
     """The speculative all-gather is verified lazily (comm.hip settle_allgather): with
     gs_cc_fold_windows nothing consumes an emission between windows, so an outgrown slot's tail
     round runs only after the NEXT window's local fold. The final emission must still be exact and
@@ -158,7 +171,10 @@ def test_lazy_verification_overflow_in_a_batch(oracle, world, mode):
     s1 = np.zeros(W, dtype=np.int64)
     s2, d2 = oracle.gen_er(0, 3 * W, cap, 4)
     s = np.concatenate([s1, s2]); d = np.concatenate([s1, d2])
-    want = oracle.run(s, d, W, partitions=world, emit=EMIT_CHECKSUM, label_cap=cap, want_final=True)
+    if sparse:
+        s, d = _long_ids(s), _long_ids(d)
+    want = oracle.run(s, d, W, partitions=world, emit=EMIT_CHECKSUM, label_cap=0 if sparse else cap,
+                      want_final=not sparse)
     assert W % world == 0
     per = []
     for r in range(world):
@@ -169,11 +185,12 @@ def test_lazy_verification_overflow_in_a_batch(oracle, world, mode):
 
     def rank(r):
         try:
-            ts = torch.from_numpy(per[r][0].astype(np.int32)).cuda()
-            td = torch.from_numpy(per[r][1].astype(np.int32)).cuda()
-            ds = DisjointSet(cap, id_bits=32, track_marks=True)
+            dt = np.int64 if sparse else np.int32
+            ts = torch.from_numpy(per[r][0].astype(dt)).cuda()
+            td = torch.from_numpy(per[r][1].astype(dt)).cuda()
+            ds = DisjointSet(cap, id_bits=64 if sparse else 32, track_marks=True, sparse=sparse)
             assert ds.fold_windows(ts, td, W // world, comm=comms[r], mode=mode) == s.size // W
-            finals[r] = (ds.checksum()[0], ds.dense().astype(np.int64))
+            finals[r] = (ds.checksum()[0], None if sparse else ds.dense().astype(np.int64))
             ov[r] = comms[r].info()[5]
             ds.close()
         except Exception as e:
@@ -190,8 +207,36 @@ def test_lazy_verification_overflow_in_a_batch(oracle, world, mode):
     assert not errors, errors
     for r in (range(world) if mode == "allgather" else [0]):
         assert finals[r][0] == int(want["checksums"][-1]), "rank %d" % r
-        np.testing.assert_array_equal(finals[r][1], want["final"])
+        if not sparse:
+            np.testing.assert_array_equal(finals[r][1], want["final"])
     assert all(o >= 1 for o in ov) and (mode == "gather" or len(set(ov)) == 1), ov
+
+
+@pytest.mark.parametrize("mode", ["allgather", "gather", "tree"])
+def test_mismatched_capacities_fail_every_rank(mode):
+    """Every rank sizes its exchange buffers and speculative slots from its own summary: ranks whose
+    capacities differ are refused when the communicator is bound, on every rank alike (ADVICE r04:
+    the speculative gather's send and receive sizes would otherwise disagree)."""
+    comms = Comm.local_group(2, 0)
+    errors = [None, None]
+
+    def rank(r):
+        try:
+            ds = DisjointSet(1 << (12 + r), id_bits=32, track_marks=True)
+            ds.fold(np.array([1, 2]), np.array([2, 3]))
+            ds.merge_window(comms[r], mode)
+        except gsgpu.GsError as e:
+            errors[r] = e.code
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "a rank hung"
+    for c in comms:
+        c.close()
+    # (a rank that sees its peer's abort first reports the group failure, GS_ERR_COMM)
+    assert set(errors) <= {gsgpu._abi.GS_ERR_INVALID, gsgpu._abi.GS_ERR_COMM} and gsgpu._abi.GS_ERR_INVALID in errors, errors
 
 
 def test_merge_window_errors():

@@ -88,8 +88,6 @@ VARIANTS = {
     # no list-mode closes: every close after a logging fold is a bitmap or full one (the A/B knob
     # the round-4 list-close measurements ran against)
     "list_close_off": {"GSGPU_LIST_CLOSE": "0"},
-    # gs_cc_fold_windows without the run-ahead filter (k_fold_ring per steady window, as round 4)
-    "ring_run_ahead_off": {"GSGPU_RING_MIN_BITS": "20", "GSGPU_RUN_AHEAD": "0"},
 }
 
 

@@ -28,6 +28,7 @@ __global__ __launch_bounds__(256) void k(const uint32_t* __restrict__ ids, uint6
         if (MODE == 4) __hip_atomic_fetch_or(&mem[a], 1u << (v & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (MODE == 2) acc += atomicCAS(&mem[a], 0xFFFFFFFFu, v);
         if (MODE == 3) mem[a] = v;
+        if (MODE == 5) __hip_atomic_store(&mem[a], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (acc == 0x12345678u) out[0] = acc;
 }
@@ -73,7 +74,11 @@ int main() {
            1e3 * run<4, true>(ids, n, mem, m8, out, b8), 1e3 * run<4, false>(ids, n, mem, m8, out, b8));
     printf(" \"cas_uniform_256MiB_us\": %.1f, \"cas_rmat_256MiB_us\": %.1f,\n",
            1e3 * run<2, false>(ids, n, mem, m256, out, b256), 1e3 * run<2, true>(ids, n, mem, m256, out, b256));
-    printf(" \"store_uniform_256MiB_us\": %.1f, \"store_rmat_256MiB_us\": %.1f}\n",
+    printf(" \"store_uniform_256MiB_us\": %.1f, \"store_rmat_256MiB_us\": %.1f,\n",
            1e3 * run<3, false>(ids, n, mem, m256, out, b256), 1e3 * run<3, true>(ids, n, mem, m256, out, b256));
+    // a relaxed agent-scope atomic STORE (non-returning, coherent): the claim of a never-touched vertex
+    // when no union can race with it (round 5, k_filter CLAIM)
+    printf(" \"atomic_store_uniform_256MiB_us\": %.1f, \"atomic_store_rmat_256MiB_us\": %.1f}\n",
+           1e3 * run<5, false>(ids, n, mem, m256, out, b256), 1e3 * run<5, true>(ids, n, mem, m256, out, b256));
     return 0;
 }
