@@ -119,3 +119,43 @@ def test_handle_on_its_own_stream_reads_torch_inputs_in_order(oracle, torch_cuda
         ds.close_window()
         del junk
         assert ds.checksum()[0] == int(want["checksums"][w]), "window %d" % w
+
+
+@pytest.mark.parametrize("W", [4096, 1 << 15])
+def test_giant_root_changes_every_window(oracle, torch_cuda, W):
+    """The giant's root (its minimum id) drops in every window: a smaller id joins it each time, so
+    every close is a full pass over a giant whose gbits were built for its previous root — the
+    rename shortcut (cc_kernels.hpp k_compress s_ren: members labelled with the new root without a
+    walk), in both close kernels (list-mode windows and bitmap windows) — window by window vs the
+    oracle, with claimed first touches (cbits) and stragglers outside the giant in the mix."""
+    torch = torch_cuda
+    scale = 17
+    cap = 1 << scale
+    rng = np.random.default_rng(9)
+    hi0 = cap // 2
+    nwin = 40
+    src, dst = [], []
+    for w in range(nwin):
+        a = rng.integers(hi0, cap, W)
+        b = rng.integers(hi0, cap, W)
+        if w >= 2:                                   # a smaller id joins the giant: its root changes
+            a[:4] = hi0 - 1 - 64 * w
+            b[:4] = rng.integers(hi0, cap, 4)
+            a[4:8] = rng.integers(0, hi0 // 2, 4)    # and a few stragglers outside it
+            b[4:8] = rng.integers(0, hi0 // 2, 4)
+        p = rng.permutation(W)
+        src.append(a[p]); dst.append(b[p])
+    s = np.concatenate(src).astype(np.int64)
+    d = np.concatenate(dst).astype(np.int64)
+    want = oracle.run(s, d, W, partitions=2, threads=2, emit=EMIT_CHECKSUM, label_cap=cap, want_final=True)
+    ts = torch.from_numpy(s.astype(np.int32)).cuda()
+    td = torch.from_numpy(d.astype(np.int32)).cuda()
+    ds = DisjointSet(cap, id_bits=32, stream=torch.cuda.current_stream())
+    for w, lo in enumerate(range(0, s.size, W)):
+        ds.fold(ts[lo:lo + W], td[lo:lo + W])
+        ds.close_window()
+        assert ds.checksum()[0] == int(want["checksums"][w]), "window %d" % w
+    np.testing.assert_array_equal(ds.dense().astype(np.int64), want["final"])
+    ds.reset()                                       # the same through gs_cc_fold_windows
+    assert ds.fold_windows(ts, td, W) == nwin
+    assert ds.checksum()[0] == int(want["checksums"][-1])

@@ -105,6 +105,68 @@ __device__ __forceinline__ void grid_barrier2(const Bar2& b, unsigned nblocks, u
     __syncthreads();
 }
 
+// three-level cost split (round 5): the grid barrier above spends its time in the per-workgroup
+// agent-scope fences (an L2 write-back on release, an invalidate on acquire, each serialised per
+// XCD). Here only the LAST arrival of each XCD group fences at agent scope (after every workgroup
+// of its group has arrived with a workgroup-scope release: its stores are in the XCD's L2), the
+// top release bumps the generation, and each group's first leaver invalidates for its group while
+// the others only wait for that on a group word. kFence = false: no agent-scope fence at all (the
+// synchronisation alone; not a valid barrier for plain stores across XCDs, a lower bound).
+struct Bar3 {
+    unsigned* group;   // 8 arrival counters, 32 words apart
+    unsigned* ggen;    // 8 per-group release words, 32 words apart
+    unsigned* top;
+    unsigned* gen;
+    unsigned* err;
+};
+template <bool kFence>
+__device__ __forceinline__ void grid_barrier3(const Bar3& b, unsigned nblocks, unsigned& g) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned x = blockIdx.x & 7u;
+        const unsigned members = nblocks / 8 + ((nblocks & 7u) > x ? 1u : 0u);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        unsigned* gc = b.group + 32 * x;
+        const unsigned a = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        if (a == members - 1) {                          // this XCD's last arrival: one write-back for all
+            __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (kFence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            const unsigned groups = nblocks < 8 ? nblocks : 8u;
+            const unsigned t = __hip_atomic_fetch_add(b.top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t == groups - 1) {
+                __hip_atomic_store(b.top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(b.gen, g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                while (__hip_atomic_load(b.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+                    if (__hip_atomic_load(b.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) { atomicOr(b.err, 1u); break; }
+                }
+            }
+            if (kFence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // one invalidate per XCD
+            __hip_atomic_store(b.ggen + 32 * x, g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            while (__hip_atomic_load(b.ggen + 32 * x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+                if (__hip_atomic_load(b.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) { atomicOr(b.err, 1u); break; }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        g += 1;
+    }
+    __syncthreads();
+}
+template <bool kFence>
+__global__ void k_barriers3(Bar3 b, unsigned iters, unsigned* __restrict__ a, unsigned n, int store) {
+    unsigned g = 0;
+    if (threadIdx.x == 0) g = __hip_atomic_load(b.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    for (unsigned it = 0; it < iters; ++it) {
+        if (store && i < n) a[i] = a[i] + it;
+        grid_barrier3<kFence>(b, gridDim.x, g);
+    }
+}
+
 template <bool kSpin>
 __global__ void k_barriers2(Bar2 b, unsigned iters, unsigned* __restrict__ a, unsigned n, int store) {
     unsigned g = 0;
@@ -160,6 +222,10 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&ctl2, 4096));
     CK(hipMemset(ctl2, 0, 4096));
     Bar2 b2{ctl2, ctl2 + 8 * 32, ctl2 + 9 * 32, ctl + 64};
+    unsigned* ctl3 = nullptr;
+    CK(hipMalloc(&ctl3, 8192));
+    CK(hipMemset(ctl3, 0, 8192));
+    Bar3 b3{ctl3, ctl3 + 8 * 32, ctl3 + 16 * 32, ctl3 + 17 * 32, ctl + 64};
     const unsigned blocks_list[] = {32u, 64u, (unsigned)cus, 2u * cus, 4u * cus};
     for (unsigned threads : {256u, 1024u}) {
         for (unsigned blocks : blocks_list) {
@@ -209,6 +275,21 @@ int main(int argc, char** argv) {
                     CK(hipEventElapsedTime(&ms, e0, e1));
                     printf(", \"bar2%s%s_us_%ux%u\": %.3f", spin ? "_spin" : "", store ? "_store" : "", blocks, threads,
                            ms * 1e3 / iters);
+                    CK(hipMemcpy(&e, ctl + 64, 4, hipMemcpyDeviceToHost));
+                    if (e) { printf(", \"spin_cap_hit\": 1}\n"); return 2; }
+                }
+                for (int fence = 1; fence >= 0; --fence) {        // leaders-only fences / no fences
+                    void* args3[] = {&b3, (void*)&iters, &a, (void*)&n, &store};
+                    const void* k3 = fence ? (const void*)k_barriers3<true> : (const void*)k_barriers3<false>;
+                    CK(hipLaunchCooperativeKernel(k3, dim3(blocks), dim3(threads), args3, 0, s));
+                    CK(hipStreamSynchronize(s));
+                    CK(hipEventRecord(e0, s));
+                    CK(hipLaunchCooperativeKernel(k3, dim3(blocks), dim3(threads), args3, 0, s));
+                    CK(hipEventRecord(e1, s));
+                    CK(hipEventSynchronize(e1));
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    printf(", \"bar3%s%s_us_%ux%u\": %.3f", fence ? "_leaderfence" : "_nofence", store ? "_store" : "",
+                           blocks, threads, ms * 1e3 / iters);
                     CK(hipMemcpy(&e, ctl + 64, 4, hipMemcpyDeviceToHost));
                     if (e) { printf(", \"spin_cap_hit\": 1}\n"); return 2; }
                 }
