@@ -115,6 +115,7 @@ struct gs_cc {
     uint64_t pick_edges = 0;             // edges_since_reset at the last forced giant re-pick
     uint64_t reset_gen = 0;              // gs_cc_reset calls (a communicator's per-stream state follows it)
     unsigned long long* dstats = nullptr;    // GSGPU_FOLD_STATS=1: per-window fold counters
+    unsigned ring_clock_groups = 0;          // ... and the last k_fold_ring launch's clocks (its grid)
     uint2* hot = nullptr;                // LDS hot set master copy (kHotBuckets uint2), steady folds
     uint32_t hot_bits = 0;               // ids < 2^hot_bits
     uint32_t* hot_cand = nullptr;        // hot-set admission candidates (2^kHotCandBits ids)
@@ -291,12 +292,14 @@ constexpr int kSmallEpt = 1;
 
 // ---- debug variables (read once per process; none is needed in production) ----
 //   GSGPU_FOLD_STATS=1       per-window fold counters on stderr (STATS kernel variants; same results)
+//   GSGPU_RING_CLOCKS=1      per-workgroup phase clocks of the window's last k_fold_ring launch on stderr
 //   GSGPU_FOLD_MODE=plain|ring|auto   force the steady fold variant (parity tests of each variant)
 //   GSGPU_RING_MIN_BITS=B    ring fold + warm set from ids >= 2^B instead of 2^25 (tests at small sizes)
 //   GSGPU_YOUNG_SPLIT=S      young split after S edges instead of capacity/16 (0 = off; tests)
 enum FoldMode { kFoldPlain = 0, kFoldRing = 1, kFoldAuto = 2 };
 struct DebugEnv {
     bool fold_stats = false;
+    int ring_clocks = 0;                            // GSGPU_RING_CLOCKS=1: k_fold_ring phase clocks on stderr (2: per XCD)
     int fold_mode = kFoldAuto;
     uint32_t ring_min_bits = kRingMinBits;
     uint64_t young_split = ~0ull;                   // ~0: the production rule
@@ -308,6 +311,8 @@ struct DebugEnv {
     DebugEnv() {
         const char* e = getenv("GSGPU_FOLD_STATS");
         fold_stats = e && atoi(e) != 0;
+        e = getenv("GSGPU_RING_CLOCKS");
+        ring_clocks = e ? atoi(e) : 0;
         e = getenv("GSGPU_FOLD_MODE");
         if (e && !strcmp(e, "plain")) fold_mode = kFoldPlain;
         if (e && !strcmp(e, "ring")) fold_mode = kFoldRing;
@@ -457,6 +462,7 @@ static HotArgs ring_hot_args(gs_cc_t* h, bool* build_out) {
     hot.wkeys = build ? h->wkeys : nullptr;
     hot.wctl = h->wctl;
     hot.count_edges = build ? h->warm_sample : 0;
+    hot.clocks = dbg().ring_clocks ? 1u : 0u;
     *build_out = build;
     return hot;
 }
@@ -488,6 +494,7 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
         if (st) klaunch(k_fold_ring<IdT, false, true>, grid, dim3(kHotThreads), h->stream, start, stop, a, b, f, hot);
         else klaunch(k_fold_ring<IdT, false, false>, grid, dim3(kHotThreads), h->stream, start, stop, a, b, f, hot);
     }
+    if (hot.clocks) h->ring_clock_groups = std::min<unsigned>(grid.x, kRingPhaseGroups);
     if (build) launch_warm_build(h, t.stop(), h->stream);
 }
 
@@ -680,11 +687,50 @@ void report_fold_stats(gs_cc_t* h) {
     (void)hipMemsetAsync(h->dstats, 0, sizeof(c), h->stream);
 }
 
+void report_ring_clocks(gs_cc_t* h) {
+    const unsigned ng = h->ring_clock_groups;
+    h->ring_clock_groups = 0;
+    if (!ng) return;
+    // the last ring launch's phases, in wall_clock64 ticks (100 MHz) relative to the first entry:
+    // entry skew, hot-set fill, main loop, final flush (medians and maxima over workgroups)
+    std::vector<unsigned long long> ph(4ull * ng);
+    if (hipStreamSynchronize(h->stream) != hipSuccess ||
+        hipMemcpyFromSymbol(ph.data(), HIP_SYMBOL(g_ring_phase), ph.size() * 8, 0, hipMemcpyDeviceToHost) != hipSuccess) return;
+    unsigned long long t0 = ~0ull, tend = 0;
+    std::vector<double> d[4];
+    for (unsigned g = 0; g < ng; ++g) t0 = std::min(t0, ph[4 * g]);
+    for (unsigned g = 0; g < ng; ++g) {
+        const unsigned long long* p = &ph[4 * g];
+        tend = std::max(tend, p[3]);
+        d[0].push_back((p[0] - t0) * 0.01);
+        d[1].push_back((p[1] - p[0]) * 0.01);
+        d[2].push_back((p[2] - p[1]) * 0.01);
+        d[3].push_back((p[3] - p[2]) * 0.01);
+    }
+    for (auto& x : d) std::sort(x.begin(), x.end());
+    fprintf(stderr, "[gsgpu ring-clocks] groups=%u span=%.2fus entry(med/max)=%.2f/%.2f fill=%.2f/%.2f loop=%.2f/%.2f final=%.2f/%.2f\n",
+            ng, (tend - t0) * 0.01, d[0][ng / 2], d[0][ng - 1], d[1][ng / 2], d[1][ng - 1], d[2][ng / 2], d[2][ng - 1],
+            d[3][ng / 2], d[3][ng - 1]);
+    // per XCD (workgroups are dispatched round-robin over the 8 XCDs): mean / max end time
+    if (dbg().ring_clocks > 1) {
+        double sum[8] = {0}, mx[8] = {0};
+        unsigned cntx[8] = {0};
+        for (unsigned g = 0; g < ng; ++g) {
+            const double e = (ph[4 * g + 3] - t0) * 0.01;
+            sum[g & 7] += e; mx[g & 7] = std::max(mx[g & 7], e); ++cntx[g & 7];
+        }
+        fprintf(stderr, "[gsgpu ring-xcd]");
+        for (int x = 0; x < 8; ++x) fprintf(stderr, " %.1f/%.1f", cntx[x] ? sum[x] / cntx[x] : 0.0, mx[x]);
+        fprintf(stderr, "\n");
+    }
+}
+
 constexpr uint64_t kEarlyPicks = 4;
 constexpr uint64_t kPickMinEdges = 1ull << 22;
 
 int compress_impl(gs_cc_t* h) {
     report_fold_stats(h);
+    report_ring_clocks(h);
     if (h->compressed) return GS_OK;
     {
         KTimer t(h, GS_K_COMPRESS, h->cap);
@@ -1069,7 +1115,7 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
             }
         }
     }
-    if (hipMemsetAsync(h->derr, 0, 4, h->stream) != hipSuccess) return bail(fail(GS_ERR_HIP, "memset failed"));
+    if (hipMemsetAsync(h->derr, 0, kDerrBytes, h->stream) != hipSuccess) return bail(fail(GS_ERR_HIP, "memset failed"));
     int rc = gs_cc_reset(h);
     if (rc != GS_OK) return bail(rc);
     if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(fail(GS_ERR_HIP, "stream sync failed"));

@@ -444,6 +444,7 @@ struct HotArgs {
     uint32_t* wkeys = nullptr;                 // warm build: endpoint keys, 512 per wave step (count launches only)
     unsigned long long* wctl = nullptr;        // warm build: edges counted (written by count launches)
     uint64_t count_edges = 0;                  // count this launch's first edges (if !*warm_valid)
+    uint32_t clocks = 0;                       // GSGPU_RING_CLOCKS: record g_ring_phase (k_fold_ring)
 };
 
 // ---- warm set (L2-resident second tier) ----
@@ -1035,12 +1036,19 @@ struct Raw4<int64_t> {
     }
 };
 
+// GSGPU_RING_CLOCKS only: per-workgroup clocks (wall_clock64) of the last k_fold_ring launch — entry,
+// hot set in LDS, every wave's main loop done, final flush done (report_fold_stats prints them)
+constexpr uint32_t kRingPhaseGroups = 4096;
+__device__ unsigned long long g_ring_phase[kRingPhaseGroups][4];
+
 template <typename IdT, bool MARK, bool STATS>
 __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict__ a, const IdT* __restrict__ b,
                                                            FoldArgs f, HotArgs hot) {
     __shared__ __attribute__((aligned(16))) uint2 tab[kHotBuckets];
     __shared__ uint2 rings[kHotThreads / 64][kRingCap];
     const uint64_t n = f.n;
+    const bool clocks = hot.clocks && threadIdx.x == 0 && blockIdx.x < kRingPhaseGroups;
+    if (clocks) g_ring_phase[blockIdx.x][0] = wall_clock64();
     const bool filt = *f.giant != kInvalid;          // uniform
     if (!filt) f.sbits = nullptr;                    // the next close is a full pass (k_fold)
     else f.hbits = nullptr;
@@ -1056,6 +1064,7 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
     const bool warm_ok = filt && hot.warm && *hot.warm_valid != 0;                        // uniform
     const uint64_t count_edges = (filt && hot.wkeys && hot.warm_valid && *hot.warm_valid == 0) ? hot.count_edges : 0;
     __syncthreads();
+    if (clocks) g_ring_phase[blockIdx.x][1] = wall_clock64();
     if (blockIdx.x == 0 && threadIdx.x == 0 && hot.budget && budget) *hot.budget = budget - 1;
     if (blockIdx.x == 0 && threadIdx.x == 0 && hot.wkeys)            // key slots written below
         *hot.wctl = (min(count_edges, n / 4 * 4) + 255) / 256 * 256;
@@ -1066,7 +1075,8 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
     const uint64_t groups = n / 4;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint64_t nvalid = 0, nkept = 0;
-    for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < groups; g0 += stride) {
+    // one wave round: 64 groups of 4 edges from g0 — filter, then ring or union in place
+    auto wave_round = [&](const uint64_t g0) {
         const uint64_t g = g0 + lane;
         uint32_t u[4] = {0, 0, 0, 0}, v[4] = {0, 0, 0, 0};
         bool ok[4] = {false, false, false, false};
@@ -1103,10 +1113,10 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
             if (lane >= off) incl += y;
         }
         const uint32_t wtot = __shfl(incl, 63, 64);
-        if (wtot == 0) continue;                     // uniform
+        if (wtot == 0) return;                       // uniform
         if (wtot > kRingCap / 2) {                   // young window: union in place
             union_group_g<MARK, STATS, 4>(f, u, v, ok, gf, gR, st);
-            continue;
+            return;
         }
         if (cnt + wtot > kRingCap) ring_flush<MARK, STATS>(f, ring, cnt, kRingCap - wtot, st, gR);
         uint32_t pos = cnt + incl - c;
@@ -1118,10 +1128,20 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
         }
         cnt += wtot;
         if (cnt >= 64) ring_flush<MARK, STATS>(f, ring, cnt, cnt - 64, st, gR);
-    }
+    };
+    for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < groups; g0 += stride)
+        wave_round(g0);
     __shared__ uint32_t s_mcnt;
     __shared__ unsigned long long s_mbase;
+    if (hot.clocks) {                                // uniform
+        __syncthreads();
+        if (clocks) g_ring_phase[blockIdx.x][2] = wall_clock64();
+    }
     ring_flush_final<MARK, STATS>(f, ring, cnt, st, gR, &s_mcnt, &s_mbase);
+    if (hot.clocks) {
+        __syncthreads();
+        if (clocks) g_ring_phase[blockIdx.x][3] = wall_clock64();
+    }
     if (STATS) {
         atomicAdd(&f.stats[0], nvalid);
         atomicAdd(&f.stats[1], nvalid - nkept);
