@@ -50,7 +50,7 @@ for scheme in schemes:
     ag = scheme == "allgather"       # replicated summaries: every rank folds every other rank's delta
     ranks = [gsgpu.DisjointSet(V, id_bits=32, track_marks=(ag or r != 0), stream=torch.cuda.current_stream()) for r in range(P)]
     if ag:
-        dbufs = [torch.empty(2 * V, dtype=torch.int32, device="cuda") for _ in range(P)]
+        dbufs = [torch.empty(4 * V, dtype=torch.int32, device="cuda") for _ in range(P)]   # 2V pairs: the export contract
         rbuf = [torch.empty(2, dtype=torch.int32, device="cuda")]
     scheds = [tree_schedule(r, P) for r in range(P)]
     print("== %s P=%d scale=%d W/rank=2^%d" % (scheme, P, scale, W.bit_length() - 1), flush=True)
