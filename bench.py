@@ -95,10 +95,15 @@ def parse():
     ap.add_argument("--host-loop", action="store_true",
                     help="drive the windows from Python (fold + close / merge per window) instead of one "
                          "gs_cc_fold_windows call per step (an A/B of the host loop)")
-    ap.add_argument("--merge", default="allgather", choices=["allgather", "gather", "tree"],
+    ap.add_argument("--merge", default="allgather", choices=["allgather", "gather", "tree", "prefilter"],
                     help="multi-rank CombineCC: allgather = replicated global summary (every rank folds every "
                          "delta); gather = windowAll gather to rank 0 (SummaryBulkAggregation.java:81); tree = "
-                         "log2(P) pairwise rounds (SummaryTreeReduce.java:95-123)")
+                         "log2(P) pairwise rounds (SummaryTreeReduce.java:95-123); prefilter = ranks 1..P-1 "
+                         "filter their slices against rank 0's broadcast giant bitmap and send the survivors, "
+                         "rank 0 (the Merger) folds and emits (C ABI / RCCL only)")
+    ap.add_argument("--share0", type=float, default=None,
+                    help="prefilter, strong layout: rank 0's share of every global window (default 1/(2P)); "
+                         "the other ranks split the rest evenly")
     ap.add_argument("--no-fold-timing", action="store_true",
                     help="no HIP events on the timed region's fold launches (value only; the roofline "
                          "figures are then omitted)")
@@ -115,20 +120,30 @@ def parse():
 
 
 def layout(a, world: int, rank: int):
-    """(edges this rank folds, its slice per window, global window, windows, global stream edges)."""
+    """(edges this rank folds, its slice per window, global window, windows, global stream edges,
+    the slice's offset inside a global window)."""
     E = a.edge_factor << a.scale
     if a.scaling == "strong":
         W_glob = min(1 << a.window_log2, E)
-        if W_glob % world:
-            raise SystemExit("global window %d does not split over %d ranks" % (W_glob, world))
-        W_rank = W_glob // world
         nwin = (E + W_glob - 1) // W_glob
         if E % W_glob:
             raise SystemExit("stream of %d edges is not a whole number of %d-edge windows" % (E, W_glob))
-        return nwin * W_rank, W_rank, W_glob, nwin, E
+        if a.merge == "prefilter" and world > 1:
+            # the Merger (rank 0) takes share0 of each window, the filtering ranks the rest; slices
+            # are multiples of 4 edges (16-B aligned SoA groups)
+            share0 = a.share0 if a.share0 is not None else 1.0 / (2 * world)
+            W1 = int(W_glob * (1 - share0) / (world - 1)) // 4 * 4
+            W0 = W_glob - (world - 1) * W1
+            W_rank = W0 if rank == 0 else W1
+            off = 0 if rank == 0 else W0 + (rank - 1) * W1
+            return nwin * W_rank, W_rank, W_glob, nwin, E, off
+        if W_glob % world:
+            raise SystemExit("global window %d does not split over %d ranks" % (W_glob, world))
+        W_rank = W_glob // world
+        return nwin * W_rank, W_rank, W_glob, nwin, E, rank * W_rank
     W_rank = min(1 << a.window_log2, E)
     nwin = (E + W_rank - 1) // W_rank
-    return E, W_rank, W_rank * world, nwin, E * world
+    return E, W_rank, W_rank * world, nwin, E * world, rank * W_rank
 
 
 def main():
@@ -159,14 +174,16 @@ def main():
         print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (a.gpus, world), file=sys.stderr)
 
     V = (1 << a.scale) if a.kind == "rmat" else (1 << a.scale)
-    E_rank, W_rank, W_glob, nwin, E_glob = layout(a, world, rank)
+    E_rank, W_rank, W_glob, nwin, E_glob, off_rank = layout(a, world, rank)
+    if a.merge == "prefilter" and world > 1 and a.dist_backend != "nccl":
+        raise SystemExit("--merge prefilter runs over the C ABI (RCCL) only")
     idt = torch.int32 if a.id_bits == 32 else torch.int64
 
     # ---- inputs resident in HBM (or pinned host memory) before timing ----
     src = torch.empty(E_rank, dtype=idt, device=dev)
     dst = torch.empty(E_rank, dtype=idt, device=dev)
     for w in range(nwin):
-        lo, first = w * W_rank, w * W_glob + rank * W_rank
+        lo, first = w * W_rank, w * W_glob + off_rank
         if a.kind == "er":
             gen.erdos_renyi(src[lo:lo + W_rank], dst[lo:lo + W_rank], first, V, a.seed)
         else:
@@ -179,7 +196,8 @@ def main():
         fsrc, fdst = src, dst
 
     stream = torch.cuda.current_stream()
-    marks = (world > 1 and (a.merge == "allgather" or a.dist_backend == "nccl" or rank != 0)) or a.exchange_world1
+    marks = ((world > 1 and (a.merge == "allgather" or a.dist_backend == "nccl" or rank != 0)) or a.exchange_world1) \
+        and a.merge != "prefilter"                   # the pre-filter exports no deltas
     ds = gsgpu.DisjointSet(V, id_bits=a.id_bits, device=local, track_marks=marks, stream=stream)
     comm = tree = None
     if world > 1 and a.dist_backend == "nccl":
@@ -207,8 +225,13 @@ def main():
         lo = w * W_rank
         if gather:
             tree.before_fold()
-        ds.fold(fsrc[lo:lo + W_rank], fdst[lo:lo + W_rank])
-        if comm is not None:
+        if comm is not None and a.merge == "prefilter":    # (the exchange takes the window's edges)
+            ds.fold_windows(fsrc[lo:lo + W_rank], fdst[lo:lo + W_rank], W_rank, comm=comm, mode="prefilter")
+        else:
+            ds.fold(fsrc[lo:lo + W_rank], fdst[lo:lo + W_rank])
+        if comm is not None and a.merge == "prefilter":
+            pass
+        elif comm is not None:
             ds.merge_window(comm, a.merge)
         elif tree is not None:
             tree.merge_window()
@@ -323,7 +346,7 @@ def main():
         # every term (32 B) and is reported beside it as frac_survey_int64
         per_edge = eb + 8
         per_edge_survey = eb + 8 if a.id_bits == 32 else 2 * 16
-        total_edges = a.steps * E_rank * world
+        total_edges = a.steps * E_glob
         folds = nwin                                  # the timed launches: the last step's
         fold_win_ms = (young_ms + ring_ms) / max(folds, 1) or float("nan")
         # the dominant kernel: the steady fold k_fold_ring, bytes per launch from the edges each timed
@@ -337,7 +360,7 @@ def main():
         alg_launch = per_edge * e_l
         achieved = alg_launch / (avg_ms * 1e-3) / 1e9
         prof, prof_note = steady_profile(a, kernel, e_l)
-        step_b = per_edge * E_rank * world                                  # SURVEY 8(d) edge term per step
+        step_b = per_edge * E_glob                                  # SURVEY 8(d) edge term per step
         step_gbs = step_b * a.steps / elapsed / 1e9
         nv, nc = ds.stats()
         fx_path, fx_last = fixture_last(a, world)

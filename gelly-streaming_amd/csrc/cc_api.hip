@@ -128,6 +128,10 @@ struct gs_cc {
     uint32_t warm_bcap = 0;              // keys per hash bucket
     int cus = 0;                         // compute units: k_fold_ring grid
     void* ingest = nullptr;              // streaming text ingestion state (parse.hip), freed by ingest_free
+    uint2* fscratch = nullptr;           // partition pre-filter: per-workgroup survivor regions
+    size_t fscratch_bytes = 0;
+    void* fstage = nullptr;              // ... and the device copy of host edge batches
+    size_t fstage_bytes = 0;
     void (*ingest_free)(void*) = nullptr;
     // GS_CC_SPARSE_IDS: id -> slot table; cap (above) = slots = 2^hbits + 1
     bool sparse = false;
@@ -957,6 +961,86 @@ int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int ns
 }
 void cc_count_folded(gs_cc_t* h, uint64_t n) { h->edges_since_reset += n; }
 
+// Partition pre-filter (comm.hip GS_MERGE_PREFILTER senders, gs_cc_filter_edges): the survivors of
+// the SoA edges (a[i], b[i]), i < n, against this handle's giant filter, appended as (u, v) uint32
+// pairs to out (cap pairs) behind the u64 count word *dcount, which is zeroed first. Launches of at
+// most kFilterChunk edges, each workgroup's survivors staged in its region of h->fscratch.
+constexpr uint64_t kFilterChunk = 1ull << 22;
+int cc_filter_async(gs_cc_t* h, const void* a, const void* b, uint64_t n, void* out, uint64_t cap,
+                    unsigned long long* dcount) {
+    GS_TRY(check(h));
+    if (h->sparse) return fail(GS_ERR_UNSUPPORTED, "partition pre-filter: dense ids only");
+    if (n > cap) return fail(GS_ERR_CAPACITY, "partition pre-filter: %llu edges, room for %llu survivors",
+                             (unsigned long long)n, (unsigned long long)cap);
+    DeviceGuard g(h->device);
+    GS_HIP(hipMemsetAsync(dcount, 0, sizeof(unsigned long long), h->stream));
+    if (n == 0) return GS_OK;
+    const unsigned grid = grid_for((std::min(n, kFilterChunk) + 3) / 4, kHotThreads, (unsigned)std::max(h->cus, 1));
+    const uint64_t stride = (uint64_t)grid * kHotThreads;                       // groups per round
+    const uint64_t region = ((kFilterChunk / 4 + stride - 1) / stride) * (uint64_t)kHotThreads * 4;   // edges per workgroup
+    const size_t need = (size_t)grid * region * sizeof(uint2);
+    if (h->fscratch_bytes < need) {
+        if (h->fscratch) {
+            GS_HIP(hipStreamSynchronize(h->stream));
+            GS_HIP(hipFree(h->fscratch));
+            h->fscratch = nullptr;
+            h->fscratch_bytes = 0;
+        }
+        if (hipMalloc(&h->fscratch, need) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(GS_ERR_NOMEM, "partition pre-filter scratch of %zu bytes", need);
+        }
+        h->fscratch_bytes = need;
+    }
+    const size_t esz = h->cfg.id_bits / 8;
+    const bool hot_on = h->hot && use_ring(h);
+    uint2* o = static_cast<uint2*>(out);
+    if (!is_device_pointer(a) || !is_device_pointer(b)) {
+        // host edges: staged through a device copy of the batch (the pre-filter reads device memory)
+        const size_t bytes = (size_t)n * esz;
+        if (h->fstage_bytes < 2 * bytes) {
+            if (h->fstage) {
+                GS_HIP(hipStreamSynchronize(h->stream));
+                GS_HIP(hipFree(h->fstage));
+                h->fstage = nullptr;
+                h->fstage_bytes = 0;
+            }
+            if (hipMalloc(&h->fstage, 2 * bytes) != hipSuccess) {
+                (void)hipGetLastError();
+                return fail(GS_ERR_NOMEM, "partition pre-filter staging of %zu bytes", 2 * bytes);
+            }
+            h->fstage_bytes = 2 * bytes;
+        }
+        char* da = static_cast<char*>(h->fstage);
+        GS_HIP(hipMemcpyAsync(da, a, bytes, hipMemcpyHostToDevice, h->stream));
+        GS_HIP(hipMemcpyAsync(da + bytes, b, bytes, hipMemcpyHostToDevice, h->stream));
+        a = da;
+        b = da + bytes;
+    }
+    for (uint64_t off = 0; off < n; off += kFilterChunk) {
+        const uint64_t m = std::min(kFilterChunk, n - off);
+        const char* pa = static_cast<const char*>(a) + off * esz;
+        const char* pb = static_cast<const char*>(b) + off * esz;
+        const int aligned = ((reinterpret_cast<uintptr_t>(pa) | reinterpret_cast<uintptr_t>(pb)) & 15) == 0;
+        FoldArgs f{m, h->parent, nullptr, nullptr, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, nullptr};
+        bool build = false;
+        HotArgs hot{};
+        if (hot_on) hot = ring_hot_args(h, &build);
+        const dim3 gd(grid_for((m + 3) / 4, kHotThreads, (unsigned)std::max(h->cus, 1)));
+        KTimer t(h, GS_K_RING, m);
+        hipEvent_t stop = build ? nullptr : t.stop();
+#define GS_LAUNCH_FILTER(IDT, HOTV)                                                                                \
+    klaunch(k_filter_out<IDT, HOTV>, gd, dim3(kHotThreads), h->stream, t.start(), stop, (const IDT*)pa, (const IDT*)pb, \
+            f, hot, h->fscratch, region, o, dcount, aligned)
+        if (h->cfg.id_bits == 32) { if (hot_on) GS_LAUNCH_FILTER(uint32_t, true); else GS_LAUNCH_FILTER(uint32_t, false); }
+        else { if (hot_on) GS_LAUNCH_FILTER(int64_t, true); else GS_LAUNCH_FILTER(int64_t, false); }
+#undef GS_LAUNCH_FILTER
+        GS_HIP(hipGetLastError());
+        if (build) launch_warm_build(h, t.stop(), h->stream);
+    }
+    return GS_OK;
+}
+
 int cc_fold_pairs_any(gs_cc_t* h, const void* pairs, uint64_t n) {
     GS_TRY(check(h));
     GS_TRY(cc_settle(h));
@@ -964,6 +1048,24 @@ int cc_fold_pairs_any(gs_cc_t* h, const void* pairs, uint64_t n) {
     const int rc = fold_impl(h, pairs, nullptr, n, true, h->sparse ? 64 : 32);
     h->fold_timer = GS_K_FOLD;
     return rc;
+}
+
+int cc_filter_state(gs_cc_t* h, uint32_t** gbits, uint64_t* gbits_bytes, uint32_t** giant_words) {
+    GS_TRY(check(h));
+    if (h->sparse || !h->gbits) return fail(GS_ERR_UNSUPPORTED, "giant filter state: dense ids only");
+    *gbits = h->gbits;
+    *gbits_bytes = (((uint64_t)h->cap + 31) >> 5) * 4;
+    *giant_words = giant_state(h);
+    return GS_OK;
+}
+
+int cc_install_giant(gs_cc_t* h, const uint32_t* words) {
+    GS_TRY(check(h));
+    DeviceGuard g(h->device);
+    hipLaunchKernelGGL(k_install_giant, dim3(1), dim3(1024), 0, h->stream, words, giant_state(h), h->derr + 5,
+                       (h->hot && use_ring(h)) ? h->hot : nullptr);
+    GS_HIP(hipGetLastError());
+    return GS_OK;
 }
 
 void* cc_ingest_get(gs_cc_t* h) { return h->ingest; }
@@ -1146,6 +1248,8 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->dbits) (void)hipFree(h->dbits);
     if (h->elab) (void)hipFree(h->elab);
     if (h->dstats) (void)hipFree(h->dstats);
+    if (h->fscratch) (void)hipFree(h->fscratch);
+    if (h->fstage) (void)hipFree(h->fstage);
     if (h->hot) (void)hipFree(h->hot);
     if (h->hot_cand) (void)hipFree(h->hot_cand);
     if (h->warm) (void)hipFree(h->warm);
@@ -1347,10 +1451,14 @@ static int fold_windows_loop(gs_cc_t* h, gs_comm_t* comm, int mode, const char* 
     const size_t esz = h->cfg.id_bits / 8;
     const int dev = (n && is_device_pointer(a) && is_device_pointer(b)) ? 1 : 0;
     uint64_t w = 0;
+    // GS_MERGE_PREFILTER: only the Merger (rank 0) folds; the exchange takes the window's edges
+    const bool pre = comm && mode == GS_MERGE_PREFILTER;
+    const bool fold_here = !pre || cc_comm_rank(comm) == 0;
     for (uint64_t off = 0; off < n; off += window_edges, ++w) {
         const uint64_t m = std::min(window_edges, n - off);
-        GS_TRY(fold_impl(h, a + off * esz, b + off * esz, m, false, h->cfg.id_bits, dev));   // (no settle: above)
-        GS_TRY(comm ? gs_cc_merge_window(h, comm, mode) : gs_cc_close_window(h));
+        if (fold_here) GS_TRY(fold_impl(h, a + off * esz, b + off * esz, m, false, h->cfg.id_bits, dev));   // (no settle: above)
+        if (pre) GS_TRY(cc_merge_edges(h, comm, mode, a + off * esz, b + off * esz, m));
+        else GS_TRY(comm ? gs_cc_merge_window(h, comm, mode) : gs_cc_close_window(h));
         if (windows_out) *windows_out = w + 1;
     }
     return GS_OK;
@@ -1365,7 +1473,10 @@ int gs_cc_fold_windows(gs_cc_t* h, gs_comm_t* comm, int mode, const void* src, c
     const char* a = static_cast<const char*>(src);
     const char* b = static_cast<const char*>(dst);
     GS_TRY(fold_windows_loop(h, comm, mode, a, b, n, window_edges, windows_out));
-    return cc_settle(h);                             // the last window's exchange verified
+    GS_TRY(cc_settle(h));                            // the last window's exchange verified
+    // a pre-filtering sender folds nothing: its filters' range-error flag is reported here
+    if (comm && mode == GS_MERGE_PREFILTER && cc_comm_rank(comm) != 0) return sync_and_check(h);
+    return GS_OK;
 }
 
 int gs_cc_stats(gs_cc_t* h, uint64_t* nv, uint64_t* nc) {
@@ -1773,6 +1884,23 @@ int gs_cc_export_marks_async(gs_cc_t* h, void* pairs, uint64_t cap, void* dev_co
                                          (unsigned long long)cap, h->cap);
     DeviceGuard g(h->device);
     return export_launch(h, pairs, cap, static_cast<unsigned long long*>(dev_count));
+}
+
+int gs_cc_filter_edges(gs_cc_t* h, const void* src, const void* dst, uint64_t n, void* pairs, uint64_t cap,
+                       uint64_t* n_out) {
+    GS_TRY(check(h));
+    GS_TRY(cc_settle(h));
+    if (!n_out || (n && (!src || !dst || !pairs))) return fail(GS_ERR_INVALID, "gs_cc_filter_edges: null argument");
+    if (n && !is_device_pointer(pairs)) return fail(GS_ERR_INVALID, "gs_cc_filter_edges: pairs must be device memory");
+    *n_out = 0;
+    DeviceGuard g(h->device);
+    unsigned long long* dcount = reinterpret_cast<unsigned long long*>(h->dscratch);
+    GS_TRY(cc_filter_async(h, src, dst, n, pairs, cap, dcount));
+    uint64_t* hc = reinterpret_cast<uint64_t*>(h->hscratch + 5);
+    GS_HIP(hipMemcpyAsync(hc, dcount, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
+    GS_TRY(sync_and_check(h));
+    *n_out = *hc;
+    return GS_OK;
 }
 
 int gs_cc_set_marking(gs_cc_t* h, int on) {

@@ -23,6 +23,18 @@ void cc_count_folded(gs_cc_t* h, uint64_t n);
 // folds n exported partial-summary pairs (device buffer) as CombineCC does: uint32 (vertex, root)
 // pairs for dense handles, int64 (id, root id) pairs for sparse-id handles; timed as a merge
 int cc_fold_pairs_any(gs_cc_t* h, const void* pairs, uint64_t n);
+// partition pre-filter (GS_MERGE_PREFILTER senders): survivors of n SoA edges against the handle's
+// giant filter as (u, v) uint32 pairs behind the u64 count word *dcount (zeroed first)
+int cc_filter_async(gs_cc_t* h, const void* a, const void* b, uint64_t n, void* out, uint64_t cap,
+                    unsigned long long* dcount);
+// the giant filter state a Merger broadcasts: gbits (words, bytes) and the 2-word giant slot the
+// next fold reads; cc_install_giant puts broadcast slot words (device) in place on a sending rank
+int cc_filter_state(gs_cc_t* h, uint32_t** gbits, uint64_t* gbits_bytes, uint32_t** giant_words);
+int cc_install_giant(gs_cc_t* h, const uint32_t* words);
+// the exchange of one window whose own edges the exchange needs (comm.hip: GS_MERGE_PREFILTER);
+// the rank of a communicator
+int cc_merge_edges(gs_cc_t* h, gs_comm_t* c, int mode, const void* a, const void* b, uint64_t m);
+int cc_comm_rank(const gs_comm_t* c);
 // a pending exchange verification of the handle's last window (comm.hip): cc_settle runs it once
 void cc_set_settle(gs_cc_t* h, int (*fn)(void*), void* ctx);
 int cc_settle(gs_cc_t* h);

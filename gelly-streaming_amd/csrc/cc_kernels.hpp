@@ -1152,6 +1152,130 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
     }
 }
 
+// ---- partition pre-filter (GS_MERGE_PREFILTER senders, comm.hip) ----
+// SummaryBulkAggregation.java:76-83 folds every partition's slice with UpdateCC and ships the
+// partial to the parallelism-1 Merger. Here a sending rank keeps no forest: it runs only the giant
+// FILTER of the fold over its slice — against the giant bitmap and root the Merger (rank 0)
+// broadcasts, plus this rank's own LDS hot set / L2 warm set admitted against that bitmap — and
+// the survivors go to the Merger as plain (u, v) edges. A stale bitmap is safe: components only
+// merge until reset, so two endpoints flagged in the broadcast giant stay in one component.
+// Each workgroup collects its survivors in its region of a scratch buffer, then reserves its range
+// of the count-headed output with ONE atomic and copies them there (order is free: union is
+// commutative). Range errors set f.rc.err, like a fold. HOT: the hot / warm sets exist (ring-sized
+// ids); otherwise gbits only.
+template <typename IdT, bool HOT>
+__global__ __launch_bounds__(kHotThreads) void k_filter_out(const IdT* __restrict__ a, const IdT* __restrict__ b,
+                                                            FoldArgs f, HotArgs hot, uint2* __restrict__ regions,
+                                                            uint64_t region, uint2* __restrict__ out,
+                                                            unsigned long long* __restrict__ count, int aligned) {
+    __shared__ __attribute__((aligned(16))) uint2 tab[HOT ? kHotBuckets : 1];
+    __shared__ uint32_t s_pos;
+    __shared__ unsigned long long s_base;
+    const uint64_t n = f.n;
+    const bool filt = *f.giant != kInvalid;          // uniform: a bitmap has been broadcast
+    if (HOT && filt) lds_fill<2 * kHotBuckets>(reinterpret_cast<uint32_t*>(tab), reinterpret_cast<const uint32_t*>(hot.table), 2 * kHotBuckets);
+    const uint32_t budget = (HOT && hot.budget) ? *hot.budget : 0u;
+    const uint64_t sample_edges = (HOT && (hot.periodic || budget)) ? hot.sample_edges : 0;
+    const bool warm_ok = HOT && filt && hot.warm && *hot.warm_valid != 0;
+    const uint64_t count_edges = (HOT && filt && hot.wkeys && hot.warm_valid && *hot.warm_valid == 0) ? hot.count_edges : 0;
+    if (threadIdx.x == 0) s_pos = 0;
+    __syncthreads();
+    if (HOT && blockIdx.x == 0 && threadIdx.x == 0 && hot.budget && budget) *hot.budget = budget - 1;
+    if (HOT && blockIdx.x == 0 && threadIdx.x == 0 && hot.wkeys)
+        *hot.wctl = (min(count_edges, n / 4 * 4) + 255) / 256 * 256;
+    const int lane = threadIdx.x & 63;
+    uint2* const reg = regions + (uint64_t)blockIdx.x * region;
+    const uint64_t groups = (n + 3) / 4;             // a partial last group: its lanes past n are not ok
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const bool vec = (n & 3) == 0;
+    // aligned: both streams 16-B aligned, so whole groups load as Raw4 (otherwise element loads)
+    for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < groups; g0 += stride) {
+        const uint64_t g = g0 + lane;
+        uint32_t u[4] = {0, 0, 0, 0}, v[4] = {0, 0, 0, 0};
+        bool ok[4] = {false, false, false, false};
+        uint32_t gf[4];
+        if (g < groups) {
+            bool oka[4] = {true, true, true, true}, okb[4] = {true, true, true, true};
+            if (aligned && (vec || g + 1 < groups)) {
+                Raw4<IdT> ra, rb;
+                ra.load(a, g);
+                rb.load(b, g);
+                ra.unpack(u, oka, f.rc.cap);
+                rb.unpack(v, okb, f.rc.cap);
+            } else {                                 // unaligned, or the ragged last group
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint64_t e = 4 * g + k;
+                    const bool in = e < n;
+                    const uint64_t x = in ? (uint64_t)a[e] : 0, y = in ? (uint64_t)b[e] : 0;
+                    oka[k] = x < (uint64_t)f.rc.cap || !in;
+                    okb[k] = y < (uint64_t)f.rc.cap || !in;
+                    u[k] = (uint32_t)x;
+                    v[k] = (uint32_t)y;
+                }
+            }
+            bool bad = false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool in = 4 * g + k < n;
+                ok[k] = in && oka[k] && okb[k];
+                bad |= in && !(oka[k] && okb[k]);
+                if (!ok[k]) { u[k] = 0; v[k] = 0; }
+            }
+            if (bad) atomicOr(f.rc.err, 1u);
+        }
+        if (filt) filter_group<false, 4, HOT>(f, u, v, ok, tab, hot, g * 4 < sample_edges, warm_ok,
+                                              g0 * 4 < count_edges ? g0 / 64 : ~0ull, gf);
+        const uint32_t c = (uint32_t)ok[0] + ok[1] + ok[2] + ok[3];
+        uint32_t incl = c;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        const uint32_t wtot = __shfl(incl, 63, 64);
+        if (wtot == 0) continue;                     // uniform
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&s_pos, wtot);   // LDS: the wave's place in the region
+        uint32_t pos = __shfl(base, 0, 64) + incl - c;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (!ok[k]) continue;
+            reg[pos] = make_uint2(u[k], v[k]);
+            ++pos;
+        }
+    }
+    __syncthreads();
+    const uint32_t total = s_pos;
+    if (threadIdx.x == 0) s_base = total ? atomicAdd(count, (unsigned long long)total) : 0ull;
+    __syncthreads();
+    const unsigned long long at = s_base;
+    for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) out[at + i] = reg[i];
+}
+
+// A sending rank's filter state after the Merger's broadcast (its gbits already in place): the
+// giant words go to the slot its filters read; the hot set (and warm set) are dropped when the
+// giant's root differs from the one they were admitted for — another component, or a renamed root
+// of the same one, which a rank without a forest cannot tell apart. owner = derr + 5 (owner, hot
+// admission budget, warm set valid), as k_compress keeps them.
+__global__ __launch_bounds__(1024) void k_install_giant(const uint32_t* __restrict__ in, uint32_t* __restrict__ slot,
+                                                        uint32_t* __restrict__ owner, uint2* __restrict__ hot) {
+    const uint32_t g = in[0];
+    const bool clear = g != owner[0];                // uniform
+    __syncthreads();                                 // every thread has read owner[0]
+    if (clear && hot)
+        for (uint32_t i = threadIdx.x; i < kHotBuckets; i += blockDim.x) hot[i] = make_uint2(0u, 0u);
+    if (threadIdx.x == 0) {
+        slot[0] = in[0];
+        slot[1] = in[1];
+        if (clear) {
+            owner[0] = g;
+            owner[1] = kHotAdmitLaunches;
+            owner[2] = 0;
+        }
+    }
+}
+
 // Warm build without global counters (the count launch's per-endpoint atomicAdd into 2^B 16-bit
 // counters cost ~390 us and four band scans of them ~400 us per RMAT-26 build): the count launch
 // writes its LDS-miss giant endpoints into key slots (512 per wave step, kInvalid where none);

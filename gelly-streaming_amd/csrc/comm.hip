@@ -126,6 +126,8 @@ struct gs_comm {
     uint32_t* pend_buf = nullptr;                  // its export (the tail pairs [S, n) are sent from it)
     uint64_t last_delta = 0;                       // the largest delta of the last verified window
     std::vector<uint64_t> gslot;                   // gather: every sender's speculative slot (empty: exact round next)
+    uint64_t win = 0;                              // prefilter: windows since the stream's start (broadcast schedule)
+    uint32_t* bword = nullptr;                     // prefilter: the broadcast giant slot words (device, 2)
     uint64_t bytes_sent = 0, bytes_recv = 0, exchanges = 0, overflows = 0;
 };
 
@@ -212,6 +214,29 @@ int recv(gs_comm_t* c, void* p, size_t bytes, int peer, hipStream_t s) {
     return GS_OK;
 }
 
+// rank 0's buffer into every rank's buffer of the same address role, in place
+int bcast(gs_comm_t* c, void* buf, size_t bytes, hipStream_t s) {
+    if (c->nccl) {
+        GS_NCCL(ncclBroadcast(buf, buf, bytes, ncclUint8, 0, c->nccl, s));
+        return GS_OK;
+    }
+    LocalGroup& g = *c->local;
+    GS_HIP(hipEventRecord(c->ev_ready, s));
+    g.send[c->rank] = buf;
+    g.ev[c->rank] = c->ev_ready;
+    if (!g.barrier()) return fail(GS_ERR_COMM, "in-process group: a peer's exchange failed");
+    if (c->rank != 0) {
+        GS_HIP(hipStreamWaitEvent(s, g.ev[0], 0));
+        GS_HIP(hipMemcpyAsync(buf, g.send[0], bytes, hipMemcpyDeviceToDevice, s));
+    }
+    GS_HIP(hipEventRecord(c->ev_done, s));
+    g.done[c->rank] = c->ev_done;
+    if (!g.barrier()) return fail(GS_ERR_COMM, "in-process group: a peer's exchange failed");
+    if (c->rank == 0)                              // rank 0's buffer changes only after the copies
+        for (int q = 1; q < c->world; ++q) GS_HIP(hipStreamWaitEvent(s, g.done[q], 0));
+    return GS_OK;
+}
+
 struct Group {                                     // ncclGroupStart/End around p2p batches
     gs_comm_t* c;
     explicit Group(gs_comm_t* c_) : c(c_) { if (c->nccl) (void)ncclGroupStart(); }
@@ -239,9 +264,12 @@ int ensure(void** p, size_t* have, size_t need, hipStream_t s) {
     return GS_OK;
 }
 
-int prepare(gs_comm_t* c, gs_cc_t* h, CcInfo* info) {
+int prepare(gs_comm_t* c, gs_cc_t* h, CcInfo* info, int mode) {
     GS_TRY(cc_info(h, info));
-    if (!info->marks) return fail(GS_ERR_UNSUPPORTED, "gs_cc_merge_window: handle created without GS_CC_TRACK_MARKS");
+    if (mode == GS_MERGE_PREFILTER && info->sparse)
+        return fail(GS_ERR_UNSUPPORTED, "GS_MERGE_PREFILTER: dense ids only");
+    if (!info->marks && mode != GS_MERGE_PREFILTER)     // (the pre-filter exports no deltas)
+        return fail(GS_ERR_UNSUPPORTED, "gs_cc_merge_window: handle created without GS_CC_TRACK_MARKS");
     if (info->device != c->device) return fail(GS_ERR_INVALID, "gs_cc_merge_window: handle on device %d, communicator on %d",
                                                info->device, c->device);
     const uint64_t need = 2ull * info->cap;        // an export never exceeds 2 x capacity pairs
@@ -400,7 +428,8 @@ int abort_exchange(gs_comm_t* c, int rc);
 int settle_gather(gs_comm_t* c, bool close);
 int settle_cb(void* ctx) {
     gs_comm_t* c = static_cast<gs_comm_t*>(ctx);
-    const int rc = c->mode == GS_MERGE_GATHER ? settle_gather(c, true) : settle_allgather(c, true);
+    const int rc = (c->mode == GS_MERGE_GATHER || c->mode == GS_MERGE_PREFILTER) ? settle_gather(c, true)
+                                                                                 : settle_allgather(c, true);
     return rc == GS_OK ? rc : abort_exchange(c, rc);
 }
 
@@ -624,6 +653,152 @@ int merge_gather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
     return GS_OK;
 }
 
+// ---- GS_MERGE_PREFILTER: the partitions filter, the Merger unions ----
+// SummaryBulkAggregation.java:76-83: every partition folds its slice of a window (UpdateCC) and the
+// window's partials go to the parallelism-1 Merger, which combines them and emits. Here ranks
+// 1..P-1 keep no forest: a rank runs only the giant FILTER of the fold over its slice, against the
+// giant bitmap and root rank 0 broadcasts (a stale bitmap is safe: components only merge until
+// reset), with its own LDS hot / L2 warm sets, and sends the survivors — plain (u, v) edges — to
+// rank 0 in the gather's count-headed slots. Rank 0 folds its own slice and every rank's survivors,
+// closes and emits. The filter (the fold's expensive, read-only part) runs on P - 1 GPUs in
+// parallel; the unions, the close and the emission stay on the Merger, whose per-window work is the
+// survivors (~3.5 % of a steady RMAT-26 window) instead of every rank's full delta fold.
+// The first kExactYoung windows of a stream are exact rounds (counts to the host first): their
+// survivors are large (a padded speculative slot would move twice their bytes), and rank 0 folds
+// them in one call through the young fold. Then speculative slots sized from each sender's last
+// count, verified lazily (settle_gather), as the gather. After rank 0's close of each of the first
+// kBcastYoung windows, then of every kBcastEvery-th, the bitmap and the giant words are broadcast
+// (8 MiB at 2^26 ids; a staler bitmap only lets more edges survive).
+constexpr uint64_t kExactYoung = 16;
+constexpr uint64_t kBcastYoung = 4;                // the giant forms in the first windows
+constexpr uint64_t kBcastEvery = 8;
+bool bcast_due(uint64_t win) { return win < kBcastYoung || win % kBcastEvery == kBcastEvery - 1; }
+
+int bcast_filter_state(gs_comm_t* c, gs_cc_t* h, hipStream_t s) {
+    uint32_t *gb = nullptr, *words = nullptr;
+    uint64_t gbytes = 0;
+    GS_TRY(cc_filter_state(h, &gb, &gbytes, &words));
+    if (!c->bword) {
+        if (hipMalloc(&c->bword, 2 * sizeof(uint32_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(GS_ERR_NOMEM, "broadcast words");
+        }
+    }
+    if (c->rank == 0) GS_HIP(hipMemcpyAsync(c->bword, words, 2 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    {
+        Group g(c);
+        GS_TRY(bcast(c, gb, gbytes, s));
+        GS_TRY(bcast(c, c->bword, 2 * sizeof(uint32_t), s));
+        GS_TRY(g.end());
+    }
+    if (c->rank != 0) GS_TRY(cc_install_giant(h, c->bword));
+    if (c->rank == 0) c->bytes_sent += (gbytes + 8) * (c->world - 1);
+    else c->bytes_recv += gbytes + 8;
+    return GS_OK;
+}
+
+int merge_prefilter(gs_comm_t* c, gs_cc_t* h, const CcInfo& in, const void* a, const void* b, uint64_t m) {
+    const int P = c->world;
+    hipStream_t s = in.stream;
+    const uint64_t win = c->win++;
+    const bool exact = win < kExactYoung || c->gslot.empty() || P > kMaxSlotCaps;
+    if (c->gslot.empty()) c->gslot.assign(P, 0);
+    if (c->rank != 0) {
+        if (exact) {
+            GS_TRY(cc_filter_async(h, a, b, m, c->sendbuf + 2, c->cap_pairs - 1, reinterpret_cast<unsigned long long*>(c->sendbuf)));
+            GS_HIP(hipMemcpyAsync(c->hcnt + P, c->sendbuf, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+            GS_HIP(hipStreamSynchronize(s));
+            const uint64_t n = c->hcnt[P];
+            GS_TRY(send(c, c->sendbuf, sizeof(unsigned long long), 0, s));
+            if (n) GS_TRY(send(c, c->sendbuf + 2, n * 8, 0, s));
+            c->bytes_sent += n * 8 + 8;
+            c->gslot[c->rank] = next_slot(c, n);
+            c->last_delta = n;
+            c->pend_buf = c->sendbuf;
+        } else {
+            uint32_t* send_buf = (c->pend_buf == c->sendbuf) ? c->sendbuf2 : c->sendbuf;
+            const uint64_t S = c->gslot[c->rank];
+            GS_TRY(cc_filter_async(h, a, b, m, send_buf + 2, c->cap_pairs - 1, reinterpret_cast<unsigned long long*>(send_buf)));
+            GS_TRY(send(c, send_buf, (2 + 2 * S) * 4, 0, s));
+            GS_HIP(hipEventRecord(c->ev_slots, s));                 // the count word to the host, aside
+            GS_HIP(hipStreamWaitEvent(c->side, c->ev_slots, 0));
+            GS_HIP(hipMemcpyAsync(c->hcnt + P, send_buf, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->side));
+            GS_HIP(hipEventRecord(c->ev_counts, c->side));
+            c->bytes_sent += (2 + 2 * S) * 4;
+            c->pending = true;
+            c->pend_slot = S;
+            c->pend_buf = send_buf;
+            cc_set_settle(h, settle_cb, c);
+        }
+        if (bcast_due(win)) GS_TRY(bcast_filter_state(c, h, s));
+        return GS_OK;
+    }
+    if (!c->root_marking_off) {                    // the Merger never exports
+        GS_TRY(gs_cc_set_marking(h, 0));
+        c->root_marking_off = true;
+    }
+    if (exact) {
+        {
+            Group g(c);
+            for (int q = 1; q < P; ++q) GS_TRY(recv(c, c->dcnt + q, sizeof(unsigned long long), q, s));
+            GS_TRY(g.end());
+        }
+        GS_HIP(hipMemcpyAsync(c->hcnt, c->dcnt, P * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+        GS_HIP(hipStreamSynchronize(s));
+        std::vector<uint64_t> cnt(P, 0);
+        uint64_t total = 0, mx = 0;
+        for (int q = 1; q < P; ++q) {
+            cnt[q] = c->hcnt[q];
+            if (cnt[q] > c->cap_pairs - 1) return fail(GS_ERR_CAPACITY, "rank %d: %llu survivors past the exchange buffer", q,
+                                                       (unsigned long long)cnt[q]);
+            total += cnt[q];
+            mx = std::max(mx, cnt[q]);
+            c->gslot[q] = next_slot(c, cnt[q]);
+        }
+        if (total) {
+            GS_TRY(ensure(reinterpret_cast<void**>(&c->recvbuf), &c->recv_bytes, (size_t)total * 8, s));
+            {
+                Group g(c);
+                uint64_t off = 0;
+                for (int q = 1; q < P; ++q) {
+                    if (cnt[q]) GS_TRY(recv(c, c->recvbuf + 2 * off, cnt[q] * 8, q, s));
+                    off += cnt[q];
+                }
+                GS_TRY(g.end());
+            }
+            // every survivor in one fold call, through the young fold (its internal giant split
+            // included): one call per slice cost ~7 dependent launches per young window
+            GS_TRY(cc_fold_pairs_any(h, c->recvbuf, total));
+            c->bytes_recv += total * 8 + 8 * (P - 1);
+        }
+        c->last_delta = mx;
+        GS_TRY(gs_cc_close_window(h));
+    } else {
+        uint64_t smax = 0;
+        for (int q = 1; q < P; ++q) smax = std::max(smax, c->gslot[q]);
+        const uint64_t slot_words = 2 + 2 * smax;
+        GS_TRY(ensure(reinterpret_cast<void**>(&c->slotbuf), &c->slot_bytes, (size_t)P * slot_words * 4, s));
+        {
+            Group g(c);
+            for (int q = 1; q < P; ++q)
+                GS_TRY(recv(c, c->slotbuf + (uint64_t)q * slot_words, (2 + 2 * c->gslot[q]) * 4, q, s));
+            GS_TRY(g.end());
+        }
+        GS_HIP(hipEventRecord(c->ev_slots, s));
+        GS_HIP(hipStreamWaitEvent(c->side, c->ev_slots, 0));
+        GS_HIP(hipMemcpy2DAsync(c->hcnt, sizeof(unsigned long long), c->slotbuf, slot_words * 4, sizeof(unsigned long long), P,
+                                hipMemcpyDeviceToHost, c->side));
+        GS_HIP(hipEventRecord(c->ev_counts, c->side));
+        GS_TRY(cc_fold_slots(h, c->slotbuf, slot_words, P, 0, smax, c->gslot.data()));
+        GS_TRY(gs_cc_close_window(h));                          // optimistic: no sender outgrew its slot
+        for (int q = 1; q < P; ++q) c->bytes_recv += (2 + 2 * c->gslot[q]) * 4;
+        c->pending = true;
+        cc_set_settle(h, settle_cb, c);
+    }
+    if (bcast_due(win)) GS_TRY(bcast_filter_state(c, h, s));
+    return GS_OK;
+}
+
 // ConnectedComponentsTree's pairwise rounds (SummaryTreeReduce.enhance): in round r (step 2^r)
 // rank i + step sends its delta to rank i (i % 2^(r+1) == 0), which folds it with marking on (it
 // forwards what it gained in a later round). After ceil(log2 P) rounds rank 0 holds every edge.
@@ -754,6 +929,7 @@ int gs_comm_destroy(gs_comm_t* c) {
     if (c->sendbuf2) (void)hipFree(c->sendbuf2);
     if (c->recvbuf) (void)hipFree(c->recvbuf);
     if (c->slotbuf) (void)hipFree(c->slotbuf);
+    if (c->bword) (void)hipFree(c->bword);
     if (c->dcnt) (void)hipFree(c->dcnt);
     if (c->hcnt) (void)hipHostFree(c->hcnt);
     delete c;
@@ -789,9 +965,9 @@ int abort_exchange(gs_comm_t* c, int rc) {
     return rc;
 }
 
-int merge_window(gs_cc_t* h, gs_comm_t* c, int mode) {
+int merge_window(gs_cc_t* h, gs_comm_t* c, int mode, const void* a = nullptr, const void* b = nullptr, uint64_t m = 0) {
     CcInfo in;
-    GS_TRY(prepare(c, h, &in));
+    GS_TRY(prepare(c, h, &in, mode));
     // a communicator carries per-stream state (the speculative slot size, rank 0's paused
     // marking): it serves one handle in one mode; a reset of that handle starts a new stream
     if (c->bound && (c->bound != h || c->mode != mode))
@@ -824,21 +1000,44 @@ int merge_window(gs_cc_t* h, gs_comm_t* c, int mode) {
         c->reset_gen = in.reset_gen;
         c->spec_slot = 0;                            // its first window runs the exact round again
         c->gslot.clear();
+        c->win = 0;
     }
     DeviceGuard g(in.device);
     switch (mode) {
     case GS_MERGE_ALLGATHER: return merge_allgather(c, h, in);
     case GS_MERGE_GATHER: return merge_gather(c, h, in);
+    case GS_MERGE_PREFILTER: return merge_prefilter(c, h, in, a, b, m);
     default: return merge_tree(c, h, in);
     }
 }
 }  // namespace
+
+extern "C++" {
+namespace gsgpu {
+int cc_comm_rank(const gs_comm_t* c) { return c ? c->rank : 0; }
+
+// gs_cc_fold_windows with GS_MERGE_PREFILTER: the window's own edges go to the exchange (rank 0
+// has folded them already; the other ranks filter them there)
+int cc_merge_edges(gs_cc_t* h, gs_comm_t* c, int mode, const void* a, const void* b, uint64_t m) {
+    if (!c) return fail(GS_ERR_INVALID, "null communicator");
+    if (c->broken) return fail(GS_ERR_COMM, "the communicator failed in an earlier exchange");
+    const int rc = merge_window(h, c, mode, a, b, m);
+    if (rc == GS_OK) {
+        ++c->exchanges;
+        return rc;
+    }
+    return abort_exchange(c, rc);
+}
+}  // namespace gsgpu
+}  // extern "C++"
 
 int gs_cc_merge_window(gs_cc_t* h, gs_comm_t* c, int mode) {
     if (!c) return fail(GS_ERR_INVALID, "gs_cc_merge_window: null communicator");
     if (c->broken) return fail(GS_ERR_COMM, "gs_cc_merge_window: the communicator failed in an earlier exchange");
     int rc;
     if (!h) rc = fail(GS_ERR_INVALID, "gs_cc_merge_window: null handle");
+    else if (mode == GS_MERGE_PREFILTER)
+        rc = fail(GS_ERR_INVALID, "gs_cc_merge_window: GS_MERGE_PREFILTER needs the window's edges (gs_cc_fold_windows)");
     else if (mode != GS_MERGE_ALLGATHER && mode != GS_MERGE_GATHER && mode != GS_MERGE_TREE)
         rc = fail(GS_ERR_INVALID, "gs_cc_merge_window: mode %d", mode);
     else rc = merge_window(h, c, mode);

@@ -27,7 +27,7 @@ GS_CC_TRACK_MARKS = 1
 GS_CC_SPARSE_IDS = 2
 
 GS_K_FOLD, GS_K_COMPRESS, GS_K_MERGE, GS_K_EXPORT, GS_K_RING = 0, 1, 2, 3, 4
-GS_MERGE_ALLGATHER, GS_MERGE_GATHER, GS_MERGE_TREE = 0, 1, 2
+GS_MERGE_ALLGATHER, GS_MERGE_GATHER, GS_MERGE_TREE, GS_MERGE_PREFILTER = 0, 1, 2, 3
 GS_TIMING_MASK = 0x100
 
 _ERRNAMES = {GS_ERR_INVALID: "INVALID", GS_ERR_HIP: "HIP", GS_ERR_RANGE: "RANGE",
@@ -41,7 +41,7 @@ EXPORTED_SYMBOLS = (
     "gs_cc_close_window", "gs_cc_stats", "gs_cc_emit_dense", "gs_cc_emit_pairs", "gs_cc_emit_delta",
     "gs_cc_emit_delta_async", "gs_cc_emit_wait",
     "gs_cc_checksum", "gs_cc_find", "gs_cc_find_flags", "gs_cc_labels_device", "gs_cc_export_marks",
-    "gs_cc_fold_pairs32", "gs_cc_export_marks_async", "gs_cc_set_marking", "gs_cc_timing", "gs_cc_kernel_time", "gs_cc_kernel_units", "gs_gen_rmat", "gs_gen_er", "gs_parse_edges",
+    "gs_cc_fold_pairs32", "gs_cc_export_marks_async", "gs_cc_filter_edges", "gs_cc_set_marking", "gs_cc_timing", "gs_cc_kernel_time", "gs_cc_kernel_units", "gs_gen_rmat", "gs_gen_er", "gs_parse_edges",
     "gs_cc_fold_text", "gs_cc_fold_file",
     "gs_bip_create", "gs_bip_destroy", "gs_bip_reset", "gs_bip_set_stream", "gs_bip_sync", "gs_bip_fold",
     "gs_bip_fold_pairs", "gs_bip_merge", "gs_bip_close_window", "gs_bip_status", "gs_bip_checksum",
@@ -121,6 +121,7 @@ def lib() -> ctypes.CDLL:
         "gs_cc_fold_pairs32": [vp, vp, u64],
         "gs_cc_set_marking": [vp, ctypes.c_int],
         "gs_cc_export_marks_async": [vp, vp, u64, vp],
+        "gs_cc_filter_edges": [vp, vp, vp, u64, vp, u64, P(u64)],
         "gs_cc_merge": [vp, vp],
         "gs_cc_combine": [vp, vp, P(vp)],
         "gs_cc_close_window": [vp],

@@ -13,9 +13,10 @@ import ctypes
 from typing import List, Tuple
 
 from . import _abi
-from ._abi import GS_MERGE_ALLGATHER, GS_MERGE_GATHER, GS_MERGE_TREE, call
+from ._abi import GS_MERGE_ALLGATHER, GS_MERGE_GATHER, GS_MERGE_PREFILTER, GS_MERGE_TREE, call
 
-MODES = {"allgather": GS_MERGE_ALLGATHER, "gather": GS_MERGE_GATHER, "tree": GS_MERGE_TREE}
+MODES = {"allgather": GS_MERGE_ALLGATHER, "gather": GS_MERGE_GATHER, "tree": GS_MERGE_TREE,
+         "prefilter": GS_MERGE_PREFILTER}   # prefilter: fold_windows only
 UNIQUE_ID_BYTES = 128
 
 

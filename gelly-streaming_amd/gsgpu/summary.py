@@ -418,6 +418,20 @@ class DisjointSet:
         call("gs_cc_export_marks_async", self.handle, p, total // 2, ctypes.c_void_p(count.data_ptr()))
         self._torch_after(keep, count)
 
+    def filter_edges(self, src, dst, out) -> int:
+        """The giant pre-filter alone (gs_cc_filter_edges): the edges of (src, dst) that survive this
+        summary's giant filter, as uint32 (u, v) pairs into the int32 device tensor ``out``
+        (>= 2 x len(src) elements); returns their number. Nothing is folded."""
+        ps, ks, n = _buf(src, self.id_bits, "src")
+        pd, kd, m = _buf(dst, self.id_bits, "dst")
+        if n != m:
+            raise ValueError("src and dst differ in length")
+        po, ko, total = _buf(out, 32, "out")
+        self._after_torch(ks, kd, ko)
+        cnt = ctypes.c_uint64()
+        call("gs_cc_filter_edges", self.handle, ps, pd, n, po, total // 2, ctypes.byref(cnt))
+        return int(cnt.value)
+
     def set_marking(self, on: bool) -> None:
         """Pause / resume marking (GS_CC_TRACK_MARKS): folds while paused are not exported."""
         call("gs_cc_set_marking", self.handle, 1 if on else 0)

@@ -164,6 +164,13 @@ int gs_cc_fold_pairs32(gs_cc_t* h, const void* pairs, uint64_t n);
  * device uint64 *dev_count (no host synchronisation; a collective can take it from there).
  * pairs and dev_count are device pointers; cap must be >= 2 x vertex_capacity (never overflows). */
 int gs_cc_export_marks_async(gs_cc_t* h, void* pairs, uint64_t cap, void* dev_count);
+/* The giant pre-filter alone (UpdateCC's read-only half; what a GS_MERGE_PREFILTER sender runs):
+ * the edges (src[i], dst[i]), i < n (id_bits wide, host or device), that survive this handle's
+ * giant filter — NOT both endpoints in the giant component it last picked — written as uint32
+ * (u, v) pairs to the device buffer pairs (cap >= n pairs); *n_out = their number (synchronous).
+ * Nothing is folded. Dense ids only. Out-of-range ids are skipped and reported (GS_ERR_RANGE). */
+int gs_cc_filter_edges(gs_cc_t* h, const void* src, const void* dst, uint64_t n, void* pairs, uint64_t cap,
+                       uint64_t* n_out);
 /* Pause (on = 0) / resume (on = 1) marking on a GS_CC_TRACK_MARKS handle: folds while paused leave
  * no marks (a replica folding the other ranks' partial summaries must not re-export them). */
 int gs_cc_set_marking(gs_cc_t* h, int on);
@@ -185,6 +192,11 @@ int gs_cc_set_marking(gs_cc_t* h, int on);
  *                         more exact round, decided alike on every rank)
  *     GS_MERGE_GATHER     windowAll: deltas to rank 0, which folds them and emits
  *     GS_MERGE_TREE       log2(P) pairwise rounds to rank 0 (SummaryTreeReduce.enhance)
+ *     GS_MERGE_PREFILTER  gs_cc_fold_windows only (the exchange needs the window's edges): ranks
+ *                         1..P-1 keep no forest — each filters its slice of a window against the
+ *                         giant bitmap rank 0 broadcasts and sends the surviving edges to rank 0,
+ *                         which folds its own slice and every survivor, closes and emits (dense
+ *                         ids; GS_CC_TRACK_MARKS not needed). Slices may differ in size per rank.
  *   Every rank must call it once per window with the same mode. In GATHER / TREE only rank 0's
  *   emission is the job's, and the call waits for the delta sizes. In ALLGATHER it does not wait:
  *   the sizes are checked lazily (an outgrown slot's tail round) by the next merge_window, or first
@@ -192,7 +204,7 @@ int gs_cc_set_marking(gs_cc_t* h, int on);
  *   labels_device, sync, fold*, merge, combine, reset, destroy) — gs_cc_fold_windows alone folds
  *   the next window without that wait (its merge exports before settling). */
 typedef struct gs_comm gs_comm_t;
-enum { GS_MERGE_ALLGATHER = 0, GS_MERGE_GATHER = 1, GS_MERGE_TREE = 2 };
+enum { GS_MERGE_ALLGATHER = 0, GS_MERGE_GATHER = 1, GS_MERGE_TREE = 2, GS_MERGE_PREFILTER = 3 };
 int gs_comm_unique_id(void* id, uint64_t id_bytes);
 int gs_comm_create(gs_comm_t** out, const void* unique_id, int rank, int world, int device);
 int gs_comm_create_local(gs_comm_t** comms, int world, int device);
@@ -209,7 +221,9 @@ int gs_cc_merge_window(gs_cc_t* h, gs_comm_t* comm, int mode);
  * window may be shorter) gs_cc_fold, then gs_cc_merge_window(h, comm, mode) when comm is not NULL,
  * else gs_cc_close_window — the per-window host loop run inside the library (one ABI call per batch
  * instead of two per window). After it returns, the labels are those of the last window's
- * emission; *windows_out (may be NULL) = windows folded. Stops at the first failure. */
+ * emission; *windows_out (may be NULL) = windows folded. Stops at the first failure. With
+ * GS_MERGE_PREFILTER only rank 0 folds (the others filter their slices for it); every rank must
+ * pass the same number of windows (n / window_edges rounded up), window_edges may differ. */
 int gs_cc_fold_windows(gs_cc_t* h, gs_comm_t* comm, int mode, const void* src, const void* dst, uint64_t n,
                        uint64_t window_edges, uint64_t* windows_out);
 

@@ -4,7 +4,10 @@ PartitionMapper split, SummaryBulkAggregation.java:76-80,93-106; bench.py --scal
 window exchanged and closed through the C ABI (gs_cc_merge_window) in the chosen mode:
   allgather  every rank keeps the global summary (replicated Merger): every rank is checked;
   gather     the windowAll gather to rank 0 (SummaryBulkAggregation.java:81-83): rank 0 is checked;
-  tree       ConnectedComponentsTree's pairwise rounds (SummaryTreeReduce.java:95-123): rank 0.
+  tree       ConnectedComponentsTree's pairwise rounds (SummaryTreeReduce.java:95-123): rank 0;
+  prefilter  ranks 1..P-1 filter their slices against rank 0's broadcast giant bitmap (with their own
+             hot / warm sets at these ids) and send the survivors; rank 0 takes 1/(2P) of each
+             window, folds everything and emits (gs_cc_fold_windows per window): rank 0.
 RCCL cannot put several ranks on one GPU, so the ranks are threads over the in-process transport
 (gs_comm_create_local): the same exchange code, collectives as device copies.
 
@@ -37,7 +40,7 @@ def main():
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--scale", type=int, default=26)
     ap.add_argument("--windows", type=int, default=64, help="global windows folded (a prefix of the fixture)")
-    ap.add_argument("--mode", default="allgather", choices=["allgather", "gather", "tree"])
+    ap.add_argument("--mode", default="allgather", choices=["allgather", "gather", "tree", "prefilter"])
     ap.add_argument("--no-torch", action="store_true")
     a = ap.parse_args()
     import torch
@@ -61,14 +64,25 @@ def main():
     finals = [None] * P
     errors = []
     Wr = W // P
+    pre = a.mode == "prefilter"
+    if pre:                                   # bench.py's prefilter layout: rank 0 1/(2P) of each window
+        W1 = int(W * (1 - 1.0 / (2 * P)) / (P - 1)) // 4 * 4
+        W0 = W - (P - 1) * W1
+        sl = [(0, W0)] + [(W0 + (q - 1) * W1, W1) for q in range(1, P)]
+    else:
+        sl = [(q * Wr, Wr) for q in range(P)]
 
     def rank(r):
         try:
-            ds = gsgpu.DisjointSet(V, id_bits=32, track_marks=True)
+            ds = gsgpu.DisjointSet(V, id_bits=32, track_marks=not pre)
+            off, ln = sl[r]
             for w in range(N):
-                lo = w * W + r * Wr
-                ds.fold(src[lo:lo + Wr], dst[lo:lo + Wr])
-                ds.merge_window(comms[r], a.mode)
+                lo = w * W + off
+                if pre:
+                    ds.fold_windows(src[lo:lo + ln], dst[lo:lo + ln], ln, comm=comms[r], mode="prefilter")
+                else:
+                    ds.fold(src[lo:lo + ln], dst[lo:lo + ln])
+                    ds.merge_window(comms[r], a.mode)
                 if r in checked:
                     sums[r].append(ds.checksum())
             if r in checked:

@@ -1,0 +1,160 @@
+"""GPU parity of GS_MERGE_PREFILTER (csrc/comm.hip merge_prefilter): ranks 1..P-1 filter their
+slices of every window against the giant bitmap rank 0 broadcasts and send the survivors; rank 0
+(the Merger, SummaryBulkAggregation.java:76-83 / SummaryAggregation.java:106-119) folds its own
+slice and every survivor, closes and emits. Rank 0's emission after every window is compared,
+bit-exact, with the C oracle's (canonical labels do not depend on the partitioning).
+
+* in-process groups of 2, 3 and 8 ranks (one thread per rank on this GPU) and RCCL at world 1;
+* uneven slices (rank 0's share of a window 1/16 .. 1/2), one call per window and one call per
+  stream, int32 and int64 ids;
+* speculative slots past the exact young rounds, and survivor bursts that outgrow them (tail rounds);
+* a sender's out-of-range id (GS_ERR_RANGE on that rank, the others unaffected), sparse handles and
+  gs_cc_merge_window with this mode (rejected).
+The hot / warm-set paths of the senders (a giant switching components between broadcasts) run in
+tests/variant_check.py under every fold variant (test_gpu_variants.py).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from gsgpu import Comm, DisjointSet, GsError, _abi
+from gsgpu.comm import unique_id
+from pyoracle import EMIT_CHECKSUM
+from variant_check import rank_slices, run_prefilter
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch
+
+
+def _rmat(oracle, scale, n, seed):
+    """n edges: RMAT, then the largest ids, a self-loop and a duplicate (every window of a multiple
+    of the window size is full, so no rank's slice is empty: each rank exchanges every window)."""
+    s, d = oracle.gen_rmat(0, n - 4, scale, seed)
+    cap = 1 << scale
+    s = np.concatenate([s, [cap - 1, cap - 2, 5, 5]])          # the largest ids, a self-loop, a duplicate
+    d = np.concatenate([d, [cap - 2, cap - 1, 5, 5]])
+    return s, d, cap
+
+
+@pytest.mark.parametrize("world,share0", [(2, 0.5), (3, 0.125), (8, 0.0625)])
+def test_prefilter_every_window_vs_oracle(oracle, torch_cuda, world, share0):
+    s, d, cap = _rmat(oracle, 15, 400000, 21)
+    r = run_prefilter(torch_cuda, oracle, "rmat15", s, d, 8000, cap, world=world, share0=share0)
+    assert r["ok"], r
+
+
+@pytest.mark.parametrize("id_bits", [32, 64])
+def test_prefilter_one_call_per_stream(oracle, torch_cuda, id_bits):
+    s, d, cap = _rmat(oracle, 16, 600000, 22)                   # 100 windows, the same slices each
+    r = run_prefilter(torch_cuda, oracle, "rmat16_one_call", s, d, 6000, cap, world=4, share0=0.25,
+                      per_window=False, id_bits=id_bits)
+    assert r["ok"], r
+
+
+def test_prefilter_survivor_bursts_outgrow_slots(oracle, torch_cuda):
+    """After the exact young rounds the slots follow each sender's last survivor count; windows of
+    fresh vertices (every edge survives) between RMAT windows outgrow them: tail rounds, still exact."""
+    rng = np.random.default_rng(4)
+    scale, W = 18, 20000                                         # sender slices 8000 > the 4096-pair floor
+    cap = 1 << scale
+    s0, d0 = oracle.gen_rmat(0, 40 * W, scale - 1, 23)          # ids < 2^17: the giant's half
+    src, dst = [s0[:30 * W]], [d0[:30 * W]]
+    fresh = np.arange(1 << 17, 1 << 18)
+    rng.shuffle(fresh)
+    for k in range(3):                                           # bursts of new vertices (pairs)
+        f = fresh[k * 2 * W:(k + 1) * 2 * W]
+        src += [f[0::2], s0[(30 + 2 * k) * W:(31 + 2 * k) * W]]
+        dst += [f[1::2], d0[(30 + 2 * k) * W:(31 + 2 * k) * W]]
+    s, d = np.concatenate(src).astype(np.int64), np.concatenate(dst).astype(np.int64)
+    r = run_prefilter(torch_cuda, oracle, "bursts", s, d, W, cap, world=3, share0=0.2)
+    assert r["ok"], r
+    assert sum(r["overflows"]) > 0, r                            # the bursts did outgrow their slots
+
+
+def test_prefilter_rccl_world1(oracle, torch_cuda):
+    """World 1 through RCCL: rank 0 alone (no senders), the emission of every window."""
+    torch = torch_cuda
+    s, d, cap = _rmat(oracle, 14, 200000, 24)
+    W = 9000                                                     # (a short last window: world 1)
+    want = oracle.run(s, d, W, partitions=1, emit=EMIT_CHECKSUM, label_cap=cap, want_final=True)
+    comm = Comm.create(unique_id(), 0, 1, 0)
+    ds = DisjointSet(cap, id_bits=32, stream=torch.cuda.current_stream())
+    ts = torch.from_numpy(s.astype(np.int32)).cuda()
+    td = torch.from_numpy(d.astype(np.int32)).cuda()
+    got = []
+    for lo in range(0, s.size, W):
+        assert ds.fold_windows(ts[lo:lo + W], td[lo:lo + W], W, comm=comm, mode="prefilter") == 1
+        got.append(ds.checksum()[0])
+    assert got == [int(x) for x in want["checksums"]]
+    np.testing.assert_array_equal(ds.dense().astype(np.int64), want["final"])
+    ds.close()
+    comm.close()
+
+
+def test_prefilter_sender_range_error(oracle, torch_cuda):
+    """An id >= capacity in a sender's slice: that rank's call fails with GS_ERR_RANGE after the
+    stream (its filters skip the edge, as a fold does); rank 0 folds the rest and stays exact."""
+    torch = torch_cuda
+    s, d, cap = _rmat(oracle, 14, 120000, 25)
+    W, world = 6000, 3
+    sl = rank_slices(s.size, W, world, 0.25)
+    lo, hi = sl[2][7]
+    bad_at = lo + 3
+    keep = np.ones(s.size, bool)
+    keep[bad_at] = False
+    s_bad = s.copy()
+    s_bad[bad_at] = cap + 5
+    comms = Comm.local_group(world, 0)
+    res, errs = [None] * world, [None] * world
+
+    def rank(r):
+        ds = DisjointSet(cap, id_bits=32)
+        ts = torch.from_numpy(s_bad.astype(np.int32)).cuda()
+        td = torch.from_numpy(d.astype(np.int32)).cuda()
+        for lo_, hi_ in sl[r]:
+            try:                                                 # (the exchange itself completed)
+                ds.fold_windows(ts[lo_:hi_], td[lo_:hi_], hi_ - lo_, comm=comms[r], mode="prefilter")
+            except GsError as e:
+                errs[r] = e.code
+        res[r] = ds.dense().astype(np.int64) if r == 0 else True
+        ds.close()
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th), "a rank hung"
+    for c in comms:
+        c.close()
+    assert errs[2] == _abi.GS_ERR_RANGE and errs[0] is None and errs[1] is None, errs
+    # rank 0's final labels = the oracle's over every edge but the bad one
+    fin = oracle.run(s[keep], d[keep], s.size, partitions=1, emit=EMIT_CHECKSUM, label_cap=cap, want_final=True)
+    np.testing.assert_array_equal(res[0], fin["final"])
+
+
+def test_prefilter_rejected_where_it_cannot_run(torch_cuda):
+    torch = torch_cuda
+    comm = Comm.create(unique_id(), 0, 1, 0)
+    ds = DisjointSet(1 << 12, id_bits=32, track_marks=True, stream=torch.cuda.current_stream())
+    ds.fold(torch.tensor([1, 2], dtype=torch.int32).cuda(), torch.tensor([2, 3], dtype=torch.int32).cuda())
+    with pytest.raises(GsError) as ei:
+        ds.merge_window(comm, "prefilter")                       # needs the window's edges
+    assert ei.value.code == _abi.GS_ERR_INVALID
+    ds.close()
+    comm.close()
+    comm = Comm.create(unique_id(), 0, 1, 0)
+    sp = DisjointSet(1 << 12, id_bits=64, sparse=True, stream=torch.cuda.current_stream())
+    t = torch.tensor([1, 2], dtype=torch.int64).cuda()
+    with pytest.raises(GsError) as ei:
+        sp.fold_windows(t, t, 2, comm=comm, mode="prefilter")
+    assert ei.value.code == _abi.GS_ERR_UNSUPPORTED
+    sp.close()
+    comm.close()

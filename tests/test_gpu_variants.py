@@ -64,7 +64,7 @@ def test_c5_config_production(args):
     assert r["ok"], r
 
 
-@pytest.mark.parametrize("mode", ["allgather", "gather", "tree"])
+@pytest.mark.parametrize("mode", ["allgather", "gather", "tree", "prefilter"])
 def test_headline_config_eight_ranks_one_gpu(mode):
     """BASELINE config 3's 8-rank strong layout at full scale through the C-ABI exchange
     (in-process transport): every window's emission vs the fixture, replicas equal, final vs torch CC."""

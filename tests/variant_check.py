@@ -103,6 +103,89 @@ def run_fold_windows(ds, ts, td, W, want):
     return None
 
 
+def rank_slices(n, W, world, share0=None):
+    """Rank r's part of every window of a stream of n edges in windows of W: [(lo, hi) per window]
+    per rank. share0 (GS_MERGE_PREFILTER's Merger): rank 0's fraction of each window, the rest split
+    evenly; None: even slices."""
+    out = [[] for _ in range(world)]
+    for lo in range(0, n, W):
+        ln = min(W, n - lo)
+        if share0 is None or world == 1:
+            cut = [lo + (ln * r) // world for r in range(world + 1)]
+        else:
+            c0 = max(1, int(ln * share0))
+            cut = [lo] + [lo + c0 + ((ln - c0) * r) // (world - 1) for r in range(world)]
+        for r in range(world):
+            out[r].append((cut[r], cut[r + 1]))
+    return out
+
+
+def run_prefilter(torch, oracle, name, s, d, W, cap, world=4, share0=0.125, per_window=True, id_bits=32, want=None):
+    """GS_MERGE_PREFILTER over an in-process group of `world` ranks on this GPU (rank 0 the Merger
+    with share0 of every window, the others filtering theirs): one gs_cc_fold_windows call per
+    window (rank 0's emission after each checked) or one call for the whole stream (per_window
+    False: rank r's slices laid out contiguously, every window the same size per rank, final
+    emission checked)."""
+    import threading
+    import gsgpu
+    from gsgpu import Comm
+    from pyoracle import EMIT_CHECKSUM
+    if want is None:
+        want = oracle.run(s, d, W, partitions=world, threads=8, emit=EMIT_CHECKSUM, label_cap=cap, want_final=True)
+    nwin = len(want["checksums"])
+    sl = rank_slices(s.size, W, world, share0)
+    dt = np.int32 if id_bits == 32 else np.int64
+    comms = Comm.local_group(world, 0)
+    got, finals, errors = [], [None], []
+
+    def rank(r):
+        try:
+            ds = gsgpu.DisjointSet(cap, id_bits=id_bits)
+            if per_window:
+                ts = torch.from_numpy(s.astype(dt)).cuda()
+                td = torch.from_numpy(d.astype(dt)).cuda()
+                for w, (lo, hi) in enumerate(sl[r]):
+                    assert ds.fold_windows(ts[lo:hi], td[lo:hi], max(hi - lo, 1), comm=comms[r], mode="prefilter") == 1
+                    if r == 0:
+                        got.append(ds.checksum()[0])
+            else:
+                idx = np.concatenate([np.arange(lo, hi) for lo, hi in sl[r]])
+                ts = torch.from_numpy(s[idx].astype(dt)).cuda()
+                td = torch.from_numpy(d[idx].astype(dt)).cuda()
+                Wr = sl[r][0][1] - sl[r][0][0]
+                assert ds.fold_windows(ts, td, Wr, comm=comms[r], mode="prefilter") == nwin
+                if r == 0:
+                    got.append(ds.checksum()[0])
+            if r == 0:
+                finals[0] = ds.dense().astype(np.int64)
+            ds.close()
+        except Exception as e:                             # noqa: BLE001
+            errors.append((r, repr(e)))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    hung = any(t.is_alive() for t in th)
+    info = [] if hung else [c.info() for c in comms]
+    if not hung:
+        for c in comms:
+            c.close()
+    ws = [int(x) for x in want["checksums"]]
+    bad = None
+    if per_window:
+        for w in range(min(len(got), nwin)):
+            if got[w] != ws[w]:
+                bad = w
+                break
+    ok = (not hung and not errors and bad is None and len(got) == (nwin if per_window else 1)
+          and (per_window or got[0] == ws[-1]) and finals[0] is not None
+          and bool(np.array_equal(finals[0], want["final"])))
+    return {"case": name, "windows": nwin, "world": world, "first_bad_window": bad, "errors": errors, "hung": hung,
+            "overflows": [i[5] for i in info], "ok": ok}
+
+
 def main():
     import torch
     import gsgpu
@@ -123,10 +206,13 @@ def main():
         res.append({"case": "golden/" + n, "ok": ok})
     s, d = oracle.gen_rmat(0, 1 << 24, 21, 5)
     res.append(run_case(torch, oracle, "rmat21", s, d, 1 << 20, 1 << 21))
+    res.append(run_prefilter(torch, oracle, "rmat21_prefilter_4ranks", s, d, 1 << 20, 1 << 21, world=4))
     s, d = oracle.gen_er(0, 1 << 22, 1 << 21, 6)
     res.append(run_case(torch, oracle, "er21", s, d, 1 << 19, 1 << 21))
+    res.append(run_prefilter(torch, oracle, "er21_prefilter_4ranks", s, d, 1 << 19, 1 << 21, world=4))
     s, d, W, cap = giant_switch_stream()
     res.append(run_case(torch, oracle, "giant_switch", s, d, W, cap))
+    res.append(run_prefilter(torch, oracle, "giant_switch_prefilter_3ranks", s, d, W, cap, world=3))
     env = {k: v for k, v in os.environ.items() if k.startswith("GSGPU_")}
     print(json.dumps({"env": env, "ok": all(r["ok"] for r in res), "cases": res}), flush=True)
 

@@ -4,7 +4,7 @@ step is timed with HIP events. Measures what a multi-GPU run cannot show from a 
 payload (pairs) each exchange moves per window and the merge folds on the receiving ranks; the
 xGMI transfer time is modelled as bytes / 150 GB/s per link.
 
-usage (GPU box): python tools/sim_ranks.py P windows [scheme ...]   schemes: gather tree allgather
+usage (GPU box): python tools/sim_ranks.py P windows [scheme ...]   schemes: gather tree allgather prefilter
 (allgather: every rank keeps the global summary; per window each rank's delta goes to every other
 rank over its own link and every rank folds the others' deltas with marking paused)
 """
@@ -46,7 +46,94 @@ for _w in range(3):
 _wa.close(); _wb.close()
 torch.cuda.synchronize()
 
+def sim_prefilter(P, NW):
+    """GS_MERGE_PREFILTER: the global window (P x the per-rank W) split into rank 0's share
+    (SIM_SHARE0) and P - 1 equal sender slices. Rank 0 folds its share; each sender slice is
+    filtered (gs_cc_filter_edges, against rank 0's own current filter state: the broadcast is not
+    stale here, so survivors are a lower bound) and its survivors folded by rank 0; rank 0 closes.
+    Per window: with a broadcast due (each of the first 4 windows, then every 8th: 8 MiB at
+    BCAST_BW) the chain is serial — sender filters, transfer, rank 0's survivor fold + close, the
+    broadcast; otherwise senders (filtering window w + 1) and rank 0 (its fold, the survivors and
+    the close of window w) overlap and the window costs the longer of the two."""
+    share0 = float(os.environ.get("SIM_SHARE0", str(1.0 / (2 * P))))
+    BCAST_BW = 64e9
+    GAP = 3.0                                         # us per dependent launch boundary (barrier lab)
+    # the one-GPU reference on the same clock: whole windows folded and closed, kernel time + 2 gaps
+    one = gsgpu.DisjointSet(V, id_bits=32, stream=torch.cuda.current_stream())
+    one.timing(True)
+    wa = torch.empty(W * P, dtype=torch.int32, device="cuda")
+    wb = torch.empty(W * P, dtype=torch.int32, device="cuda")
+    base = 0.0
+    for w in range(NW):
+        gen.rmat(wa, wb, w * W * P, scale, 1)
+        k0_ = sum(one.kernel_time(k)[0] for k in range(6))
+        one.fold(wa, wb)
+        one.close_window()
+        torch.cuda.synchronize()
+        base += (sum(one.kernel_time(k)[0] for k in range(6)) - k0_) * 1e3 + 2 * GAP
+    one.close()
+    del wa, wb
+    print("one GPU, same stream, kernel time + 2 launch gaps per window: %.2f ms" % (base / 1e3), flush=True)
+    Wg = W * P
+    W0 = max(4, int(Wg * share0) // 4 * 4)
+    W1 = (Wg - W0) // (P - 1) // 4 * 4
+    W0 = Wg - W1 * (P - 1)
+    m0 = gsgpu.DisjointSet(V, id_bits=32, stream=torch.cuda.current_stream())
+    ss = torch.empty(max(W0, W1), dtype=torch.int32, device="cuda")
+    sd = torch.empty(max(W0, W1), dtype=torch.int32, device="cuda")
+    outs = [torch.empty(2 * W1, dtype=torch.int32, device="cuda") for _ in range(P - 1)]
+    gbytes = V // 8
+    m0.timing(True)                                   # kernel time of every launch (HIP events)
+
+    def ktime():
+        return sum(m0.kernel_time(k)[0] for k in range(6)) * 1e3        # us, cumulative
+
+    def ktimed(fn):                                   # (result, kernel-only us of the launches fn made)
+        k0 = ktime()
+        r = fn()
+        torch.cuda.synchronize()
+        return r, ktime() - k0
+    kt = dict(crit=0.0)
+    print("== prefilter P=%d scale=%d global window 2^%d: rank 0 %d edges, senders %d each" %
+          (P, scale, Wg.bit_length() - 1, W0, W1), flush=True)
+    tot = dict(crit=0.0, filt=0.0, merge=0.0, close=0.0, own=0.0, surv=0)
+    for w in range(NW):
+        gen.rmat(ss[:W0], sd[:W0], w * Wg, scale, 1)
+        _, k0 = ktimed(lambda: m0.fold(ss[:W0], sd[:W0]))
+        ns, kf = [], []
+        for r in range(1, P):
+            gen.rmat(ss[:W1], sd[:W1], w * Wg + W0 + (r - 1) * W1, scale, 1)
+            n, k = ktimed(lambda: m0.filter_edges(ss[:W1], sd[:W1], outs[r - 1]))
+            ns.append(n); kf.append(k)
+        allp = torch.cat([outs[r - 1][:2 * ns[r - 1]] for r in range(1, P)])     # every survivor, one fold
+        _, km = ktimed(lambda: m0.fold_pairs(allp, allp.numel() // 2, id_bits=32) if allp.numel() else None)
+        _, kc = ktimed(lambda: m0.close_window())
+        t0, tf, tm, tc = k0, kf, km, kc              # kernel time only (HIP events on the launches)
+        xfer = max(8 * n / LINK * 1e6 for n in ns)
+        due = w < 4 or w % 8 == 7
+        bc = gbytes / BCAST_BW * 1e6 if due else 0.0
+        if due:
+            crit = max(max(tf) + xfer, t0) + tm + tc + bc
+        else:
+            crit = max(max(tf) + xfer, t0 + tm + tc)
+        crit += GAP * 4                               # rank 0's chain: own fold, receive, fold, close
+        tot["crit"] += crit; tot["filt"] += max(tf); tot["merge"] += tm; tot["close"] += tc; tot["own"] += t0
+        tot["surv"] += sum(ns)
+        print("w%3d own fold %6.0f us  sender filter max %6.0f us  survivors %8d (max %7d)  xfer %5.0f  "
+              "merge folds %6.0f  close %5.0f  bcast %5.0f  critical %6.0f us" %
+              (w + 1, t0, max(tf), sum(ns), max(ns), xfer, tm, tc, bc, crit), flush=True)
+    print("TOTAL prefilter: own %.2f ms, sender filter %.2f, merge %.2f, close %.2f, critical %.2f ms, survivors %d; "
+          "one GPU %.2f ms -> model speedup %.2fx at P=%d"
+          % (tot["own"] / 1e3, tot["filt"] / 1e3, tot["merge"] / 1e3, tot["close"] / 1e3, tot["crit"] / 1e3,
+             tot["surv"], base / 1e3, base / tot["crit"], P), flush=True)
+    m0.close()
+    torch.cuda.synchronize()
+
+
 for scheme in schemes:
+    if scheme == "prefilter":
+        sim_prefilter(P, NW)
+        continue
     ag = scheme == "allgather"       # replicated summaries: every rank folds every other rank's delta
     ranks = [gsgpu.DisjointSet(V, id_bits=32, track_marks=(ag or r != 0), stream=torch.cuda.current_stream()) for r in range(P)]
     if ag:
