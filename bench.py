@@ -95,14 +95,16 @@ def parse():
     ap.add_argument("--host-loop", action="store_true",
                     help="drive the windows from Python (fold + close / merge per window) instead of one "
                          "gs_cc_fold_windows call per step (an A/B of the host loop)")
-    ap.add_argument("--merge", default="allgather", choices=["allgather", "gather", "tree", "prefilter"],
+    ap.add_argument("--merge", default=None, choices=["allgather", "gather", "tree", "prefilter"],
                     help="multi-rank CombineCC: allgather = replicated global summary (every rank folds every "
                          "delta); gather = windowAll gather to rank 0 (SummaryBulkAggregation.java:81); tree = "
                          "log2(P) pairwise rounds (SummaryTreeReduce.java:95-123); prefilter = ranks 1..P-1 "
                          "filter their slices against rank 0's broadcast giant bitmap and send the survivors, "
-                         "rank 0 (the Merger) folds and emits (C ABI / RCCL only)")
+                         "rank 0 (the Merger) folds and emits (C ABI / RCCL only). Default: prefilter over "
+                         "RCCL at P > 1 (the one-GPU rank model's best: DESIGN.md section 6), else allgather")
     ap.add_argument("--share0", type=float, default=None,
-                    help="prefilter, strong layout: rank 0's share of every global window (default 1/(2P)); "
+                    help="prefilter, strong layout: rank 0's share of every global window (default "
+                         "(1 + 1/8) / P - 1/8: P=2 0.44, P=4 0.16, P=8 0.016); "
                          "the other ranks split the rest evenly")
     ap.add_argument("--no-fold-timing", action="store_true",
                     help="no HIP events on the timed region's fold launches (value only; the roofline "
@@ -119,6 +121,14 @@ def parse():
     return a
 
 
+def prefilter_share0(world: int) -> float:
+    """Rank 0's default share of a window under --merge prefilter: its per-window work beyond its
+    own slice (the survivors' fold, the close, the launch gaps) costs about as much as filtering 1/8
+    of a window (tools/sim_ranks.py prefilter, profiles/r05_pre_*), so the slices balance at
+    W1 = (1 + 1/8) W / P for the filtering ranks and W0 = W1 - W / 8 for rank 0."""
+    return max(0.0, (1.0 + 0.125) / world - 0.125)
+
+
 def layout(a, world: int, rank: int):
     """(edges this rank folds, its slice per window, global window, windows, global stream edges,
     the slice's offset inside a global window)."""
@@ -131,8 +141,10 @@ def layout(a, world: int, rank: int):
         if a.merge == "prefilter" and world > 1:
             # the Merger (rank 0) takes share0 of each window, the filtering ranks the rest; slices
             # are multiples of 4 edges (16-B aligned SoA groups)
-            share0 = a.share0 if a.share0 is not None else 1.0 / (2 * world)
+            share0 = a.share0 if a.share0 is not None else prefilter_share0(world)
             W1 = int(W_glob * (1 - share0) / (world - 1)) // 4 * 4
+            if W_glob - (world - 1) * W1 < 4:                # rank 0 exchanges every window: >= 4 edges
+                W1 -= 4
             W0 = W_glob - (world - 1) * W1
             W_rank = W0 if rank == 0 else W1
             off = 0 if rank == 0 else W0 + (rank - 1) * W1
@@ -160,6 +172,8 @@ def main():
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if a.merge is None:
+        a.merge = "prefilter" if world > 1 and a.dist_backend == "nccl" else "allgather"
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
     local = local % max(ndev, 1)          # more ranks than GPUs only in the gloo test mode

@@ -671,7 +671,7 @@ int merge_gather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
 // (8 MiB at 2^26 ids; a staler bitmap only lets more edges survive).
 constexpr uint64_t kExactYoung = 16;
 constexpr uint64_t kBcastYoung = 4;                // the giant forms in the first windows
-constexpr uint64_t kBcastEvery = 8;
+constexpr uint64_t kBcastEvery = 16;               // 8 MiB at 2^26 ids: ~130 us at 64 GB/s
 bool bcast_due(uint64_t win) { return win < kBcastYoung || win % kBcastEvery == kBcastEvery - 1; }
 
 int bcast_filter_state(gs_comm_t* c, gs_cc_t* h, hipStream_t s) {

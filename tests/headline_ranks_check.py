@@ -6,8 +6,8 @@ window exchanged and closed through the C ABI (gs_cc_merge_window) in the chosen
   gather     the windowAll gather to rank 0 (SummaryBulkAggregation.java:81-83): rank 0 is checked;
   tree       ConnectedComponentsTree's pairwise rounds (SummaryTreeReduce.java:95-123): rank 0;
   prefilter  ranks 1..P-1 filter their slices against rank 0's broadcast giant bitmap (with their own
-             hot / warm sets at these ids) and send the survivors; rank 0 takes 1/(2P) of each
-             window, folds everything and emits (gs_cc_fold_windows per window): rank 0.
+             hot / warm sets at these ids) and send the survivors; rank 0 takes bench.py's default
+             share of each window, folds everything and emits (gs_cc_fold_windows per window): rank 0.
 RCCL cannot put several ranks on one GPU, so the ranks are threads over the in-process transport
 (gs_comm_create_local): the same exchange code, collectives as device copies.
 
@@ -65,8 +65,9 @@ def main():
     errors = []
     Wr = W // P
     pre = a.mode == "prefilter"
-    if pre:                                   # bench.py's prefilter layout: rank 0 1/(2P) of each window
-        W1 = int(W * (1 - 1.0 / (2 * P)) / (P - 1)) // 4 * 4
+    if pre:                                   # bench.py's prefilter layout (its default share for rank 0)
+        from bench import prefilter_share0
+        W1 = int(W * (1 - prefilter_share0(P)) / (P - 1)) // 4 * 4
         W0 = W - (P - 1) * W1
         sl = [(0, W0)] + [(W0 + (q - 1) * W1, W1) for q in range(1, P)]
     else:

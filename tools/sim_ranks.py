@@ -51,11 +51,11 @@ def sim_prefilter(P, NW):
     (SIM_SHARE0) and P - 1 equal sender slices. Rank 0 folds its share; each sender slice is
     filtered (gs_cc_filter_edges, against rank 0's own current filter state: the broadcast is not
     stale here, so survivors are a lower bound) and its survivors folded by rank 0; rank 0 closes.
-    Per window: with a broadcast due (each of the first 4 windows, then every 8th: 8 MiB at
+    Per window: with a broadcast due (each of the first 4 windows, then every 16th: 8 MiB at
     BCAST_BW) the chain is serial — sender filters, transfer, rank 0's survivor fold + close, the
     broadcast; otherwise senders (filtering window w + 1) and rank 0 (its fold, the survivors and
     the close of window w) overlap and the window costs the longer of the two."""
-    share0 = float(os.environ.get("SIM_SHARE0", str(1.0 / (2 * P))))
+    share0 = float(os.environ.get("SIM_SHARE0", str(max(0.0, 1.125 / P - 0.125))))   # bench.py prefilter_share0
     BCAST_BW = 64e9
     GAP = 3.0                                         # us per dependent launch boundary (barrier lab)
     # the one-GPU reference on the same clock: whole windows folded and closed, kernel time + 2 gaps
@@ -110,7 +110,7 @@ def sim_prefilter(P, NW):
         _, kc = ktimed(lambda: m0.close_window())
         t0, tf, tm, tc = k0, kf, km, kc              # kernel time only (HIP events on the launches)
         xfer = max(8 * n / LINK * 1e6 for n in ns)
-        due = w < 4 or w % 8 == 7
+        due = w < 4 or w % 16 == 15
         bc = gbytes / BCAST_BW * 1e6 if due else 0.0
         if due:
             crit = max(max(tf) + xfer, t0) + tm + tc + bc
