@@ -46,6 +46,38 @@ for _w in range(3):
 _wa.close(); _wb.close()
 torch.cuda.synchronize()
 
+KT = not os.environ.get("SIM_WALL")     # kernel time (HIP events on the launches) + GAP per boundary;
+GAP = 3.0                               # SIM_WALL=1: the round-1..4 wall accounting per operation
+
+
+def op(h, fn):
+    """(result, us) of fn's work on handle h: its kernels' time (KT) or the wall time of the op."""
+    if not KT:
+        return timed(fn)
+    k0 = sum(h.kernel_time(k)[0] for k in range(6))
+    r = fn()
+    torch.cuda.synchronize()
+    return r, (sum(h.kernel_time(k)[0] for k in range(6)) - k0) * 1e3
+
+
+def one_gpu_base(P, NW):
+    """The one-GPU reference on the same clock: whole global windows folded and closed."""
+    one = gsgpu.DisjointSet(V, id_bits=32, stream=torch.cuda.current_stream())
+    one.timing(True)
+    wa = torch.empty(W * P, dtype=torch.int32, device="cuda")
+    wb = torch.empty(W * P, dtype=torch.int32, device="cuda")
+    base = 0.0
+    for w in range(NW):
+        gen.rmat(wa, wb, w * W * P, scale, 1)
+        _, t1 = op(one, lambda: one.fold(wa, wb))
+        _, t2 = op(one, lambda: one.close_window())
+        base += t1 + t2 + (2 * GAP if KT else 0.0)
+    one.close()
+    print("one GPU, same stream: %.2f ms (%s)" % (base / 1e3, "kernel time + 2 launch gaps per window" if KT
+                                                  else "wall time per operation"), flush=True)
+    return base
+
+
 def sim_prefilter(P, NW):
     """GS_MERGE_PREFILTER: the global window (P x the per-rank W) split into rank 0's share
     (SIM_SHARE0) and P - 1 equal sender slices. Rank 0 folds its share; each sender slice is
@@ -57,23 +89,7 @@ def sim_prefilter(P, NW):
     the close of window w) overlap and the window costs the longer of the two."""
     share0 = float(os.environ.get("SIM_SHARE0", str(max(0.0, 1.125 / P - 0.125))))   # bench.py prefilter_share0
     BCAST_BW = 64e9
-    GAP = 3.0                                         # us per dependent launch boundary (barrier lab)
-    # the one-GPU reference on the same clock: whole windows folded and closed, kernel time + 2 gaps
-    one = gsgpu.DisjointSet(V, id_bits=32, stream=torch.cuda.current_stream())
-    one.timing(True)
-    wa = torch.empty(W * P, dtype=torch.int32, device="cuda")
-    wb = torch.empty(W * P, dtype=torch.int32, device="cuda")
-    base = 0.0
-    for w in range(NW):
-        gen.rmat(wa, wb, w * W * P, scale, 1)
-        k0_ = sum(one.kernel_time(k)[0] for k in range(6))
-        one.fold(wa, wb)
-        one.close_window()
-        torch.cuda.synchronize()
-        base += (sum(one.kernel_time(k)[0] for k in range(6)) - k0_) * 1e3 + 2 * GAP
-    one.close()
-    del wa, wb
-    print("one GPU, same stream, kernel time + 2 launch gaps per window: %.2f ms" % (base / 1e3), flush=True)
+    base = one_gpu_base(P, NW)
     Wg = W * P
     W0 = max(4, int(Wg * share0) // 4 * 4)
     W1 = (Wg - W0) // (P - 1) // 4 * 4
@@ -135,7 +151,10 @@ for scheme in schemes:
         sim_prefilter(P, NW)
         continue
     ag = scheme == "allgather"       # replicated summaries: every rank folds every other rank's delta
+    base = one_gpu_base(P, NW)
     ranks = [gsgpu.DisjointSet(V, id_bits=32, track_marks=(ag or r != 0), stream=torch.cuda.current_stream()) for r in range(P)]
+    for h in ranks:
+        h.timing(True)
     if ag:
         dbufs = [torch.empty(4 * V, dtype=torch.int32, device="cuda") for _ in range(P)]   # 2V pairs: the export contract
         rbuf = [torch.empty(2, dtype=torch.int32, device="cuda")]
@@ -146,14 +165,14 @@ for scheme in schemes:
         fold_us = []
         for r in range(P):
             gen.rmat(s, d, w * W * P + r * W, scale, 1)
-            _, t = timed(lambda: ranks[r].fold(s, d))
+            _, t = op(ranks[r], lambda: ranks[r].fold(s, d))
             fold_us.append(t)
         merge_us, xfer_us, npairs = 0.0, 0.0, []
         if ag:
             tex = []
             cnt_dev = torch.zeros(P, dtype=torch.int64, device="cuda")
             for r in range(P):
-                _, te = timed(lambda: ranks[r].export_marks_async(dbufs[r], cnt_dev[r:r + 1]))
+                _, te = op(ranks[r], lambda: ranks[r].export_marks_async(dbufs[r], cnt_dev[r:r + 1]))
                 tex.append(te)
             ns = [int(x) for x in cnt_dev.tolist()]
             if os.environ.get("SIM_VERBOSE") and w in (0, 15, 63):
@@ -172,7 +191,7 @@ for scheme in schemes:
             mt = []
             for r in range(P):
                 ranks[r].set_marking(False)
-                _, tf = timed(lambda: fold_slots(ranks[r], rbuf[0], m, [0 if q == r else ns[q] for q in range(P)]) if m else None)
+                _, tf = op(ranks[r], lambda: fold_slots(ranks[r], rbuf[0], m, [0 if q == r else ns[q] for q in range(P)]) if m else None)
                 ranks[r].set_marking(True)
                 mt.append(tf)
             merge_us = max(mt)
@@ -181,8 +200,8 @@ for scheme in schemes:
         elif scheme == "gather":
             per = []
             for r in range(1, P):
-                n, te = timed(lambda: ranks[r].export_marks(buf))
-                _, tf = timed(lambda: ranks[0].fold_pairs(buf, n, id_bits=32))
+                n, te = op(ranks[r], lambda: ranks[r].export_marks(buf))
+                _, tf = op(ranks[0], lambda: ranks[0].fold_pairs(buf, n, id_bits=32))
                 npairs.append(n); merge_us += tf; per.append(te + 8 * n / LINK * 1e6)
                 if os.environ.get("SIM_VERBOSE") and w < 2:
                     print("   w%d rank %d: %d pairs, export %.0f us, merge fold %.0f us" % (w + 1, r, n, te, tf), flush=True)
@@ -193,25 +212,27 @@ for scheme in schemes:
                 for r in range(P):
                     role, peer = scheds[r][i]
                     if role == "send":
-                        n, te = timed(lambda: ranks[r].export_marks(buf))
-                        _, tf = timed(lambda: ranks[peer].fold_pairs(buf, n, id_bits=32))
+                        n, te = op(ranks[r], lambda: ranks[r].export_marks(buf))
+                        _, tf = op(ranks[peer], lambda: ranks[peer].fold_pairs(buf, n, id_bits=32))
                         npairs.append(n)
                         rnd_x = max(rnd_x, te + 8 * n / LINK * 1e6)
                         rnd_m = max(rnd_m, tf)
                 xfer_us += rnd_x; merge_us += rnd_m
         close_us = []
         for r in range(P):
-            _, t = timed(lambda: ranks[r].close_window())
+            _, t = op(ranks[r], lambda: ranks[r].close_window())
             close_us.append(t)
-        crit = max(fold_us) + xfer_us + merge_us + (max(close_us) if ag else close_us[0])
+        crit = max(fold_us) + xfer_us + merge_us + (max(close_us) if ag else close_us[0]) + (GAP * 4 if KT else 0.0)
         tot["fold"] += max(fold_us); tot["close"] += close_us[0]; tot["crit"] += crit
         tot["xfer"] += xfer_us; tot["merge"] += merge_us; tot["pairs"] += sum(npairs)
         print("w%3d fold max %6.0f us (r0 %6.0f)  pairs %8d (max %7d)  xfer %6.0f  merge folds %6.0f  close r0 %5.0f  "
               "critical %6.0f us" % (w + 1, max(fold_us), fold_us[0], sum(npairs), max(npairs or [0]), xfer_us,
                                      merge_us, close_us[0], crit), flush=True)
     print("TOTAL %s: fold %.2f ms, xfer %.2f, merge %.2f, close %.2f, critical %.2f ms -> efficiency vs no-merge %.3f, "
-          "pairs %d" % (scheme, tot["fold"] / 1e3, tot["xfer"] / 1e3, tot["merge"] / 1e3, tot["close"] / 1e3,
-                        tot["crit"] / 1e3, (tot["fold"] + tot["close"]) / tot["crit"], tot["pairs"]), flush=True)
+          "pairs %d; one GPU %.2f ms -> model speedup %.2fx at P=%d"
+          % (scheme, tot["fold"] / 1e3, tot["xfer"] / 1e3, tot["merge"] / 1e3, tot["close"] / 1e3,
+             tot["crit"] / 1e3, (tot["fold"] + tot["close"]) / tot["crit"], tot["pairs"], base / 1e3,
+             base / tot["crit"], P), flush=True)
     for r in ranks:
         r.close()
     torch.cuda.synchronize()
