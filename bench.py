@@ -104,7 +104,7 @@ def parse():
                          "RCCL at P > 1 (the one-GPU rank model's best: DESIGN.md section 6), else allgather")
     ap.add_argument("--share0", type=float, default=None,
                     help="prefilter, strong layout: rank 0's share of every global window (default "
-                         "(1 + 1/8) / P - 1/8: P=2 0.44, P=4 0.16, P=8 0.016); "
+                         "(1 + 1/8) / P - 1/8: P=2 0.44, P=4 0.16, P=8 0 = 4 edges); "
                          "the other ranks split the rest evenly")
     ap.add_argument("--no-fold-timing", action="store_true",
                     help="no HIP events on the timed region's fold launches (value only; the roofline "
@@ -124,9 +124,12 @@ def parse():
 def prefilter_share0(world: int) -> float:
     """Rank 0's default share of a window under --merge prefilter: its per-window work beyond its
     own slice (the survivors' fold, the close, the launch gaps) costs about as much as filtering 1/8
-    of a window (tools/sim_ranks.py prefilter, profiles/r05_pre_*), so the slices balance at
-    W1 = (1 + 1/8) W / P for the filtering ranks and W0 = W1 - W / 8 for rank 0."""
-    return max(0.0, (1.0 + 0.125) / world - 0.125)
+    of a window (tools/sim_ranks.py prefilter, profiles/r05_prefilter_sim_*), so the slices balance
+    at W1 = (1 + 1/8) W / P for the filtering ranks and W0 = W1 - W / 8 for rank 0. Below 1/32 of a
+    window rank 0's own fold is mostly its launch (24 us for 2^18 edges at P = 8): it then keeps
+    only the 4-edge minimum (layout())."""
+    s = max(0.0, (1.0 + 0.125) / world - 0.125)
+    return s if s >= 1.0 / 32 else 0.0
 
 
 def layout(a, world: int, rank: int):

@@ -87,7 +87,8 @@ def sim_prefilter(P, NW):
     BCAST_BW) the chain is serial — sender filters, transfer, rank 0's survivor fold + close, the
     broadcast; otherwise senders (filtering window w + 1) and rank 0 (its fold, the survivors and
     the close of window w) overlap and the window costs the longer of the two."""
-    share0 = float(os.environ.get("SIM_SHARE0", str(max(0.0, 1.125 / P - 0.125))))   # bench.py prefilter_share0
+    s0 = max(0.0, 1.125 / P - 0.125)                                                   # bench.py prefilter_share0
+    share0 = float(os.environ.get("SIM_SHARE0", str(s0 if s0 >= 1.0 / 32 else 0.0)))
     BCAST_BW = 64e9
     base = one_gpu_base(P, NW)
     Wg = W * P
