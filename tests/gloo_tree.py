@@ -7,7 +7,7 @@ delta contract.
 Three exchanges behind one contract (``merge_window()`` after each window's fold; True on the
 rank that emitted):
 
-``AllgatherMerge`` (bench default): replicated summaries. Every rank keeps the GLOBAL summary: per
+``AllgatherMerge`` (bench.py's gloo-mode default): replicated summaries. Every rank keeps the GLOBAL summary: per
 window each rank exports its delta (the connectivity its own slice added), the deltas are
 all-gathered (one RCCL all-gather of slots padded to the largest delta; on xGMI every pair of
 GPUs has its own link), and each rank folds the others' deltas with marking paused. Every rank's filter is then the global giant component, so the
@@ -18,6 +18,9 @@ partition's partial summary goes to the one parallelism-1 task) as one flat gath
 every other rank sends its window's pairs straight to rank 0 over its own xGMI link, all at once,
 and rank 0 folds them.
 ``TreeMerge`` (ConnectedComponentsTree): log2(P) pairwise rounds (SummaryTreeReduce.enhance).
+``PrefilterMerge`` (GS_MERGE_PREFILTER, bench.py's default over RCCL at P > 1): ranks 1..P-1 filter
+their slices against rank 0's broadcast giant bitmap and send the survivors to rank 0 (CPU tests
+only: the product path is comm.hip).
 
 Restates the reference's tree reduction ``SummaryTreeReduce.enhance``
 (src/main/java/org/apache/flink/graph/streaming/SummaryTreeReduce.java:95-123: each round keys
@@ -43,6 +46,7 @@ from __future__ import annotations
 
 from typing import List, Tuple
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -407,3 +411,67 @@ def fold_slots(summary, buf, m: int, counts) -> None:
         npairs = (e - q) * m + counts[e]
         summary.fold_pairs(buf[2 * q * m: 2 * (q * m + npairs)], npairs, id_bits=32)
         q = e + 1
+
+
+class PrefilterMerge:
+    """GS_MERGE_PREFILTER restated over torch.distributed (csrc/comm.hip merge_prefilter): rank 0
+    is the Merger (the summary); ranks 1..P-1 keep only a giant bitmap — the component rank 0
+    broadcasts after its closes of windows w < BCAST_YOUNG and every BCAST_EVERY-th — and send the
+    edges of their slice that are NOT inside it (count, then the pairs) to rank 0, which folds its
+    own slice and everyone's survivors and closes. The giant here is the largest component at the
+    close (the device samples it; any component is correct: a stale or switched bitmap only lets
+    more edges through, components only merge). ``merge_window(src, dst)`` takes this rank's slice
+    of the window (rank 0 has folded its own already) and returns True on rank 0."""
+    BCAST_YOUNG, BCAST_EVERY = 4, 16
+
+    def __init__(self, summary, capacity: int, device: torch.device, group=None):
+        self.summary, self.cap, self.device, self.group = summary, int(capacity), device, group
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        self.gbits = torch.zeros(self.cap, dtype=torch.uint8, device=device)
+        self.win = 0
+        self.survivors_sent = 0
+
+    def _g(self, r: int) -> int:
+        return dist.get_global_rank(self.group, r) if self.group is not None else r
+
+    def _pick(self) -> None:
+        p = self.summary.parent
+        seen = p >= 0
+        if not seen.any():
+            self.gbits.zero_()
+            return
+        self.summary.close_window()
+        roots = p[seen]
+        vals, cnt = np.unique(roots, return_counts=True)
+        g = vals[int(np.argmax(cnt))]
+        self.gbits.copy_(torch.from_numpy((p == g).astype(np.uint8)))
+
+    def merge_window(self, src, dst) -> bool:
+        w, self.win = self.win, self.win + 1
+        if self.rank != 0:
+            s = np.asarray(src, dtype=np.int64)
+            d = np.asarray(dst, dtype=np.int64)
+            gb = self.gbits.cpu().numpy().astype(bool)
+            keep = ~(gb[s] & gb[d])
+            pairs = np.empty(2 * int(keep.sum()), dtype=np.int64)
+            pairs[0::2], pairs[1::2] = s[keep], d[keep]
+            n = torch.tensor([pairs.size // 2], dtype=torch.int64, device=self.device)
+            dist.send(n, self._g(0), group=self.group)
+            if pairs.size:
+                dist.send(torch.from_numpy(pairs).to(self.device), self._g(0), group=self.group)
+            self.survivors_sent += pairs.size // 2
+        else:
+            for q in range(1, self.world):
+                n = torch.zeros(1, dtype=torch.int64, device=self.device)
+                dist.recv(n, self._g(q), group=self.group)
+                if int(n.item()):
+                    buf = torch.empty(2 * int(n.item()), dtype=torch.int64, device=self.device)
+                    dist.recv(buf, self._g(q), group=self.group)
+                    b = buf.cpu().numpy()
+                    self.summary.fold(b[0::2], b[1::2])
+            self.summary.close_window()
+        if w < self.BCAST_YOUNG or w % self.BCAST_EVERY == self.BCAST_EVERY - 1:
+            if self.rank == 0:
+                self._pick()
+            dist.broadcast(self.gbits, self._g(0), group=self.group)
+        return self.rank == 0

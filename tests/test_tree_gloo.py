@@ -24,6 +24,32 @@ def _free_port():
     return p
 
 
+def _worker_prefilter(rank, world, port, src, dst, W, cap, outdir, share0):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "gelly-streaming_amd"), os.path.join(root, "oracle"), os.path.join(root, "tests")]
+    from gloo_tree import PrefilterMerge
+    from pyoracle import PyMarkedSummary
+    from variant_check import rank_slices
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        summ = PyMarkedSummary(cap, track_marks=False)
+        pm = PrefilterMerge(summ, cap, torch.device("cpu"))
+        emis = []
+        for lo, hi in rank_slices(len(src), W, world, share0)[rank]:
+            if rank == 0:
+                summ.fold(src[lo:hi], dst[lo:hi])
+            if pm.merge_window(src[lo:hi], dst[lo:hi]):
+                emis.append(summ.dense())
+        if rank == 0:
+            np.save(os.path.join(outdir, "emis0.npy"), np.stack(emis))
+        np.save(os.path.join(outdir, "sent%d.npy" % rank), np.array([pm.survivors_sent]))
+    finally:
+        dist.destroy_process_group()
+
+
 def _worker(rank, world, port, src, dst, W, cap, outdir, kind):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -123,3 +149,40 @@ def test_fold_slots_covers_real_pairs_only(monkeypatch, bulk):
     r = Rec()
     tree.fold_slots(r, buf, m, counts)
     assert r.got == real
+
+
+@pytest.mark.parametrize("world,share0", [(2, 0.4), (3, 0.0), (4, 0.15)])
+def test_prefilter_merge_gloo_matches_oracle(tmp_path, oracle, world, share0):
+    """GS_MERGE_PREFILTER's dataflow (tests/gloo_tree.py PrefilterMerge = csrc/comm.hip
+    merge_prefilter): ranks 1..P-1 filter their slices against rank 0's broadcast giant bitmap
+    (stale between broadcasts) and send survivors; rank 0's emission after every window equals the
+    oracle pipeline's. Two vertex blocks: the first giant forms in one block, a bigger one in the
+    other takes over, then they join — a broadcast bitmap of the wrong (old) component between
+    broadcasts is what the filter must tolerate."""
+    rng = np.random.default_rng(7)
+    W, cap = 800, 2048
+
+    def block(lo, hi, n):
+        return rng.integers(lo, hi, n), rng.integers(lo, hi, n)
+    src, dst = [], []
+    for _ in range(6):
+        a, b = block(0, 400, W); src.append(a); dst.append(b)
+    for _ in range(14):
+        a, b = block(1024, 2048, W); src.append(a); dst.append(b)
+    for _ in range(20):
+        a1, b1 = block(0, 512, W // 2)
+        a2, b2 = block(1024, 2048, W // 2)
+        a, b = np.concatenate([a1, a2]), np.concatenate([b1, b2])
+        b[:3] = rng.integers(1024, 2048, 3)                       # a few cross-block edges
+        a[3:6] = b[3:6]                                           # self-loops
+        src.append(a); dst.append(b)
+    s, d = np.concatenate(src).astype(np.int64), np.concatenate(dst).astype(np.int64)
+    mp.spawn(_worker_prefilter, args=(world, _free_port(), s, d, W, cap, str(tmp_path), share0), nprocs=world, join=True)
+    from pyoracle import EMIT_DENSE
+    want = oracle.run(s, d, W, partitions=world, emit=EMIT_DENSE, label_cap=cap)["labels"]
+    got = np.load(tmp_path / "emis0.npy")
+    assert got.shape == want.shape
+    np.testing.assert_array_equal(got, want)
+    # the filter did drop edges: the senders sent fewer than their slices
+    sent = sum(int(np.load(tmp_path / ("sent%d.npy" % r))[0]) for r in range(1, world))
+    assert 0 < sent < len(s) * (1 - share0) * 0.9
