@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 5: prefilter senders send a flagged endpoint as the giant root — tests, 8-rank headline
+# layout, rank model at P = 2, 4, 8.
+set -u
+OUT=gpurun_out/r05_pre4
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests/test_gpu_prefilter.py tests/test_gpu_variants.py -k "prefilter" -x -v \
+    --timeout 850 --timeout-method thread > "$OUT/pytest.log" 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 "$OUT/pytest.log"; [ $rc -eq 0 ] || { grep -E "Error|assert" "$OUT/pytest.log" | head -20; exit 3; }
+timeout -k 10 600 python -u tests/variant_check.py > "$OUT/variant.json" 2> "$OUT/variant.err"
+rc=$?; echo "variant rc=$rc"; python -c "
+import json; d=json.loads([l for l in open('$OUT/variant.json') if l.startswith('{')][-1]); print('ok', d['ok']); [print(c) for c in d['cases'] if 'prefilter' in c['case'] or not c['ok']]"
+[ $rc -eq 0 ] || exit 3
+for cfg in "2 23" "4 22" "8 21"; do
+  set -- $cfg
+  SIM_WLOG2=$2 timeout -k 10 600 python -u tools/sim_ranks.py $1 64 prefilter > "$OUT/sim_p$1.txt" 2>&1
+  rc=$?; echo "sim P=$1 rc=$rc"; grep TOTAL "$OUT/sim_p$1.txt"; [ $rc -eq 0 ] || { tail -5 "$OUT/sim_p$1.txt"; exit 3; }
+done
+exit 0
