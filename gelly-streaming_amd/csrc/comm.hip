@@ -20,6 +20,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstring>
 #include <memory>
@@ -424,6 +426,14 @@ int settle_allgather(gs_comm_t* c, bool close) {
 
 int abort_exchange(gs_comm_t* c, int rc);
 
+// GSGPU_PREFILTER_LOG=1: a sender's survivor count per window on stderr (once known: at once in
+// the exact rounds, at the settle of a speculative one) — the real staleness of the broadcast
+// bitmap, which tools/sim_ranks.py's filter against the Merger's current state cannot show
+void log_survivors(const gs_comm_t* c, uint64_t n) {
+    static const bool on = [] { const char* e = getenv("GSGPU_PREFILTER_LOG"); return e && atoi(e) != 0; }();
+    if (on) fprintf(stderr, "[gsgpu prefilter] rank %d survivors %llu\n", c->rank, (unsigned long long)n);
+}
+
 // cc_settle's callback: a failed verification fails the group (peers may be in the tail round)
 int settle_gather(gs_comm_t* c, bool close);
 int settle_cb(void* ctx) {
@@ -569,6 +579,7 @@ int settle_gather(gs_comm_t* c, bool close) {
         }
         c->gslot[c->rank] = next_slot(c, n);
         c->last_delta = n;
+        if (c->mode == GS_MERGE_PREFILTER) log_survivors(c, n);
         return GS_OK;
     }
     std::vector<uint64_t> tail(P, 0);
@@ -715,6 +726,7 @@ int merge_prefilter(gs_comm_t* c, gs_cc_t* h, const CcInfo& in, const void* a, c
             c->gslot[c->rank] = next_slot(c, n);
             c->last_delta = n;
             c->pend_buf = c->sendbuf;
+            log_survivors(c, n);
         } else {
             uint32_t* send_buf = (c->pend_buf == c->sendbuf) ? c->sendbuf2 : c->sendbuf;
             const uint64_t S = c->gslot[c->rank];
