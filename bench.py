@@ -322,6 +322,17 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if a.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    sender_filter = None
+    if world > 1 and a.merge == "prefilter":
+        # the filtering ranks' k_filter_out launches (timed as GS_K_RING on their handles): rank 0,
+        # the Merger, folds only survivors, so the line's dominant kernel is theirs (slowest rank)
+        mine = torch.tensor([ring_ms / ring_n if ring_n else 0.0, ring_e / ring_n if ring_n else 0.0, float(ring_n)],
+                            dtype=torch.float64, device=dev)
+        allv = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        rows = [v.tolist() for v in allv[1:]]
+        slow = max(rows, key=lambda x: x[0])
+        sender_filter = {"avg_launch_ms": slow[0], "edges_per_launch": slow[1], "launches": int(slow[2])}
 
     latency = None
     if a.workload == "c5":                    # per-window emission latency: fold -> emission ready
@@ -368,7 +379,10 @@ def main():
         fold_win_ms = (young_ms + ring_ms) / max(folds, 1) or float("nan")
         # the dominant kernel: the steady fold k_fold_ring, bytes per launch from the edges each timed
         # launch actually folded (a long fold call is cut into launches of at most 2^24 edges)
-        if ring_n:
+        if sender_filter and sender_filter["launches"]:
+            kernel, avg_ms, n_l, e_l = ("k_filter_out (filtering ranks; slowest)", sender_filter["avg_launch_ms"],
+                                        sender_filter["launches"], sender_filter["edges_per_launch"])
+        elif ring_n:
             kernel, avg_ms, n_l, e_l = "k_fold_ring", ring_ms / ring_n, ring_n, ring_e / ring_n
         else:                                        # no steady launches (small ids: plain k_fold)
             kernel, avg_ms, n_l, e_l = "k_fold (every window)", fold_win_ms, folds, W_rank
