@@ -280,9 +280,12 @@ constexpr uint32_t kWarmBucketsMaxBits = 18;
                                                     // slower per steady window, r02_u)
 constexpr uint32_t kHotThresh = 3;                  // sightings before hot-set admission (233 -> 229 us)
 // Young split: inside the young forest, close internally (compress + giant pick: no emission,
-// labels stay canonical) after capacity/16 edges, so the rest of the young window folds with the
-// giant filter on (RMAT-26 window 1: 1487 -> 1297 us for one extra full close of 118 us; splits
-// at 2^21 or 2^23, or 3-5 doubling splits, gained less). Only where gbits outgrows L2.
+// labels stay canonical) after S edges, so the rest of the young window folds with the giant
+// filter on. Round 2 measured it at capacity/16 edges: RMAT-26 window 1 1487 -> 1297 us. Round 5,
+// with the young fold's claims and the seen-bit skip since: 16.452-16.481 ms per step without it
+// against 16.572-16.589 with it, three alternations on one box (profiles/r05_young_split_ab.txt) —
+// off by default, GSGPU_YOUNG_SPLIT=S turns it on (the variant tests run it).
+// kYoungSplitDiv: a young launch of >= capacity/kYoungSplitDiv edges skips the seen bitmap (below).
 constexpr uint32_t kYoungSplitDiv = 16;
 // Small plain folds (config 5's 2^16-edge windows): one edge per thread, so a launch spreads over
 // more workgroups and each thread's chain of dependent unions is one union long (a 2^16-edge launch
@@ -299,7 +302,7 @@ constexpr int kSmallEpt = 1;
 //   GSGPU_RING_CLOCKS=1      per-workgroup phase clocks of the window's last k_fold_ring launch on stderr
 //   GSGPU_FOLD_MODE=plain|ring|auto   force the steady fold variant (parity tests of each variant)
 //   GSGPU_RING_MIN_BITS=B    ring fold + warm set from ids >= 2^B instead of 2^25 (tests at small sizes)
-//   GSGPU_YOUNG_SPLIT=S      young split after S edges instead of capacity/16 (0 = off; tests)
+//   GSGPU_YOUNG_SPLIT=S      young split after S edges (default: none; tests and A/B)
 enum FoldMode { kFoldPlain = 0, kFoldRing = 1, kFoldAuto = 2 };
 struct DebugEnv {
     bool fold_stats = false;
@@ -506,7 +509,7 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
 // reset where gbits outgrows L2 (ids >= 2^kRingMinBits), or at GSGPU_YOUNG_SPLIT
 static uint64_t next_young_split(const gs_cc_t* h, uint64_t done) {
     uint64_t s = dbg().young_split;
-    if (s == ~0ull) s = (uint64_t)h->cap >= (1ull << std::min<uint32_t>(dbg().ring_min_bits, 63)) ? h->cap / kYoungSplitDiv : 0;
+    if (s == ~0ull) s = 0;                           // production: no split (above)
     return (s && done < s) ? s : 0;
 }
 
