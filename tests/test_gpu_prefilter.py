@@ -158,3 +158,38 @@ def test_prefilter_rejected_where_it_cannot_run(torch_cuda):
     assert ei.value.code == _abi.GS_ERR_UNSUPPORTED
     sp.close()
     comm.close()
+
+
+def test_prefilter_host_edge_buffers(oracle, torch_cuda):
+    """Host (numpy) slices on every rank: the senders' pre-filter stages them to the device
+    (cc_filter_async's staging copy), rank 0's fold takes its host path; every window vs the oracle."""
+    from variant_check import rank_slices
+    s, d, cap = _rmat(oracle, 14, 96000, 26)
+    W, world = 6000, 3
+    want = oracle.run(s, d, W, partitions=world, emit=EMIT_CHECKSUM, label_cap=cap, want_final=True)
+    sl = rank_slices(s.size, W, world, 0.3)
+    s32, d32 = s.astype(np.int32), d.astype(np.int32)
+    comms = Comm.local_group(world, 0)
+    got, errs = [], []
+
+    def rank(r):
+        try:
+            ds = DisjointSet(cap, id_bits=32)
+            for lo, hi in sl[r]:
+                ds.fold_windows(s32[lo:hi], d32[lo:hi], hi - lo, comm=comms[r], mode="prefilter")
+                if r == 0:
+                    got.append(ds.checksum()[0])
+            ds.close()
+        except Exception as e:                                   # noqa: BLE001
+            errs.append((r, repr(e)))
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th), "a rank hung"
+    for c in comms:
+        c.close()
+    assert not errs, errs
+    assert got == [int(x) for x in want["checksums"]]
