@@ -33,13 +33,22 @@ comms = Comm.local_group(P, 0)
 errors = []
 
 
+merge_ms = [0.0, 0]
+
+
 def rank(r):
     try:
         ds = gsgpu.DisjointSet(V, id_bits=32)
+        if r == 0:                                   # the Merger's survivor folds (GS_K_MERGE launches)
+            from gsgpu._abi import GS_K_MERGE, GS_TIMING_MASK
+            ds.timing(GS_TIMING_MASK | (1 << GS_K_MERGE))
         off, ln = sl[r]
         for w in range(N):
             lo = w * W + off
             ds.fold_windows(src[lo:lo + ln], dst[lo:lo + ln], ln, comm=comms[r], mode="prefilter")
+        if r == 0:
+            from gsgpu._abi import GS_K_MERGE
+            merge_ms[0], merge_ms[1] = ds.kernel_time(GS_K_MERGE)
         ds.close()
     except Exception as e:                                       # noqa: BLE001
         errors.append((r, repr(e)))
@@ -52,4 +61,5 @@ for t in th:
     t.join(timeout=900)
 for c in comms:
     c.close()
-print({"P": P, "rank0_edges": W0, "sender_edges": W1, "errors": errors}, flush=True)
+print({"P": P, "rank0_edges": W0, "sender_edges": W1, "errors": errors,
+       "rank0_merge_ms": round(merge_ms[0], 3), "rank0_merge_launches": merge_ms[1]}, flush=True)
