@@ -43,6 +43,37 @@ inline void check(int rc, const char* where) {
     if (rc != GS_OK) throw GsError(rc, where);
 }
 
+// One rank's communicator for the multi-GPU CombineCC (gs_comm_*, csrc/comm.hip): RCCL from a
+// 128-byte unique id that rank 0 makes (uniqueId) and every rank passes, or an in-process group of
+// `world` ranks on one device (local: one thread per rank, for tests).
+class Comm {
+public:
+    using Id = std::vector<uint8_t>;
+    static Id uniqueId() {
+        Id id(128);
+        check(gs_comm_unique_id(id.data(), id.size()), "gs_comm_unique_id");
+        return id;
+    }
+    Comm(const Id& id, int rank, int world, int device = 0) {
+        check(gs_comm_create(&c_, id.data(), rank, world, device), "gs_comm_create");
+    }
+    static std::vector<std::unique_ptr<Comm>> local(int world, int device = 0) {
+        std::vector<gs_comm_t*> raw((size_t)world, nullptr);
+        check(gs_comm_create_local(raw.data(), world, device), "gs_comm_create_local");
+        std::vector<std::unique_ptr<Comm>> out;
+        for (gs_comm_t* c : raw) out.emplace_back(new Comm(c));
+        return out;
+    }
+    ~Comm() { gs_comm_destroy(c_); }
+    Comm(const Comm&) = delete;
+    Comm& operator=(const Comm&) = delete;
+    gs_comm_t* handle() const { return c_; }
+
+private:
+    explicit Comm(gs_comm_t* c) : c_(c) {}
+    gs_comm_t* c_ = nullptr;
+};
+
 // DisjointSet<K> on the device. K = int32_t or int64_t ids in [0, capacity); with
 // flags = GS_CC_SPARSE_IDS (K = int64_t) any long id, at most `capacity` distinct ones.
 template <typename K>
@@ -171,6 +202,18 @@ public:
 
     // batched UpdateCC: host or device buffers
     void fold(const K* src, const K* dst, uint64_t n) { check(gs_cc_fold(h_, src, dst, n), "gs_cc_fold"); }
+    // after this rank's fold of a window: CombineCC across the ranks + the Merger's close
+    // (GS_MERGE_ALLGATHER / GATHER / TREE; the handle needs GS_CC_TRACK_MARKS)
+    void mergeWindow(Comm& comm, int mode) { check(gs_cc_merge_window(h_, comm.handle(), mode), "gs_cc_merge_window"); }
+    // SummaryBulkAggregation over n edges in windows of windowEdges (this rank's slice of each
+    // window): fold + close, or fold + merge over comm (any mode, GS_MERGE_PREFILTER included);
+    // returns the windows folded
+    uint64_t foldWindows(const K* src, const K* dst, uint64_t n, uint64_t windowEdges, Comm* comm = nullptr,
+                         int mode = GS_MERGE_ALLGATHER) {
+        uint64_t w = 0;
+        check(gs_cc_fold_windows(h_, comm ? comm->handle() : nullptr, mode, src, dst, n, windowEdges, &w), "gs_cc_fold_windows");
+        return w;
+    }
     void closeWindow() { check(gs_cc_close_window(h_), "gs_cc_close_window"); }
     void sync() { check(gs_cc_sync(h_), "gs_cc_sync"); }
 

@@ -193,3 +193,23 @@ def test_prefilter_host_edge_buffers(oracle, torch_cuda):
         c.close()
     assert not errs, errs
     assert got == [int(x) for x in want["checksums"]]
+
+
+def test_prefilter_through_the_cpp_mirror(oracle, torch_cuda):
+    """The C++ host mirror (csrc/host/gsgpu.hpp: Comm::local, DisjointSet::foldWindows) running the
+    Merger-rank layout over 4 in-process ranks (csrc/host/cc_prefilter_check.cpp): rank 0's emission
+    checksum, vertices and components after every window vs the oracle."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "gelly-streaming_amd", "gsgpu", "lib", "cc_prefilter_check")
+    s, d, cap = _rmat(oracle, 14, 60000, 27)
+    W, world = 5000, 4
+    want = oracle.run(s, d, W, partitions=world, emit=EMIT_CHECKSUM, label_cap=cap, want_final=True)
+    text = "".join("%d %d\n" % (a, b) for a, b in zip(s.tolist(), d.tolist()))
+    out = subprocess.run([exe, str(W), str(world), "0.25", str(cap)], input=text, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr
+    rows = [line.split() for line in out.stdout.splitlines()]
+    assert len(rows) == len(want["checksums"])
+    assert [int(r[1]) for r in rows] == [int(x) for x in want["checksums"]]
