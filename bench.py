@@ -126,8 +126,8 @@ def prefilter_share0(world: int) -> float:
     own slice (the survivors' fold, the close, the launch gaps) costs about as much as filtering 1/8
     of a window (tools/sim_ranks.py prefilter, profiles/r05_prefilter_sim_*), so the slices balance
     at W1 = (1 + 1/8) W / P for the filtering ranks and W0 = W1 - W / 8 for rank 0. Below 1/32 of a
-    window rank 0's own fold is mostly its launch (24 us for 2^18 edges at P = 8): it then keeps
-    only the 4-edge minimum (layout())."""
+    window rank 0's own fold is mostly its launch (24 us for 2^18 edges at P = 8): it then folds no
+    slice of its own (the filtering ranks take the whole window, layout())."""
     s = max(0.0, (1.0 + 0.125) / world - 0.125)
     return s if s >= 1.0 / 32 else 0.0
 
@@ -146,11 +146,17 @@ def layout(a, world: int, rank: int):
             # are multiples of 4 edges (16-B aligned SoA groups)
             share0 = a.share0 if a.share0 is not None else prefilter_share0(world)
             W1 = int(W_glob * (1 - share0) / (world - 1)) // 4 * 4
-            if W_glob - (world - 1) * W1 < 4:                # rank 0 exchanges every window: >= 4 edges
-                W1 -= 4
             W0 = W_glob - (world - 1) * W1
-            W_rank = W0 if rank == 0 else W1
-            off = 0 if rank == 0 else W0 + (rank - 1) * W1
+            sizes = [W0] + [W1] * (world - 1)
+            if share0 == 0.0:
+                # no slice on rank 0 (it still joins every window's exchange: the ranks agree on the
+                # window count in gs_cc_fold_windows); the remainder (< 4 (P - 1) edges, a multiple
+                # of 4) goes 4 edges at a time to the first filtering ranks
+                sizes[0] = 0
+                for r in range(W0 // 4):
+                    sizes[1 + r % (world - 1)] += 4
+            W_rank = sizes[rank]
+            off = sum(sizes[:rank])
             return nwin * W_rank, W_rank, W_glob, nwin, E, off
         if W_glob % world:
             raise SystemExit("global window %d does not split over %d ranks" % (W_glob, world))
@@ -199,7 +205,7 @@ def main():
     # ---- inputs resident in HBM (or pinned host memory) before timing ----
     src = torch.empty(E_rank, dtype=idt, device=dev)
     dst = torch.empty(E_rank, dtype=idt, device=dev)
-    for w in range(nwin):
+    for w in range(nwin if W_rank else 0):
         lo, first = w * W_rank, w * W_glob + off_rank
         if a.kind == "er":
             gen.erdos_renyi(src[lo:lo + W_rank], dst[lo:lo + W_rank], first, V, a.seed)
@@ -243,7 +249,7 @@ def main():
         if gather:
             tree.before_fold()
         if comm is not None and a.merge == "prefilter":    # (the exchange takes the window's edges)
-            ds.fold_windows(fsrc[lo:lo + W_rank], fdst[lo:lo + W_rank], W_rank, comm=comm, mode="prefilter")
+            ds.fold_windows(fsrc[lo:lo + W_rank], fdst[lo:lo + W_rank], max(W_rank, 1), comm=comm, mode="prefilter")
         else:
             ds.fold(fsrc[lo:lo + W_rank], fdst[lo:lo + W_rank])
         if comm is not None and a.merge == "prefilter":
@@ -271,7 +277,7 @@ def main():
         ds.reset()
         if batched:
             n_all = nwin * W_rank
-            ds.fold_windows(fsrc[:n_all], fdst[:n_all], W_rank, comm=comm, mode=a.merge)
+            ds.fold_windows(fsrc[:n_all], fdst[:n_all], max(W_rank, 1), comm=comm, mode=a.merge)
         else:
             for w in range(nwin):
                 window(w)
@@ -382,16 +388,23 @@ def main():
         fold_win_ms = (young_ms + ring_ms) / max(folds, 1) or float("nan")
         # the dominant kernel: the steady fold k_fold_ring, bytes per launch from the edges each timed
         # launch actually folded (a long fold call is cut into launches of at most 2^24 edges)
+        k_bytes = per_edge                            # algorithmic bytes per edge of the dominant kernel
+        k_def = "edge read + 2 parent words, SURVEY.md 8(d); 4-B parent words for int64 ids too"
         if sender_filter and sender_filter["launches"]:
             kernel, avg_ms, n_l, e_l = ("k_filter_out (filtering ranks; slowest)", sender_filter["avg_launch_ms"],
                                         sender_filter["launches"], sender_filter["edges_per_launch"])
+            # the filter never touches parent[]: its algorithmic bytes are the edge read (plus the
+            # survivors it writes, a few % of a steady window: not counted) — not comparable with
+            # k_fold_ring rows; PMC traffic stays the comparable figure
+            k_bytes = eb
+            k_def = "filter: edge read only (k_filter_out reads no parent word)"
         elif ring_n:
             kernel, avg_ms, n_l, e_l = "k_fold_ring", ring_ms / ring_n, ring_n, ring_e / ring_n
         else:                                        # no steady launches (small ids: plain k_fold)
             kernel, avg_ms, n_l, e_l = "k_fold (every window)", fold_win_ms, folds, W_rank
         if not avg_ms:                               # --no-fold-timing
             avg_ms = float("nan")
-        alg_launch = per_edge * e_l
+        alg_launch = k_bytes * e_l
         achieved = alg_launch / (avg_ms * 1e-3) / 1e9
         prof, prof_note = steady_profile(a, kernel, e_l)
         step_b = per_edge * E_glob                                  # SURVEY 8(d) edge term per step
@@ -447,9 +460,9 @@ def main():
                 "edges_per_launch": e_l,
                 "avg_launch_ms": avg_ms,
                 "launches": n_l,
-                "definition": "dominant kernel: %d B per edge (edge read + 2 parent words, SURVEY.md 8(d); 4-B parent "
-                              "words for int64 ids too) x the edges each launch folded / its average launch duration "
-                              "(HIP events on the launch stream, the last step of the timed region)" % per_edge,
+                "definition": "dominant kernel: %d B per edge (%s) x the edges each launch folded / its average "
+                              "launch duration (HIP events on the launch stream, the last step of the timed region)"
+                              % (k_bytes, k_def),
                 "fold_all": {"achieved": per_edge * W_rank / (fold_win_ms * 1e-3) / 1e9,
                              "frac": per_edge * W_rank / (fold_win_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                              "ms_per_window": fold_win_ms, "young_launches": young_n,

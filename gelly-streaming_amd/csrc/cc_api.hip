@@ -494,7 +494,10 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     const dim3 grid(grid_for(n / 4, kHotThreads, (unsigned)std::max(h->cus, 1)));
     hipEvent_t stop = build ? nullptr : t.stop();
     hipEvent_t start = t.start();
-    if (h->mark) {
+    if (hot.clocks) {                                // GSGPU_RING_CLOCKS: the instrumented instance
+        if (h->mark) klaunch(k_fold_ring<IdT, true, false, true>, grid, dim3(kHotThreads), h->stream, start, stop, a, b, f, hot);
+        else klaunch(k_fold_ring<IdT, false, false, true>, grid, dim3(kHotThreads), h->stream, start, stop, a, b, f, hot);
+    } else if (h->mark) {
         if (st) klaunch(k_fold_ring<IdT, true, true>, grid, dim3(kHotThreads), h->stream, start, stop, a, b, f, hot);
         else klaunch(k_fold_ring<IdT, true, false>, grid, dim3(kHotThreads), h->stream, start, stop, a, b, f, hot);
     } else {
@@ -1454,11 +1457,15 @@ static int fold_windows_loop(gs_cc_t* h, gs_comm_t* comm, int mode, const char* 
                              uint64_t window_edges, uint64_t* windows_out) {
     const size_t esz = h->cfg.id_bits / 8;
     const int dev = (n && is_device_pointer(a) && is_device_pointer(b)) ? 1 : 0;
-    uint64_t w = 0;
-    // GS_MERGE_PREFILTER: only the Merger (rank 0) folds; the exchange takes the window's edges
+    // GS_MERGE_PREFILTER: only the Merger (rank 0) folds; the exchange takes the window's edges.
+    // Every window is an exchange, so the ranks first agree on the window count: a rank past its
+    // own edges (a short last global window, an empty slice) runs empty windows
     const bool pre = comm && mode == GS_MERGE_PREFILTER;
     const bool fold_here = !pre || cc_comm_rank(comm) == 0;
-    for (uint64_t off = 0; off < n; off += window_edges, ++w) {
+    uint64_t nw = (n + window_edges - 1) / window_edges;
+    if (pre) GS_TRY(cc_agree_windows(h, comm, nw, &nw));
+    for (uint64_t w = 0; w < nw; ++w) {
+        const uint64_t off = std::min(n, w * window_edges);
         const uint64_t m = std::min(window_edges, n - off);
         if (fold_here) GS_TRY(fold_impl(h, a + off * esz, b + off * esz, m, false, h->cfg.id_bits, dev));   // (no settle: above)
         if (pre) GS_TRY(cc_merge_edges(h, comm, mode, a + off * esz, b + off * esz, m));

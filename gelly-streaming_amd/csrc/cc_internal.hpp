@@ -35,6 +35,7 @@ int cc_install_giant(gs_cc_t* h, const uint32_t* words);
 // the rank of a communicator
 int cc_merge_edges(gs_cc_t* h, gs_comm_t* c, int mode, const void* a, const void* b, uint64_t m);
 int cc_comm_rank(const gs_comm_t* c);
+int cc_agree_windows(gs_cc_t* h, gs_comm_t* c, uint64_t mine, uint64_t* most);
 // a pending exchange verification of the handle's last window (comm.hip): cc_settle runs it once
 void cc_set_settle(gs_cc_t* h, int (*fn)(void*), void* ctx);
 int cc_settle(gs_cc_t* h);

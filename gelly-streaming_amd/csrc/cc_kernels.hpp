@@ -444,7 +444,7 @@ struct HotArgs {
     uint32_t* wkeys = nullptr;                 // warm build: endpoint keys, 512 per wave step (count launches only)
     unsigned long long* wctl = nullptr;        // warm build: edges counted (written by count launches)
     uint64_t count_edges = 0;                  // count this launch's first edges (if !*warm_valid)
-    uint32_t clocks = 0;                       // GSGPU_RING_CLOCKS: record g_ring_phase (k_fold_ring)
+    uint32_t clocks = 0;                       // GSGPU_RING_CLOCKS: launch k_fold_ring's CLK instance
 };
 
 // ---- warm set (L2-resident second tier) ----
@@ -1036,18 +1036,19 @@ struct Raw4<int64_t> {
     }
 };
 
-// GSGPU_RING_CLOCKS only: per-workgroup clocks (wall_clock64) of the last k_fold_ring launch — entry,
-// hot set in LDS, every wave's main loop done, final flush done (report_fold_stats prints them)
+// GSGPU_RING_CLOCKS only (the CLK instance of k_fold_ring; production launches the one without):
+// per-workgroup clocks (wall_clock64) of the last k_fold_ring launch — entry, hot set in LDS, every
+// wave's main loop done, final flush done (report_ring_clocks prints them)
 constexpr uint32_t kRingPhaseGroups = 4096;
 __device__ unsigned long long g_ring_phase[kRingPhaseGroups][4];
 
-template <typename IdT, bool MARK, bool STATS>
+template <typename IdT, bool MARK, bool STATS, bool CLK = false>
 __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict__ a, const IdT* __restrict__ b,
                                                            FoldArgs f, HotArgs hot) {
     __shared__ __attribute__((aligned(16))) uint2 tab[kHotBuckets];
     __shared__ uint2 rings[kHotThreads / 64][kRingCap];
     const uint64_t n = f.n;
-    const bool clocks = hot.clocks && threadIdx.x == 0 && blockIdx.x < kRingPhaseGroups;
+    const bool clocks = CLK && threadIdx.x == 0 && blockIdx.x < kRingPhaseGroups;
     if (clocks) g_ring_phase[blockIdx.x][0] = wall_clock64();
     const bool filt = *f.giant != kInvalid;          // uniform
     if (!filt) f.sbits = nullptr;                    // the next close is a full pass (k_fold)
@@ -1133,12 +1134,12 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
         wave_round(g0);
     __shared__ uint32_t s_mcnt;
     __shared__ unsigned long long s_mbase;
-    if (hot.clocks) {                                // uniform
+    if (CLK) {
         __syncthreads();
         if (clocks) g_ring_phase[blockIdx.x][2] = wall_clock64();
     }
     ring_flush_final<MARK, STATS>(f, ring, cnt, st, gR, &s_mcnt, &s_mbase);
-    if (hot.clocks) {
+    if (CLK) {
         __syncthreads();
         if (clocks) g_ring_phase[blockIdx.x][3] = wall_clock64();
     }

@@ -106,6 +106,8 @@ struct gs_comm {
     uint64_t cap_pairs = 0;
     uint64_t pair_bytes = 0;                       // 8: dense (uint32 vertex, root); 16: sparse (int64 ids)
     uint32_t* sendbuf = nullptr;                   // cap_pairs pairs (2 x the handle's capacity)
+    uint64_t send_pairs = 0;                       // pairs each send buffer holds (count word included):
+                                                   // cap_pairs + 1, more for a prefilter sender's big slice
     uint32_t* sendbuf2 = nullptr;                  // allgather: exports alternate between the two, so a
                                                    // pending window's tail survives the next export
     uint32_t* recvbuf = nullptr;                   // exact rounds: grows to world * m pairs
@@ -286,8 +288,29 @@ int prepare(gs_comm_t* c, gs_cc_t* h, CcInfo* info, int mode) {
             return fail(GS_ERR_NOMEM, "exchange buffers of %llu pairs", (unsigned long long)need);
         }
         c->cap_pairs = need;
+        c->send_pairs = need + 1;
         c->pair_bytes = pbytes(*info);
     }
+    return GS_OK;
+}
+
+// GS_MERGE_PREFILTER sender: room for every edge of a slice of m edges to survive (a slice can be
+// larger than the 2 x capacity pairs the deltas are sized for). Nothing is pending here (the
+// window was settled before merge_prefilter), so the old buffers are free once the stream drains.
+int ensure_send(gs_comm_t* c, uint64_t m, hipStream_t s) {
+    if (m + 1 <= c->send_pairs) return GS_OK;
+    GS_HIP(hipStreamSynchronize(s));
+    if (c->sendbuf) (void)hipFree(c->sendbuf);
+    if (c->sendbuf2) (void)hipFree(c->sendbuf2);
+    c->sendbuf = c->sendbuf2 = nullptr;
+    c->pend_buf = nullptr;
+    c->send_pairs = 0;
+    const uint64_t want = std::max<uint64_t>(m + 1, c->cap_pairs + 1);
+    if (hipMalloc(&c->sendbuf, (size_t)want * 8) != hipSuccess || hipMalloc(&c->sendbuf2, (size_t)want * 8) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(GS_ERR_NOMEM, "prefilter send buffers of %llu pairs", (unsigned long long)want);
+    }
+    c->send_pairs = want;
     return GS_OK;
 }
 
@@ -571,7 +594,7 @@ int settle_gather(gs_comm_t* c, bool close) {
     GS_HIP(hipEventSynchronize(c->ev_counts));      // normally complete long ago
     if (c->rank != 0) {
         const uint64_t n = c->hcnt[P], S = c->pend_slot;
-        if (n > c->cap_pairs - 1) return fail(GS_ERR_CAPACITY, "delta of %llu pairs past the export buffer", (unsigned long long)n);
+        if (n > c->send_pairs - 1) return fail(GS_ERR_CAPACITY, "delta of %llu pairs past the export buffer", (unsigned long long)n);
         if (n > S) {
             ++c->overflows;
             GS_TRY(send(c, c->pend_buf + 2 + pwords(in) * S, (n - S) * pbytes(in), 0, s));
@@ -586,8 +609,9 @@ int settle_gather(gs_comm_t* c, bool close) {
     uint64_t total = 0, mx = 0, folded = 0;
     for (int q = 1; q < P; ++q) {
         const uint64_t n = c->hcnt[q];
-        if (n > c->cap_pairs - 1) return fail(GS_ERR_CAPACITY, "rank %d delta of %llu pairs past the export buffer", q,
-                                              (unsigned long long)n);
+        // (a prefilter sender's survivors are bounded by its slice, which its buffers hold)
+        if (c->mode != GS_MERGE_PREFILTER && n > c->cap_pairs - 1)
+            return fail(GS_ERR_CAPACITY, "rank %d delta of %llu pairs past the export buffer", q, (unsigned long long)n);
         tail[q] = n > c->gslot[q] ? n - c->gslot[q] : 0;
         folded += n - tail[q];
         total += tail[q];
@@ -715,8 +739,9 @@ int merge_prefilter(gs_comm_t* c, gs_cc_t* h, const CcInfo& in, const void* a, c
     const bool exact = win < kExactYoung || c->gslot.empty() || P > kMaxSlotCaps;
     if (c->gslot.empty()) c->gslot.assign(P, 0);
     if (c->rank != 0) {
+        GS_TRY(ensure_send(c, m, s));
         if (exact) {
-            GS_TRY(cc_filter_async(h, a, b, m, c->sendbuf + 2, c->cap_pairs - 1, reinterpret_cast<unsigned long long*>(c->sendbuf)));
+            GS_TRY(cc_filter_async(h, a, b, m, c->sendbuf + 2, c->send_pairs - 1, reinterpret_cast<unsigned long long*>(c->sendbuf)));
             GS_HIP(hipMemcpyAsync(c->hcnt + P, c->sendbuf, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
             GS_HIP(hipStreamSynchronize(s));
             const uint64_t n = c->hcnt[P];
@@ -730,7 +755,7 @@ int merge_prefilter(gs_comm_t* c, gs_cc_t* h, const CcInfo& in, const void* a, c
         } else {
             uint32_t* send_buf = (c->pend_buf == c->sendbuf) ? c->sendbuf2 : c->sendbuf;
             const uint64_t S = c->gslot[c->rank];
-            GS_TRY(cc_filter_async(h, a, b, m, send_buf + 2, c->cap_pairs - 1, reinterpret_cast<unsigned long long*>(send_buf)));
+            GS_TRY(cc_filter_async(h, a, b, m, send_buf + 2, c->send_pairs - 1, reinterpret_cast<unsigned long long*>(send_buf)));
             GS_TRY(send(c, send_buf, (2 + 2 * S) * 4, 0, s));
             GS_HIP(hipEventRecord(c->ev_slots, s));                 // the count word to the host, aside
             GS_HIP(hipStreamWaitEvent(c->side, c->ev_slots, 0));
@@ -760,9 +785,7 @@ int merge_prefilter(gs_comm_t* c, gs_cc_t* h, const CcInfo& in, const void* a, c
         std::vector<uint64_t> cnt(P, 0);
         uint64_t total = 0, mx = 0;
         for (int q = 1; q < P; ++q) {
-            cnt[q] = c->hcnt[q];
-            if (cnt[q] > c->cap_pairs - 1) return fail(GS_ERR_CAPACITY, "rank %d: %llu survivors past the exchange buffer", q,
-                                                       (unsigned long long)cnt[q]);
+            cnt[q] = c->hcnt[q];                 // (at most the sender's slice: its buffers hold it)
             total += cnt[q];
             mx = std::max(mx, cnt[q]);
             c->gslot[q] = next_slot(c, cnt[q]);
@@ -1027,6 +1050,34 @@ int merge_window(gs_cc_t* h, gs_comm_t* c, int mode, const void* a = nullptr, co
 extern "C++" {
 namespace gsgpu {
 int cc_comm_rank(const gs_comm_t* c) { return c ? c->rank : 0; }
+
+// GS_MERGE_PREFILTER (gs_cc_fold_windows): every window is an exchange with rank 0, so every rank
+// must run the same number of them. Each rank's slice of a short last global window may be empty,
+// a rank's whole slice may be empty: the ranks agree on the largest window count (one all-gather of
+// a word per call) and a rank past its own edges runs empty windows (a rank with n == 0
+// used to skip the exchange and leave its peers waiting in it).
+int cc_agree_windows(gs_cc_t* h, gs_comm_t* c, uint64_t mine, uint64_t* most) {
+    if (!c) return fail(GS_ERR_INVALID, "null communicator");
+    if (c->broken) return fail(GS_ERR_COMM, "the communicator failed in an earlier exchange");
+    CcInfo in;
+    GS_TRY(cc_info(h, &in));
+    GS_TRY(cc_settle(h));                            // (nothing is pending between calls: settled at their end)
+    DeviceGuard g(in.device);
+    const int P = c->world;
+    auto run = [&]() -> int {
+        c->hcnt[P] = mine;                           // (pinned: the copy reads it when it runs)
+        GS_HIP(hipMemcpyAsync(c->dcnt + P, c->hcnt + P, sizeof(unsigned long long), hipMemcpyHostToDevice, in.stream));
+        GS_TRY(allgather(c, c->dcnt + P, c->dcnt, sizeof(unsigned long long), in.stream));
+        GS_HIP(hipMemcpyAsync(c->hcnt, c->dcnt, P * sizeof(unsigned long long), hipMemcpyDeviceToHost, in.stream));
+        GS_HIP(hipStreamSynchronize(in.stream));
+        uint64_t mx = 0;
+        for (int q = 0; q < P; ++q) mx = std::max<uint64_t>(mx, c->hcnt[q]);
+        *most = mx;
+        return GS_OK;
+    };
+    const int rc = run();
+    return rc == GS_OK ? rc : abort_exchange(c, rc);
+}
 
 // gs_cc_fold_windows with GS_MERGE_PREFILTER: the window's own edges go to the exchange (rank 0
 // has folded them already; the other ranks filter them there)

@@ -10,8 +10,11 @@
 //                                                folded on the device); no timestamps in the file,
 //                                                so the merge window is cut by edge count (<merge ms>
 //                                                edges per window) and the print window by window
-//                                                count (<print ms> windows); any Long ids (a sparse-id
-//                                                summary of at most [capacity] distinct ids, 2^24)
+//                                                count (<print ms> windows: the emission of every
+//                                                <print ms>-th window is printed); any Long ids (a
+//                                                sparse-id summary of at most [capacity] distinct ids;
+//                                                default: file size / 2 — a valid line has at least 4
+//                                                bytes for its 2 ids — capped at 2^28)
 //
 // Output: like the reference's FlattenSet -> keyBy(vertex) -> timeWindow(print) -> fold(identity)
 // -> print (:61-67): at the end of every print window, one "(vertex,root)" line per vertex with
@@ -25,6 +28,7 @@
 #include <map>
 #include <sstream>
 #include <string>
+#include <sys/stat.h>
 
 #include "gsgpu.hpp"
 
@@ -36,13 +40,26 @@ int main(int argc, char** argv) {
     uint64_t window_edges = 0;
     if (argc > 1) {
         if (argc != 4 && argc != 5) {
-            std::cerr << "Usage: cc_example <input edges path> <merge window time (ms)> <print window time (ms)> [capacity]\n";
+            std::cerr << "Usage: cc_example <input edges path> <merge window time (ms)> <print window time (ms)> [capacity]\n"
+                         "  (file mode: <merge window time> edges per window; the emission of every <print window\n"
+                         "   time>-th window is printed; [capacity] distinct ids, default file size / 2, at most 2^28)\n";
             return 1;
         }
         merge_ms = std::atol(argv[2]);
         print_ms = std::atol(argv[3]);
         window_edges = merge_ms > 0 ? (uint64_t)merge_ms : 1;
-        const uint64_t cap = argc == 5 ? std::strtoull(argv[4], nullptr, 0) : (1ull << 24);
+        uint64_t cap = 0;
+        if (argc == 5) {
+            cap = std::strtoull(argv[4], nullptr, 0);
+        } else {                                     // distinct ids <= 2 per line <= bytes / 2
+            struct stat st;
+            if (::stat(argv[1], &st) != 0) {
+                std::cerr << "cannot stat " << argv[1] << "\n";
+                return 2;
+            }
+            cap = std::min<uint64_t>((uint64_t)st.st_size / 2 + 1, 1ull << 28);
+            cap = std::max<uint64_t>(cap, 1024);
+        }
         try {
             DisjointSet<int64_t> ds(cap, 0, GS_CC_SPARSE_IDS);
             ConnectedComponents<int64_t> cc(merge_ms, cap, 0, window_edges);

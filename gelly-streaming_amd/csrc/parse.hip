@@ -762,13 +762,14 @@ int fold_text_impl(gs_cc_t* h, TextSource& s, uint64_t W, uint64_t chunk, const 
     };
     uint64_t G = 0, windows = 0, line0 = 0;
     int rc = GS_OK;
-    bool more = !s.done();
-    if (more) GS_TRY(stage(0));
+    int stage_rc = GS_OK;                               // the next chunk could not be staged (a line
+    bool more = !s.done();                              // longer than a chunk, a read error): chunk i
+    if (more) GS_TRY(stage(0));                         // is still parsed and folded, then the call fails
     for (uint64_t i = 0; more; ++i) {
         const int k = (int)(i & 1);
         const bool last = ch[k].final || s.done();
-        if (!last) GS_TRY(stage(i + 1));                // read + copy + count of the next chunk meanwhile
-        more = !last;
+        if (!last) stage_rc = stage(i + 1);             // read + copy + count of the next chunk meanwhile
+        more = !last && stage_rc == GS_OK;
         if (!ch[k].len) continue;
         GS_HIP(hipEventSynchronize(g->counted[k]));
         const uint64_t lines = g->sc[k].hbuf[1] + ((char)g->sc[k].hbuf[2] != '\n');
@@ -800,6 +801,7 @@ int fold_text_impl(gs_cc_t* h, TextSource& s, uint64_t W, uint64_t chunk, const 
         if (frc != GS_OK) { rc = frc; break; }
         if (rc != GS_OK) break;
     }
+    if (rc == GS_OK && stage_rc != GS_OK) rc = stage_rc;   // every line before the failed chunk folded
     if (rc == GS_OK && G % W) {                         // the last, partial window
         GS_TRY(gs_cc_close_window(h));
         if (hook.fn) hook.fn(hook.ctx, windows);

@@ -271,10 +271,12 @@ int gs_parse_edges(const char* text, uint64_t n_bytes, uint32_t id_bits, void* s
  * h: either id width; GS_CC_SPARSE_IDS summaries take any Long id. *edges_out = edges folded; *windows_out =
  * windows closed. A line the reference rejects: GS_ERR_INVALID, every line before it folded (its
  * window left open), *edges_out = its 0-based line number. A line longer than chunk_bytes:
- * GS_ERR_CAPACITY. Enqueued on h's stream like gs_cc_fold_windows. on_window (may be NULL): called on
- * the calling thread after window w's close is enqueued (w counts from 0 per call): the Merger's
+ * GS_ERR_CAPACITY (a read error: GS_ERR_INVALID), every whole chunk before the one holding it
+ * folded (its window left open), *edges_out = the lines folded. Enqueued on h's stream like
+ * gs_cc_fold_windows. on_window (may be NULL): called on the calling thread after window w's close is enqueued (w counts from 0 per call): the Merger's
  * per-window emission hook (read it with gs_cc_emit_delta / _pairs / gs_cc_checksum there); with a
- * callback every window is folded and closed on its own (no run-ahead filter across windows). */
+ * callback every window is folded and closed by a call of its own (gs_cc_fold + gs_cc_close_window)
+ * instead of in gs_cc_fold_windows batches. */
 typedef void (*gs_window_fn)(void* ctx, uint64_t window);
 int gs_cc_fold_text(gs_cc_t* h, const char* text, uint64_t n_bytes, uint64_t window_edges, uint64_t chunk_bytes,
                     gs_window_fn on_window, void* ctx, uint64_t* edges_out, uint64_t* windows_out);

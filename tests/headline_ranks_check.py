@@ -65,11 +65,15 @@ def main():
     errors = []
     Wr = W // P
     pre = a.mode == "prefilter"
-    if pre:                                   # bench.py's prefilter layout (its default share for rank 0)
-        from bench import prefilter_share0
-        W1 = int(W * (1 - prefilter_share0(P)) / (P - 1)) // 4 * 4
-        W0 = W - (P - 1) * W1
-        sl = [(0, W0)] + [(W0 + (q - 1) * W1, W1) for q in range(1, P)]
+    if pre:                                   # bench.py's prefilter layout (its default share for rank 0:
+        import bench                          # none at P = 8, rank 0 then only merges)
+
+        class _L:
+            edge_factor, scale, window_log2, scaling, share0, merge = 16, a.scale, 24, "strong", None, "prefilter"
+        sl = []
+        for q in range(P):
+            lay = bench.layout(_L, P, q)      # (edges, slice, global window, windows, stream, offset)
+            sl.append((lay[5], lay[1]))
     else:
         sl = [(q * Wr, Wr) for q in range(P)]
 
@@ -80,7 +84,7 @@ def main():
             for w in range(N):
                 lo = w * W + off
                 if pre:
-                    ds.fold_windows(src[lo:lo + ln], dst[lo:lo + ln], ln, comm=comms[r], mode="prefilter")
+                    ds.fold_windows(src[lo:lo + ln], dst[lo:lo + ln], max(ln, 1), comm=comms[r], mode="prefilter")
                 else:
                     ds.fold(src[lo:lo + ln], dst[lo:lo + ln])
                     ds.merge_window(comms[r], a.mode)

@@ -1,6 +1,6 @@
 """bench.py's per-rank layouts (CPU): every global window is covered exactly once by the ranks'
 slices, in rank order, 4-edge aligned under --merge prefilter (rank 0's share from
-prefilter_share0), and the strong layout's even split otherwise."""
+prefilter_share0; none at all when that is 0: rank 0 then only merges), and the strong layout's even split otherwise."""
 import sys
 
 import pytest
@@ -22,7 +22,8 @@ def test_prefilter_slices_tile_every_window(world, share0):
     W = rows[0][2]
     off = 0
     for r, (E_rank, W_rank, W_glob, nwin, E, o) in enumerate(rows):
-        assert W_glob == W and o == off and W_rank > 0 and E_rank == nwin * W_rank
+        assert W_glob == W and o == off and E_rank == nwin * W_rank
+        assert W_rank > 0 or (r == 0 and (share0 == 0.0 or bench.prefilter_share0(world) == 0.0))
         assert r == 0 or W_rank % 4 == 0
         off += W_rank
     assert off == W
@@ -31,7 +32,7 @@ def test_prefilter_slices_tile_every_window(world, share0):
 def test_prefilter_share0_balances_rank0():
     assert bench.prefilter_share0(1) == 1.0
     assert 0.4 < bench.prefilter_share0(2) < 0.5
-    assert bench.prefilter_share0(8) == 0.0                 # rank 0 keeps the 4-edge minimum
+    assert bench.prefilter_share0(8) == 0.0                 # rank 0 folds no slice of its own
 
 
 @pytest.mark.parametrize("world", [1, 2, 4, 8])

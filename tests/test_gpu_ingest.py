@@ -60,7 +60,8 @@ def test_fold_text_windows_vs_oracle(oracle, torch_cuda, tmp_path, source, W, ch
     else:
         f = tmp_path / "edges.txt"
         f.write_bytes(text)
-        fold = lambda cb: ds.fold_file(str(f), W, chunk_bytes=chunk, on_window=cb)
+        from gsgpu.edgefile import fold_edge_file       # the example's file path (the streaming fold)
+        fold = lambda cb: fold_edge_file(ds, str(f), W, chunk_bytes=chunk, on_window=cb)
     edges, wins, sums = _run(ds, fold, W)
     assert edges == n and wins == len(want["checksums"]) == len(sums)
     assert sums == [int(x) for x in want["checksums"]]
@@ -120,6 +121,30 @@ def test_fold_text_bad_line_folds_everything_before_it(oracle, torch_cuda, where
     assert ei.value.edges == k and ei.value.windows == k // W
     ds.close_window()                                    # the open window's prefix was folded
     want = oracle.run(s[:k], d[:k], W, partitions=1, threads=1, emit=EMIT_CHECKSUM)
+    assert ds.checksum()[0] == int(want["checksums"][-1])
+
+
+@pytest.mark.parametrize("source", ["pageable", "file"])
+def test_fold_text_long_line_after_whole_chunks(oracle, torch_cuda, tmp_path, source):
+    """A line longer than a chunk, several chunks into the text: the next chunk cannot be staged,
+    every chunk before it is still parsed and folded (the call used to return before
+    folding the chunk already counted), the call fails with GS_ERR_CAPACITY and edges_out = the
+    lines before the long one."""
+    scale, n, W = 12, 3000, 500
+    s, d = oracle.gen_rmat(0, n, scale, 6)
+    text = _text(s, d, 2) + b"7 8" + b" " * 5000 + b"\n5 6\n"
+    ds = DisjointSet(1 << scale, id_bits=32, stream=torch_cuda.cuda.current_stream())
+    if source == "pageable":
+        fold = lambda: ds.fold_text(text, W, chunk_bytes=4096)
+    else:
+        path = tmp_path / "long.txt"
+        path.write_bytes(text)
+        fold = lambda: ds.fold_file(str(path), W, chunk_bytes=4096)
+    with pytest.raises(GsError) as ei:
+        fold()
+    assert ei.value.code == _abi.GS_ERR_CAPACITY
+    assert ei.value.edges == n and ei.value.windows == n // W
+    want = oracle.run(s, d, W, partitions=1, threads=1, emit=EMIT_CHECKSUM)
     assert ds.checksum()[0] == int(want["checksums"][-1])
 
 
