@@ -26,7 +26,10 @@
 #include <cstring>
 #include <vector>
 
+#include <hipcub/hipcub.hpp>
+
 #include "common.hpp"
+#include "bip_literal.hpp"
 
 namespace gsgpu {
 
@@ -253,6 +256,84 @@ __global__ __launch_bounds__(256) void k_bip_scatter(const uint32_t* __restrict_
     }
 }
 
+// ---- GS_BIP_REFERENCE_LITERAL: the literal Candidates engine (bip_literal.hpp) as one workgroup ----
+constexpr uint32_t kLitThreads = 256;
+
+// the engine's execution context on the device: the workgroup, LDS for the block scan
+struct LitX {
+    uint32_t* scan;                                   // LDS [kLitThreads]
+    __device__ uint32_t tid() const { return threadIdx.x; }
+    __device__ uint32_t nt() const { return blockDim.x; }
+    __device__ void sync() const { __syncthreads(); }
+    __device__ uint32_t atomic_add(uint32_t* p, uint32_t v) const { return atomicAdd(p, v); }
+    __device__ void atomic_min(uint32_t* p, uint32_t v) const { atomicMin(p, v); }
+    __device__ void atomic_or(uint32_t* p, uint32_t v) const { atomicOr(p, v); }
+    // exclusive prefix sum of v over the workgroup (Hillis-Steele in LDS), *total = the sum
+    __device__ uint32_t scan_excl(uint32_t v, uint32_t* total) const {
+        const uint32_t t = threadIdx.x, n = blockDim.x;
+        scan[t] = v;
+        __syncthreads();
+        for (uint32_t off = 1; off < n; off <<= 1) {
+            const uint32_t y = t >= off ? scan[t - off] : 0u;
+            __syncthreads();
+            scan[t] += y;
+            __syncthreads();
+        }
+        *total = scan[n - 1];
+        const uint32_t incl = scan[t];
+        __syncthreads();
+        return incl - v;
+    }
+};
+
+// updateFunction.foldEdges over a batch, edge after edge (the rule is sequential; each edge's work
+// is spread over the workgroup)
+template <typename IdT>
+__global__ __launch_bounds__(kLitThreads) void k_bipl_fold(lit::State S, const IdT* a, const IdT* b, uint64_t n, int aos) {
+    __shared__ lit::Shared sh;
+    __shared__ uint32_t scan[kLitThreads];
+    LitX x{scan};
+    lit::fold_edges(x, S, sh, a, b, n, aos != 0);
+}
+
+// into.merge(from) (Candidates.java:77-139)
+__global__ __launch_bounds__(kLitThreads) void k_bipl_merge(lit::State S, lit::State F) {
+    __shared__ lit::Shared sh;
+    __shared__ uint32_t scan[kLitThreads];
+    LitX x{scan};
+    lit::merge_summaries(x, S, sh, F);
+}
+
+// the live (component, vertex, sign) entries: sort keys vertex << 32 | key (emission order: by
+// vertex, then key) with their signs, and the emission checksum (bip.hip's formula, per entry)
+__global__ __launch_bounds__(256) void k_bipl_collect(lit::State S, uint32_t nodes, uint64_t* __restrict__ keys,
+                                                      uint8_t* __restrict__ signs, unsigned long long* __restrict__ acc) {
+    unsigned long long sum = 0;
+    for (uint32_t nd = blockIdx.x * blockDim.x + threadIdx.x; nd < nodes; nd += gridDim.x * blockDim.x) {
+        const uint32_t cs = S.node_cs[nd], c = lit::slot_of(cs);
+        if (!S.comp_alive[c]) continue;
+        const uint32_t v = S.node_v[nd], k = S.comp_key[c], sg = lit::sign_of(cs);
+        sum += pair_mix(v, ((uint64_t)k << 1) | sg);
+        if (keys) {
+            const unsigned long long at = atomicAdd(&acc[1], 1ull);
+            keys[at] = ((uint64_t)v << 32) | k;
+            signs[at] = (uint8_t)sg;
+        }
+    }
+    atomicAdd(&acc[0], sum);
+}
+
+template <typename IdT>
+__global__ __launch_bounds__(256) void k_bipl_split(const uint64_t* __restrict__ keys, const uint8_t* __restrict__ sg_in,
+                                                    uint64_t n, IdT* __restrict__ v, IdT* __restrict__ k,
+                                                    uint8_t* __restrict__ sg) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        v[i] = (IdT)(keys[i] >> 32);
+        k[i] = (IdT)(keys[i] & 0xFFFFFFFFu);
+        sg[i] = sg_in[i];
+    }
+}
+
 static unsigned bgrid(uint64_t items, uint64_t per, unsigned capb) {
     uint64_t b = (items + per - 1) / per;
     if (b == 0) b = 1;
@@ -263,9 +344,17 @@ static unsigned bgrid(uint64_t items, uint64_t per, unsigned capb) {
 
 using namespace gsgpu;
 
+// device state of a GS_BIP_REFERENCE_LITERAL summary (bip_literal.hpp), in one allocation
+struct LitDev {
+    void* mem = nullptr;
+    lit::State S{};
+    lit::Ctl* hctl = nullptr;                     // pinned mirror of S.ctl
+};
+
 struct gs_bip {
     uint32_t cap = 0, id_bits = 64;
     int device = 0;
+    LitDev* lit = nullptr;                     // GS_BIP_REFERENCE_LITERAL: the literal engine's state
     hipStream_t own = nullptr, stream = nullptr;
     uint32_t* w = nullptr;
     uint32_t* flags = nullptr;                 // [0] range error, [1] not bipartite
@@ -293,8 +382,29 @@ int bensure(void** p, size_t* have, size_t need) {
     return GS_OK;
 }
 
+// literal engine: its control words to the host, errors mapped to GS_ERR_* (the range flag is
+// cleared once reported, as the union-find's is)
+int lsync(gs_bip_t* h, int* bipartite) {
+    lit::Ctl* c = h->lit->hctl;
+    GS_HIP(hipMemcpyAsync(c, h->lit->S.ctl, sizeof(lit::Ctl), hipMemcpyDeviceToHost, h->stream));
+    GS_HIP(hipStreamSynchronize(h->stream));
+    if (bipartite) *bipartite = c->ok ? 1 : 0;
+    if (c->err & lit::kErrCapacity)
+        return fail(GS_ERR_CAPACITY, "reference-literal Candidates: entry capacity exhausted (%u nodes, %u components, %u "
+                    "arena slots; gs_bip_create_ex entry_capacity)", h->lit->S.E, h->lit->S.C, h->lit->S.A);
+    if (c->err & lit::kErrThrows)
+        return fail(GS_ERR_INVALID, "reference-literal Candidates: Candidates.merge would throw here (an empty mergeBy "
+                    "list, Candidates.java:156)");
+    if (c->skipped) {
+        GS_HIP(hipMemsetAsync(reinterpret_cast<char*>(h->lit->S.ctl) + offsetof(lit::Ctl, skipped), 0, sizeof(uint32_t), h->stream));
+        return fail(GS_ERR_RANGE, "a vertex id outside [0, %u) was folded; such edges were skipped", h->cap);
+    }
+    return GS_OK;
+}
+
 // reads the flags; GS_ERR_RANGE if an out-of-range id was folded since the last check
 int bsync(gs_bip_t* h, int* bipartite) {
+    if (h->lit) return lsync(h, bipartite);
     uint32_t* hf = reinterpret_cast<uint32_t*>(h->hscr + 6);
     GS_HIP(hipMemcpyAsync(hf, h->flags, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
     GS_HIP(hipStreamSynchronize(h->stream));
@@ -307,7 +417,7 @@ int bsync(gs_bip_t* h, int* bipartite) {
 }
 
 int bcompress(gs_bip_t* h) {
-    if (h->compressed) return GS_OK;
+    if (h->lit || h->compressed) return GS_OK;        // (the literal summary needs no compression)
     hipLaunchKernelGGL(k_bip_compress, dim3(bgrid(h->cap, 256, 16384)), dim3(256), 0, h->stream, h->w, h->cap);
     GS_HIP(hipGetLastError());
     h->compressed = true;
@@ -343,6 +453,15 @@ int bfold(gs_bip_t* h, const void* a, const void* b, uint64_t n, bool aos) {
     h->compressed = false;
     const size_t esz = h->id_bits / 8;
     auto launch = [&](const void* x, const void* y, uint64_t m) {
+        if (h->lit) {                                  // one workgroup, edge after edge
+            if (h->id_bits == 32)
+                hipLaunchKernelGGL(k_bipl_fold<uint32_t>, dim3(1), dim3(kLitThreads), 0, h->stream, h->lit->S,
+                                   (const uint32_t*)x, (const uint32_t*)y, m, aos ? 1 : 0);
+            else
+                hipLaunchKernelGGL(k_bipl_fold<int64_t>, dim3(1), dim3(kLitThreads), 0, h->stream, h->lit->S,
+                                   (const int64_t*)x, (const int64_t*)y, m, aos ? 1 : 0);
+            return;
+        }
         if (h->id_bits == 32) {
             if (aos) bfold_launch<uint32_t, true>(h, (const uint32_t*)x, nullptr, m);
             else bfold_launch<uint32_t, false>(h, (const uint32_t*)x, (const uint32_t*)y, m);
@@ -374,12 +493,72 @@ int bfold(gs_bip_t* h, const void* a, const void* b, uint64_t n, bool aos) {
     return GS_OK;
 }
 
+// literal summary: every live (vertex, key, sign) entry, ordered by vertex then key (a vertex may
+// belong to several components, see bip_literal.hpp); nothing when failed
+int lemit(gs_bip_t* h, void* vertices, void* keys, uint8_t* signs, uint64_t cap, uint64_t* n_out) {
+    int ok = 1;
+    GS_TRY(lsync(h, &ok));
+    const lit::Ctl c = *h->lit->hctl;
+    const uint64_t total = ok ? c.live_entries : 0;
+    *n_out = total;
+    const uint64_t wn = std::min<uint64_t>(total, cap);
+    if (wn) {
+        size_t sort_bytes = 0;
+        GS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                   (const uint8_t*)nullptr, (uint8_t*)nullptr, (int)total, 0, 64, h->stream));
+        const size_t kb = ((size_t)total * 8 + 255) & ~(size_t)255, sb = ((size_t)total + 255) & ~(size_t)255;
+        const size_t esz = h->id_bits / 8;
+        const size_t ob = ((size_t)wn * (2 * esz + 1) + 255) & ~(size_t)255;
+        GS_TRY(bensure(&h->tmp, &h->tmp_bytes, 256 + 2 * kb + 2 * sb + ob + sort_bytes));
+        char* base = static_cast<char*>(h->tmp);
+        auto* acc = reinterpret_cast<unsigned long long*>(base);
+        auto* ki = reinterpret_cast<uint64_t*>(base + 256);
+        auto* ko = reinterpret_cast<uint64_t*>(base + 256 + kb);
+        auto* si = reinterpret_cast<uint8_t*>(base + 256 + 2 * kb);
+        auto* so = reinterpret_cast<uint8_t*>(base + 256 + 2 * kb + sb);
+        char* out = base + 256 + 2 * kb + 2 * sb;
+        void* st = out + ob;
+        GS_HIP(hipMemsetAsync(acc, 0, 2 * sizeof(unsigned long long), h->stream));
+        hipLaunchKernelGGL(k_bipl_collect, dim3(bgrid(c.n_nodes, 256, 1024)), dim3(256), 0, h->stream, h->lit->S,
+                           c.n_nodes, ki, si, acc);
+        GS_HIP(hipGetLastError());
+        GS_HIP(hipcub::DeviceRadixSort::SortPairs(st, sort_bytes, (const uint64_t*)ki, ko, (const uint8_t*)si, so,
+                                                   (int)total, 0, 64, h->stream));
+        const bool dev = is_device_pointer(vertices) && is_device_pointer(keys) && is_device_pointer(signs);
+        void* vo = dev ? vertices : out;
+        void* kout = dev ? keys : out + wn * esz;
+        uint8_t* sg = dev ? signs : reinterpret_cast<uint8_t*>(out + 2 * wn * esz);
+        if (h->id_bits == 32)
+            hipLaunchKernelGGL(k_bipl_split<uint32_t>, dim3(bgrid(wn, 256, 1024)), dim3(256), 0, h->stream,
+                               (const uint64_t*)ko, (const uint8_t*)so, wn, (uint32_t*)vo, (uint32_t*)kout, sg);
+        else
+            hipLaunchKernelGGL(k_bipl_split<int64_t>, dim3(bgrid(wn, 256, 1024)), dim3(256), 0, h->stream,
+                               (const uint64_t*)ko, (const uint8_t*)so, wn, (int64_t*)vo, (int64_t*)kout, sg);
+        GS_HIP(hipGetLastError());
+        if (!dev) {
+            GS_HIP(hipMemcpyAsync(vertices, vo, wn * esz, hipMemcpyDeviceToHost, h->stream));
+            GS_HIP(hipMemcpyAsync(keys, kout, wn * esz, hipMemcpyDeviceToHost, h->stream));
+            GS_HIP(hipMemcpyAsync(signs, sg, wn, hipMemcpyDeviceToHost, h->stream));
+        }
+        GS_HIP(hipStreamSynchronize(h->stream));
+    }
+    if (total > cap) return fail(GS_ERR_CAPACITY, "gs_bip_emit_pairs: %llu entries, capacity %llu",
+                                 (unsigned long long)total, (unsigned long long)cap);
+    return GS_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 int gs_bip_create(gs_bip_t** out, uint64_t vertex_capacity, uint32_t id_bits, int device) {
+    return gs_bip_create_ex(out, vertex_capacity, id_bits, device, 0u, 0ull);
+}
+
+int gs_bip_create_ex(gs_bip_t** out, uint64_t vertex_capacity, uint32_t id_bits, int device, uint32_t flags,
+                     uint64_t entry_capacity) {
     if (!out) return fail(GS_ERR_INVALID, "gs_bip_create: null out");
+    if (flags & ~(uint32_t)GS_BIP_REFERENCE_LITERAL) return fail(GS_ERR_INVALID, "gs_bip_create_ex: unknown flags 0x%x", flags);
     *out = nullptr;
     if (id_bits != 32 && id_bits != 64) return fail(GS_ERR_INVALID, "gs_bip_create: id_bits must be 32 or 64");
     if (vertex_capacity == 0 || vertex_capacity > kBipMaxCap)
@@ -398,9 +577,56 @@ int gs_bip_create(gs_bip_t** out, uint64_t vertex_capacity, uint32_t id_bits, in
     auto bail = [&](int rc) { gs_bip_destroy(h); return rc; };
     if (hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking) != hipSuccess) return bail(fail(GS_ERR_HIP, "hipStreamCreate failed"));
     h->stream = h->own;
-    if (hipMalloc(&h->w, (size_t)h->cap * 4) != hipSuccess || hipMalloc(&h->flags, 16) != hipSuccess ||
-        hipMalloc(&h->dscr, 8 * sizeof(unsigned long long)) != hipSuccess ||
+    if (hipMalloc(&h->dscr, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc(&h->hscr, 8 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return bail(fail(GS_ERR_NOMEM, "gs_bip_create: scratch allocation failed"));
+    }
+    if (flags & GS_BIP_REFERENCE_LITERAL) {
+        // the literal engine: nodes E (component memberships ever made between resets), as many
+        // component slots, an arena of 4 E member slots (component arrays double as they grow)
+        const uint64_t E = entry_capacity ? entry_capacity : std::max<uint64_t>(16ull * h->cap, 4096);
+        if (E > 0x7FFFFFFFull / 4) return bail(fail(GS_ERR_INVALID, "gs_bip_create_ex: entry_capacity too large"));
+        h->lit = new LitDev();
+        lit::State& S = h->lit->S;
+        S.cap = h->cap;
+        S.E = (uint32_t)E;
+        S.C = (uint32_t)E;
+        S.A = (uint32_t)(4 * E);
+        const size_t cap = h->cap;
+        size_t off = 0;
+        auto take = [&](size_t bytes) { const size_t at = off; off += (bytes + 255) & ~(size_t)255; return at; };
+        const size_t o_vhead = take(cap * 4), o_kslot = take(cap * 4), o_sv = take(cap * 4), o_keys = take(cap * 4),
+                     o_ss = take(cap), o_ncs = take(E * 4), o_nv = take(E * 4), o_nn = take(E * 4),
+                     o_ck = take(E * 4), o_ca = take(E * 4), o_cb = take(E * 4), o_csz = take(E * 4), o_ccap = take(E * 4),
+                     o_cnt = take(E * 4), o_tch = take(E * 4), o_mw = take(E * 8), o_mws = take(E * 8),
+                     o_arena = take(4 * E * 4), o_ctl = take(sizeof(lit::Ctl));
+        if (hipMalloc(&h->lit->mem, off) != hipSuccess ||
+            hipHostMalloc(&h->lit->hctl, sizeof(lit::Ctl), hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            return bail(fail(GS_ERR_NOMEM, "gs_bip_create_ex: %zu bytes for the reference-literal summary", off));
+        }
+        char* m = static_cast<char*>(h->lit->mem);
+        S.vhead = (int32_t*)(m + o_vhead);
+        S.kslot = (int32_t*)(m + o_kslot);
+        S.sv = (uint32_t*)(m + o_sv);
+        S.keys = (uint32_t*)(m + o_keys);
+        S.ss = (uint8_t*)(m + o_ss);
+        S.node_cs = (uint32_t*)(m + o_ncs);
+        S.node_v = (uint32_t*)(m + o_nv);
+        S.node_next = (int32_t*)(m + o_nn);
+        S.comp_key = (uint32_t*)(m + o_ck);
+        S.comp_alive = (uint32_t*)(m + o_ca);
+        S.comp_base = (uint32_t*)(m + o_cb);
+        S.comp_size = (uint32_t*)(m + o_csz);
+        S.comp_cap = (uint32_t*)(m + o_ccap);
+        S.cnt = (uint32_t*)(m + o_cnt);
+        S.touched = (uint32_t*)(m + o_tch);
+        S.mw = (uint64_t*)(m + o_mw);
+        S.mws = (uint64_t*)(m + o_mws);
+        S.arena = (int32_t*)(m + o_arena);
+        S.ctl = (lit::Ctl*)(m + o_ctl);
+    } else if (hipMalloc(&h->w, (size_t)h->cap * 4) != hipSuccess || hipMalloc(&h->flags, 16) != hipSuccess) {
         (void)hipGetLastError();
         return bail(fail(GS_ERR_NOMEM, "gs_bip_create: allocation of %u words failed", h->cap));
     }
@@ -419,6 +645,11 @@ int gs_bip_destroy(gs_bip_t* h) {
     for (void* p : {(void*)h->w, (void*)h->flags, (void*)h->dscr, h->tmp, h->stage})
         if (p) (void)hipFree(p);
     if (h->hscr) (void)hipHostFree(h->hscr);
+    if (h->lit) {
+        if (h->lit->mem) (void)hipFree(h->lit->mem);
+        if (h->lit->hctl) (void)hipHostFree(h->lit->hctl);
+        delete h->lit;
+    }
     if (h->own) (void)hipStreamDestroy(h->own);
     delete h;
     return GS_OK;
@@ -427,6 +658,19 @@ int gs_bip_destroy(gs_bip_t* h) {
 int gs_bip_reset(gs_bip_t* h) {
     GS_TRY(bcheck(h));
     DeviceGuard g(h->device);
+    h->edges_since_reset = 0;
+    if (h->lit) {                                      // new Candidates(true): no component, f0 true
+        lit::State& S = h->lit->S;
+        GS_HIP(hipMemsetAsync(S.vhead, 0xFF, (size_t)S.cap * 4, h->stream));
+        GS_HIP(hipMemsetAsync(S.kslot, 0xFF, (size_t)S.cap * 4, h->stream));
+        GS_HIP(hipMemsetAsync(S.cnt, 0, (size_t)S.C * 4, h->stream));
+        lit::Ctl c{};
+        c.ok = 1;
+        *h->lit->hctl = c;                             // (pinned: the copy reads it when it runs)
+        GS_HIP(hipMemcpyAsync(S.ctl, h->lit->hctl, sizeof(c), hipMemcpyHostToDevice, h->stream));
+        GS_HIP(hipStreamSynchronize(h->stream));       // (the pinned word is reused by lsync)
+        return GS_OK;
+    }
     GS_HIP(hipMemsetAsync(h->w, 0xFF, (size_t)h->cap * 4, h->stream));
     GS_HIP(hipMemsetAsync(h->flags, 0, 16, h->stream));
     h->edges_since_reset = 0;
@@ -449,6 +693,8 @@ int gs_bip_merge(gs_bip_t* into, gs_bip_t* from) {
     if (into == from) return GS_OK;
     if (into->device != from->device) return fail(GS_ERR_UNSUPPORTED, "gs_bip_merge: summaries on different devices");
     if (from->cap > into->cap) return fail(GS_ERR_RANGE, "gs_bip_merge: source capacity %u exceeds target %u", from->cap, into->cap);
+    if ((into->lit == nullptr) != (from->lit == nullptr))
+        return fail(GS_ERR_UNSUPPORTED, "gs_bip_merge: a reference-literal and an intended-semantics summary do not mix");
     DeviceGuard g(into->device);
     hipEvent_t e = nullptr;
     if (from->stream != into->stream) {
@@ -457,8 +703,11 @@ int gs_bip_merge(gs_bip_t* into, gs_bip_t* from) {
         GS_HIP(hipStreamWaitEvent(into->stream, e, 0));
     }
     into->compressed = false;
-    hipLaunchKernelGGL(k_bip_merge, dim3(bgrid(from->cap, 256, 16384)), dim3(256), 0, into->stream,
-                       (const uint32_t*)from->w, from->cap, (const uint32_t*)from->flags, bargs(into));
+    if (into->lit)
+        hipLaunchKernelGGL(k_bipl_merge, dim3(1), dim3(kLitThreads), 0, into->stream, into->lit->S, from->lit->S);
+    else
+        hipLaunchKernelGGL(k_bip_merge, dim3(bgrid(from->cap, 256, 16384)), dim3(256), 0, into->stream,
+                           (const uint32_t*)from->w, from->cap, (const uint32_t*)from->flags, bargs(into));
     GS_HIP(hipGetLastError());
     if (e) {
         GS_HIP(hipEventRecord(e, into->stream));
@@ -479,9 +728,32 @@ int gs_bip_status(gs_bip_t* h, int* bipartite, uint64_t* n_vertices, uint64_t* n
     return gs_bip_checksum(h, &sum, bipartite, n_vertices, n_components);
 }
 
+// literal summary: (checksum over live entries, ok, entries, components); a failed summary is empty
+int lstats(gs_bip_t* h, uint64_t* checksum, int* bipartite, uint64_t* n_entries, uint64_t* n_components) {
+    int ok = 1;
+    GS_TRY(lsync(h, &ok));
+    const lit::Ctl c = *h->lit->hctl;
+    uint64_t sum = 0;
+    if (ok && c.n_nodes) {
+        GS_HIP(hipMemsetAsync(h->dscr, 0, 2 * sizeof(unsigned long long), h->stream));
+        hipLaunchKernelGGL(k_bipl_collect, dim3(bgrid(c.n_nodes, 256, 1024)), dim3(256), 0, h->stream, h->lit->S,
+                           c.n_nodes, (uint64_t*)nullptr, (uint8_t*)nullptr, h->dscr);
+        GS_HIP(hipGetLastError());
+        GS_HIP(hipMemcpyAsync(h->hscr, h->dscr, sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
+        GS_HIP(hipStreamSynchronize(h->stream));
+        sum = h->hscr[0];
+    }
+    if (bipartite) *bipartite = ok;
+    if (checksum) *checksum = ok ? sum : 0;
+    if (n_entries) *n_entries = ok ? c.live_entries : 0;
+    if (n_components) *n_components = ok ? c.live_comps : 0;
+    return GS_OK;
+}
+
 int gs_bip_checksum(gs_bip_t* h, uint64_t* checksum, int* bipartite, uint64_t* n_vertices, uint64_t* n_components) {
     GS_TRY(bcheck(h));
     DeviceGuard g(h->device);
+    if (h->lit) return lstats(h, checksum, bipartite, n_vertices, n_components);
     GS_TRY(bcompress(h));
     GS_HIP(hipMemsetAsync(h->dscr, 0, 3 * sizeof(unsigned long long), h->stream));
     hipLaunchKernelGGL(k_bip_stats, dim3(bgrid(h->cap, 256, 4096)), dim3(256), 0, h->stream, (const uint32_t*)h->w, h->cap, h->dscr);
@@ -501,6 +773,7 @@ int gs_bip_emit_pairs(gs_bip_t* h, void* vertices, void* keys, uint8_t* signs, u
     if (!n_out) return fail(GS_ERR_INVALID, "gs_bip_emit_pairs: null n_out");
     if (cap && (!vertices || !keys || !signs)) return fail(GS_ERR_INVALID, "gs_bip_emit_pairs: null output");
     DeviceGuard g(h->device);
+    if (h->lit) return lemit(h, vertices, keys, signs, cap, n_out);
     GS_TRY(bcompress(h));
     const uint32_t nt = (uint32_t)((h->cap + kBipTile - 1) / kBipTile);
     const size_t esz = h->id_bits / 8;

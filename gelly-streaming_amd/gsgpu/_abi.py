@@ -25,6 +25,7 @@ GS_ERR_COMM = -8
 
 GS_CC_TRACK_MARKS = 1
 GS_CC_SPARSE_IDS = 2
+GS_BIP_REFERENCE_LITERAL = 1
 
 GS_K_FOLD, GS_K_COMPRESS, GS_K_MERGE, GS_K_EXPORT, GS_K_RING = 0, 1, 2, 3, 4
 GS_MERGE_ALLGATHER, GS_MERGE_GATHER, GS_MERGE_TREE, GS_MERGE_PREFILTER = 0, 1, 2, 3
@@ -45,7 +46,7 @@ EXPORTED_SYMBOLS = (
     "gs_cc_fold_text", "gs_cc_fold_file",
     "gs_bip_create", "gs_bip_destroy", "gs_bip_reset", "gs_bip_set_stream", "gs_bip_sync", "gs_bip_fold",
     "gs_bip_fold_pairs", "gs_bip_merge", "gs_bip_close_window", "gs_bip_status", "gs_bip_checksum",
-    "gs_bip_emit_pairs",
+    "gs_bip_emit_pairs", "gs_bip_create_ex",
     "gs_comm_unique_id", "gs_comm_create", "gs_comm_create_local", "gs_comm_destroy", "gs_comm_info",
     "gs_cc_merge_window", "gs_cc_fold_windows",
     "gs_last_error", "gs_version",
@@ -145,6 +146,7 @@ def lib() -> ctypes.CDLL:
         "gs_cc_fold_text": [vp, vp, u64, u64, u64, ctypes.CFUNCTYPE(None, vp, u64), vp, P(u64), P(u64)],
         "gs_cc_fold_file": [vp, ctypes.c_char_p, u64, u64, ctypes.CFUNCTYPE(None, vp, u64), vp, P(u64), P(u64)],
         "gs_bip_create": [P(vp), u64, u32, i32],
+        "gs_bip_create_ex": [P(vp), u64, u32, i32, u32, u64],
         "gs_bip_destroy": [vp],
         "gs_bip_reset": [vp],
         "gs_bip_set_stream": [vp, vp],

@@ -6,6 +6,13 @@
 ``SimpleEdgeStream`` and yields the cumulative summary after every window, whose ``toString()``
 is the reference's emission format, e.g. ``(true,{1={1=(1,true), 2=(2,false)}})`` or
 ``(false,{})`` (BipartitenessCheckTest.java:45-48, :70-72).
+
+``Candidates(..., literal=True)`` / ``BipartitenessCheck(..., mode="literal")``: the reference's
+Candidates.merge rule as written (GS_BIP_REFERENCE_LITERAL, csrc/bip_literal.hpp), whose emissions
+differ from the intended semantics on multi-window and multi-partition streams (a vertex can sit
+in several components, keys can be signed false); the dataflow is then the reference's own (fresh
+partial per partition per window, combined in partition order, the Merger's
+``windowResult.merge(summary)``), since the literal rule depends on it.
 """
 from __future__ import annotations
 
@@ -24,11 +31,14 @@ U64 = ctypes.c_uint64
 class Candidates:
     """Candidates (summaries/Candidates.java:25-197) on the device; ids in [0, capacity)."""
 
-    def __init__(self, vertex_capacity: int, id_bits: int = 64, device: int = 0, stream=None):
+    def __init__(self, vertex_capacity: int, id_bits: int = 64, device: int = 0, stream=None,
+                 literal: bool = False, entry_capacity: int = 0):
         self.capacity = int(vertex_capacity)
         self.id_bits = int(id_bits)
+        self.literal = bool(literal)
         h = ctypes.c_void_p()
-        call("gs_bip_create", ctypes.byref(h), self.capacity, self.id_bits, int(device))
+        call("gs_bip_create_ex", ctypes.byref(h), self.capacity, self.id_bits, int(device),
+             _abi.GS_BIP_REFERENCE_LITERAL if literal else 0, int(entry_capacity))
         self._h = h
         if stream is not None:
             call("gs_bip_set_stream", self._h, _stream_ptr(stream))
@@ -88,7 +98,8 @@ class Candidates:
         return int(s.value), bool(ok.value), int(nv.value), int(nc.value)
 
     def pairs(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
-        """(vertices, keys, signs) of every vertex, ordered by vertex."""
+        """(vertices, keys, signs) of every vertex, ordered by vertex (literal summaries: every
+        (component, vertex) entry, ordered by vertex then key)."""
         nv = self.status()[1]
         dt = np.uint32 if self.id_bits == 32 else np.int64
         v = np.empty(max(nv, 1), dtype=dt)
@@ -129,6 +140,9 @@ class Candidates:
         its component signed the other way (a connected bipartite component of several vertices
         has one); a lone key gets its self-loop (edgeToCandidate(v, v) adds it). A failed snapshot
         is restored as failed (Candidates.fail(): empty map) by an odd cycle on ids 0..2."""
+        if self.literal:
+            raise _abi.GsError(_abi.GS_ERR_UNSUPPORTED, "Candidates.restore",
+                               "a reference-literal summary (overlapping components) is not rebuilt from a snapshot")
         self.reset()
         if not success:
             if self.capacity < 3:
@@ -185,12 +199,16 @@ class BipartitenessCheck:
     mode "fused" folds every window into the one cumulative summary (production: the check and
     its bipartition do not depend on the partitioning); mode "reference" folds P fresh partials
     per window, combines them with Candidates.merge in partition order and lets the Merger merge
-    the window result with the cumulative summary (SummaryAggregation.java:106-119)."""
+    the window result with the cumulative summary (SummaryAggregation.java:106-119); mode
+    "literal" runs that same dataflow on reference-literal summaries (Candidates.java:77-192 as
+    written: the reference's own emissions, multi-window quirks included)."""
 
     def __init__(self, mergeWindowTime: int, *, vertex_capacity: Optional[int] = None, id_bits: int = 64,
-                 device: int = 0, parallelism: int = 1, window_edges: Optional[int] = None, mode: str = "fused"):
-        if mode not in ("fused", "reference"):
-            raise ValueError("mode must be 'fused' or 'reference'")
+                 device: int = 0, parallelism: int = 1, window_edges: Optional[int] = None, mode: str = "fused",
+                 entry_capacity: int = 0):
+        if mode not in ("fused", "reference", "literal"):
+            raise ValueError("mode must be 'fused', 'reference' or 'literal'")
+        self.entry_capacity = int(entry_capacity)
         self.time_millis = int(mergeWindowTime)
         self.vertex_capacity = vertex_capacity
         self.id_bits = int(id_bits)
@@ -240,7 +258,9 @@ class BipartitenessCheck:
                 summary.close()
             return
         P = self.parallelism
-        pool: List[Candidates] = [Candidates(cap, self.id_bits, self.device) for _ in range(P + 1)]
+        lit = self.mode == "literal"
+        pool: List[Candidates] = [Candidates(cap, self.id_bits, self.device, literal=lit,
+                                             entry_capacity=self.entry_capacity) for _ in range(P + 1)]
         summary: Optional[Candidates] = None
         if self._restored is not None:                 # restoreState: the Merger resumes from it
             summary = pool[P]

@@ -295,9 +295,24 @@ int gs_cc_fold_file(gs_cc_t* h, const char* path, uint64_t window_edges, uint64_
  *   gs_bip_close_window        the Merger's per-window emission           (SummaryAggregation.java:106-119)
  *   gs_bip_status / _checksum  getSuccess() (Candidates.java:40-42), sizes, and
  *                              sum over v of splitmix64(v ^ splitmix64(((key << 1) | sign) ^ 0xD1B54A32D192ED03))
- *   gs_bip_emit_pairs          (vertex, key, sign) ordered by vertex      (Candidates.getMap(), :44-46) */
+ *   gs_bip_emit_pairs          (vertex, key, sign) ordered by vertex      (Candidates.getMap(), :44-46)
+ * GS_BIP_REFERENCE_LITERAL (gs_bip_create_ex): the reference's Candidates rule as written
+ * (Candidates.java:77-192) instead of its intended semantics, for callers that need the reference's
+ * emissions on multi-window / multi-partition streams: a merge writes an input component under
+ * min(input key, lowest overlapping key) and removes only the other overlapping components (so a
+ * vertex may sit in several components), drops the result of their inner merges (:130), keeps the
+ * receiving side's signs, and skips components with an equal vertex set. The rule is sequential:
+ * one workgroup applies it edge after edge (csrc/bip_literal.hpp), for parity, not throughput.
+ * State: at most entry_capacity component memberships made between resets (0: 16 x
+ * vertex_capacity; GS_ERR_CAPACITY past it). Such summaries merge only with each other;
+ * gs_bip_status / _checksum count (component, vertex) entries; gs_bip_emit_pairs writes every
+ * entry ordered by vertex, then key; close_window is a no-op; a place where the reference's
+ * merge would throw (an empty mergeBy list, :156) fails the call with GS_ERR_INVALID. */
 typedef struct gs_bip gs_bip_t;
+enum { GS_BIP_REFERENCE_LITERAL = 1 };
 int gs_bip_create(gs_bip_t** out, uint64_t vertex_capacity, uint32_t id_bits, int device);
+int gs_bip_create_ex(gs_bip_t** out, uint64_t vertex_capacity, uint32_t id_bits, int device, uint32_t flags,
+                     uint64_t entry_capacity);
 int gs_bip_destroy(gs_bip_t* h);
 int gs_bip_reset(gs_bip_t* h);
 int gs_bip_set_stream(gs_bip_t* h, void* hip_stream);

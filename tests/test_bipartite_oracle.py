@@ -127,3 +127,53 @@ def test_c_restatement_equals_intended_semantics(seed):
         assert ok == want[0]
         if ok:
             assert nvert == len(want[1]) and ncomp == len(set(want[1].values()))
+
+
+def _literal_streams(count: int):
+    """Random multi-window, multi-partition streams: bipartite ones (cross edges and self-loops),
+    random ones (odd cycles: failures), small id ranges (shared vertices across components)."""
+    for seed in range(count):
+        rng = np.random.default_rng(seed)
+        nv = int(rng.integers(5, 60))
+        n = int(rng.integers(1, 200))
+        if seed % 3 == 0:
+            col = rng.integers(0, 2, nv)
+            s, d = [], []
+            while len(s) < n:
+                a, b = (int(x) for x in rng.integers(0, nv, 2))
+                if col[a] != col[b] or a == b:
+                    s.append(a)
+                    d.append(b)
+        else:
+            s, d = rng.integers(0, nv, n).tolist(), rng.integers(0, nv, n).tolist()
+        yield seed, nv, np.array(s), np.array(d), int(rng.integers(0, 40)), int(rng.integers(1, 4))
+
+
+def test_literal_engine_on_the_host_equals_literal_oracle(tmp_path):
+    """csrc/bip_literal.hpp (the engine libgsgpu.so runs as one HIP workgroup) run serially on the
+    host under ASan/UBSan (tests/bipl_host_check.cpp) = oracle/bipartite.py literal_run, every
+    window's emission, on 240 random streams: windows of 0-39 edges, 1-3 partitions, failures,
+    components sharing vertices and keys signed false among them."""
+    import shutil
+    import subprocess
+    here = os.path.dirname(os.path.abspath(__file__))
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("no g++")
+    exe = str(tmp_path / "bipl_host")
+    subprocess.run([gxx, "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-I", os.path.join(here, "..", "gelly-streaming_amd", "csrc"), os.path.join(here, "bipl_host_check.cpp"),
+                    "-o", exe], check=True)
+    shared = false_key = failed = 0
+    for seed, nv, s, d, W, P in _literal_streams(240):
+        want = literal_run(s, d, W, partitions=P)
+        inp = "%d %d %d %d\n" % (nv, W, P, len(s)) + "".join("%d %d\n" % (a, b) for a, b in zip(s.tolist(), d.tolist()))
+        out = subprocess.run([exe], input=inp, capture_output=True, text=True, timeout=60)
+        assert out.returncode == 0, (seed, out.stderr[-2000:])
+        assert out.stdout.splitlines() == want, seed
+        failed += want[-1] == "(false,{})"
+        false_key += any("={%d=(%d,false)" % (k, k) in want[-1] for k in range(nv))
+        import re
+        ids = re.findall(r"(\d+)=\(\1,", want[-1])
+        shared += len(ids) != len(set(ids))
+    assert failed > 20 and shared > 10 and false_key > 5, (failed, shared, false_key)

@@ -146,3 +146,93 @@ def test_restore_with_key_signed_false():
     assert c.toString() == "(true,{1={1=(1,true), 2=(2,false), 3=(3,true), 5=(5,true)}})"
     c.fold(np.array([1]), np.array([3]))                     # same side: an odd cycle
     assert c.toString() == "(false,{})"
+
+
+# ---- GS_BIP_REFERENCE_LITERAL: the reference's Candidates rule as written (csrc/bip_literal.hpp) ----
+from bipartite import literal_run  # noqa: E402
+
+
+def _literal_emissions(s, d, W, P, id_bits=64, entry_capacity=0):
+    return [c.toString() for c in SimpleEdgeStream(np.asarray(s), np.asarray(d)).aggregate(
+        BipartitenessCheck(1000, window_edges=W, mode="literal", parallelism=P, id_bits=id_bits,
+                           entry_capacity=entry_capacity))]
+
+
+@pytest.mark.parametrize("which", ["bipartite", "non_bipartite"])
+def test_literal_reference_kats(which):
+    k = _kat()
+    e = np.array(k[which + "_edges"])
+    out = [c.toString() for c in SimpleEdgeStream(e[:, 0], e[:, 1]).aggregate(
+        BipartitenessCheck(k["merge_window_ms"], mode="literal", parallelism=1))]
+    assert out == k[which + "_expect"]
+
+
+def test_literal_split_branch_and_self_loops():
+    """The triangle the literal rule loses (Candidates.java:117-134) and self-loops (edgeToCandidate)."""
+    assert _literal_emissions([5, 3, 3], [7, 7, 5], 0, 1) == ["(true,{3={3=(3,true), 5=(5,false), 7=(7,false)}})"]
+    assert _literal_emissions([3, 1], [3, 2], 0, 1) == ["(true,{1={1=(1,true), 2=(2,false)}, 3={3=(3,true)}})"]
+
+
+def _random_literal_cases(count: int, base: int):
+    for seed in range(base, base + count):
+        rng = np.random.default_rng(seed)
+        nv = int(rng.integers(5, 80))
+        n = int(rng.integers(1, 260))
+        if seed % 3 == 0:                                       # bipartite: cross edges and self-loops
+            col = rng.integers(0, 2, nv)
+            s, d = [], []
+            while len(s) < n:
+                a, b = (int(x) for x in rng.integers(0, nv, 2))
+                if col[a] != col[b] or a == b:
+                    s.append(a)
+                    d.append(b)
+        else:                                                   # random: odd cycles
+            s, d = rng.integers(0, nv, n).tolist(), rng.integers(0, nv, n).tolist()
+        yield seed, np.array(s), np.array(d), int(rng.integers(0, 50)), int(rng.integers(1, 4))
+
+
+@pytest.mark.parametrize("id_bits", [32, 64])
+def test_literal_every_window_vs_literal_oracle(id_bits):
+    """Every window's emission on 40 random multi-window streams (windows of 0-49 edges, 1-3
+    partitions: fresh partials combined in partition order, the Merger's windowResult.merge(summary))
+    equals oracle/bipartite.py's literal_run — including components that share vertices, keys
+    signed false and the sticky failure."""
+    seen_shared = seen_false = 0
+    for seed, s, d, W, P in _random_literal_cases(40, 1000 + id_bits):
+        want = literal_run(s, d, W, partitions=P)
+        got = _literal_emissions(s, d, W, P, id_bits=id_bits)
+        assert got == want, (seed, W, P)
+        seen_false += want[-1] == "(false,{})"
+        seen_shared += any(w.count("=(%d," % v) > 1 for w in want for v in range(80))
+    assert seen_false > 5 and seen_shared > 3, (seen_false, seen_shared)
+
+
+@pytest.mark.parametrize("odd_at", [-1, 2100])
+def test_literal_larger_stream(odd_at):
+    """A 3000-edge bipartite stream (and one with an odd edge late) over 8 windows and 3 partitions."""
+    s, d = _bipartite_stream(400, 3000, seed=7 + odd_at, odd_at=odd_at)
+    want = literal_run(s, d, 375, partitions=3)
+    assert _literal_emissions(s, d, 375, 3) == want
+
+
+def test_literal_errors():
+    # entry capacity: 2 edges need 4 memberships; 3 fit no window
+    with pytest.raises(GsError) as ei:
+        _literal_emissions([1, 3], [2, 4], 0, 1, entry_capacity=3)
+    assert ei.value.code == _abi.GS_ERR_CAPACITY
+    # literal and intended summaries do not merge
+    a = Candidates(16, literal=True)
+    b = Candidates(16)
+    with pytest.raises(GsError) as ei:
+        a.merge(b)
+    assert ei.value.code == _abi.GS_ERR_UNSUPPORTED
+    # an id past the capacity: that edge is skipped and reported, the rest folded
+    a.fold(np.array([1, 40, 2]), np.array([2, 3, 5]))
+    with pytest.raises(GsError) as ei:
+        a.sync()
+    assert ei.value.code == _abi.GS_ERR_RANGE
+    assert a.toString() == "(true,{1={1=(1,true), 2=(2,false), 5=(5,true)}})"
+    with pytest.raises(GsError):
+        a.restore(*a.snapshot())                       # (not rebuilt from a snapshot)
+    a.close()
+    b.close()
