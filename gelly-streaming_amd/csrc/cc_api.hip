@@ -297,13 +297,6 @@ constexpr uint64_t kSmallFoldEdges = 1u << 18;
 constexpr uint32_t kTlogSlots = 4096;
 constexpr int kSmallEpt = 1;
 
-// young folds (no seen bits, no touch log): a fresh smaller root is marked after the hook by a
-// non-returning atomicMin instead of a returning init CAS before it (union_edge, lazy)
-constexpr bool kLazyLo = true;
-// k_fold_ring: the last kRingSkew/1024 of a launch's rounds go to the even-XCD workgroups only
-// (k_fold_ring's round assignment)
-constexpr uint32_t kRingSkew = 0;
-
 // ---- debug variables (read once per process; none is needed in production) ----
 //   GSGPU_FOLD_STATS=1       per-window fold counters on stderr (STATS kernel variants; same results)
 //   GSGPU_RING_CLOCKS=1      per-workgroup phase clocks of the window's last k_fold_ring launch on stderr
@@ -322,8 +315,6 @@ struct DebugEnv {
     uint64_t young_first_min = kYoungFirstMinWg;    // GSGPU_YOUNG_FIRST_MIN: workgroup floor of the first young launch
     bool list_close = true;                         // GSGPU_LIST_CLOSE=0: no list-mode closes (A/B)
     bool small_claim = true;                        // GSGPU_SMALL_CLAIM=0: small k_fold launches without claims (A/B)
-    bool lazy_lo = kLazyLo;                         // GSGPU_LAZY_LO=0|1: young folds' lazy smaller-root init (A/B)
-    uint32_t ring_skew = kRingSkew;                 // GSGPU_RING_SKEW=N: k_fold_ring's even-XCD tail, N/1024 (A/B)
     DebugEnv() {
         const char* e = getenv("GSGPU_FOLD_STATS");
         fold_stats = e && atoi(e) != 0;
@@ -346,10 +337,6 @@ struct DebugEnv {
         if (e && *e) list_close = atoi(e) != 0;
         e = getenv("GSGPU_SMALL_CLAIM");
         if (e && *e) small_claim = atoi(e) != 0;
-        e = getenv("GSGPU_LAZY_LO");
-        if (e && *e) lazy_lo = atoi(e) != 0;
-        e = getenv("GSGPU_RING_SKEW");
-        if (e && *e) ring_skew = (uint32_t)std::min(strtoul(e, nullptr, 0), 512ul);
 
     }
 };
@@ -413,7 +400,6 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
     } else {
         h->ilist_ok = false;
     }
-    f.lazy = dbg().lazy_lo ? 1u : 0u;                // (applies where the kernel keeps no seen bits)
     if (persist) {
         f.work = reinterpret_cast<unsigned long long*>(h->derr + kWorkWord);
         (void)hipMemsetAsync(f.work, 0, sizeof(unsigned long long), h->stream);
@@ -484,7 +470,6 @@ static HotArgs ring_hot_args(gs_cc_t* h, bool* build_out) {
     hot.wctl = h->wctl;
     hot.count_edges = build ? h->warm_sample : 0;
     hot.clocks = dbg().ring_clocks ? 1u : 0u;
-    hot.skew = dbg().ring_skew;
     *build_out = build;
     return hot;
 }

@@ -101,19 +101,11 @@ __device__ __forceinline__ void first_touch(uint32_t* __restrict__ sbits, NewV* 
     set_seen(sbits, x);
 }
 
-// lazy (f.lazy; folds that keep neither seen bits, a touch log nor hooked-root marks — the young
-// forest, and partial-summary folds, before a giant exists):
-// a fresh SMALLER root keeps its kInvalid word while the larger root is hooked below it. A word that
-// is not below its index is a root to every walk (find_root), and a CAS that claims the vertex from
-// kInvalid later hangs its whole tree, so the forest stays a forest; once the hook has landed a
-// non-returning atomicMin turns the word into lo (a no-op if lo was hooked meanwhile), so the close
-// after the launch sees it. That is one returning init CAS (a round trip) less per such union.
 template <bool MARK, bool STATS = false>
 __device__ __forceinline__ uint32_t union_edge(uint32_t* __restrict__ parent, uint32_t* __restrict__ sbits,
                                                uint32_t u, uint32_t v, uint32_t pu, uint32_t pv,
                                                FoldStats* st = nullptr, bool halve = true,
-                                               uint32_t* __restrict__ hbits = nullptr, NewV* nl = nullptr,
-                                               bool lazy = false) {
+                                               uint32_t* __restrict__ hbits = nullptr, NewV* nl = nullptr) {
     if (u == v) {                                   // union(u,u): makeSet only
         if (pu == kInvalid) {
             const uint32_t old = atomicCAS(&parent[u], kInvalid, u);
@@ -136,19 +128,11 @@ __device__ __forceinline__ uint32_t union_edge(uint32_t* __restrict__ parent, ui
     }
     uint32_t ru = fu ? u : find_root(parent, u, pu, halve);
     uint32_t rv = fv ? v : find_root(parent, v, pv, halve);
-    // (not with the hooked-root bitmap: a full pass after such a fold takes an unmarked parent for a
-    // root, and a lazy root hooked later from kInvalid — the fresh-hi path, unmarked — has children)
-    const bool lazy_ok = lazy && sbits == nullptr && nl == nullptr && hbits == nullptr;
-    uint32_t lazy_v = kInvalid;                     // a fresh smaller root left uninitialised (lazy)
     while (ru != rv) {
         const bool uhi = ru > rv;
         const uint32_t hi = uhi ? ru : rv, lo = uhi ? rv : ru;
         bool& hf = uhi ? fu : fv;                   // fresh flags follow their side
         bool& lf = uhi ? fv : fu;
-        if (lf && lazy_ok) {                        // hook first, mark lo after (above)
-            lf = false;
-            lazy_v = lo;
-        }
         if (lf) {                                   // the smaller root must exist first
             const uint32_t old = atomicCAS(&parent[lo], kInvalid, lo);
             lf = false;
@@ -163,8 +147,6 @@ __device__ __forceinline__ uint32_t union_edge(uint32_t* __restrict__ parent, ui
         const uint32_t expect = hf ? kInvalid : hi;
         const uint32_t old = atomicCAS(&parent[hi], expect, lo);
         if (old == expect) {                        // hooked: hi is no longer a root
-            if (lazy_v != kInvalid)
-                __hip_atomic_fetch_min(&parent[lazy_v], lazy_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (hf) first_touch(sbits, nl, hi);
             else if (hbits) set_mark(hbits, hi);    // (a fresh hi never had children: no mark)
             if (STATS) ++st->hooks;
@@ -179,8 +161,6 @@ __device__ __forceinline__ uint32_t union_edge(uint32_t* __restrict__ parent, ui
         const uint32_t r = find_root(parent, old, parent[old], halve);
         if (uhi) ru = r; else rv = r;
     }
-    if (lazy_v != kInvalid)                         // (joined meanwhile by another hook: mark anyway)
-        __hip_atomic_fetch_min(&parent[lazy_v], lazy_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return kInvalid;
 }
 
@@ -321,8 +301,6 @@ struct FoldArgs {
     // wave 0; in the kernel, tlog is the wave's own slot and tcnt its entry count in LDS
     uint32_t* tlog = nullptr;
     uint32_t* tcnt = nullptr;
-    uint32_t lazy = 0;           // young folds without seen bits: a fresh smaller root is not initialised
-                                 // before the hook (union_edge), one returning CAS less per such union
 };
 
 // A wave's first touches (t[k] != kInvalid) appended to its touch-log slot: ballots over the active
@@ -467,8 +445,6 @@ struct HotArgs {
     unsigned long long* wctl = nullptr;        // warm build: edges counted (written by count launches)
     uint64_t count_edges = 0;                  // count this launch's first edges (if !*warm_valid)
     uint32_t clocks = 0;                       // GSGPU_RING_CLOCKS: launch k_fold_ring's CLK instance
-    uint32_t skew = 0;                         // k_fold_ring: tail rounds for even XCDs only, in 1/1024 of the
-                                               // launch (see k_fold_ring's round assignment)
 };
 
 // ---- warm set (L2-resident second tier) ----
@@ -676,7 +652,7 @@ __device__ __forceinline__ void union_group(const FoldArgs& f, const uint32_t (&
         for (int k = 0; k < EPT; ++k)
             m[k] = ok[k] ? union_edge<MARK, STATS>(f.parent, f.sbits, u[k], v[k], pu[k], pv[k], &st,
                                                    f.halve == 1 || (f.halve > 1 && ((u[k] * 0x9E3779B1u) >> 29) == 0),
-                                                   f.hbits, nullptr, f.lazy != 0) : kInvalid;
+                                                   f.hbits) : kInvalid;
     }
     if (MARK) log_append<EPT>(f.mark, f.mark_len, m);
 }
@@ -1060,9 +1036,6 @@ struct Raw4<int64_t> {
     }
 };
 
-// the even-XCD tail needs whole pairs of workgroups (even and odd alternate over the XCDs)
-#define G_SKEW_OK(g) (((g) & 1u) == 0u)
-
 // GSGPU_RING_CLOCKS only (the CLK instance of k_fold_ring; production launches the one without):
 // per-workgroup clocks (wall_clock64) of the last k_fold_ring launch — entry, hot set in LDS, every
 // wave's main loop done, final flush done (report_ring_clocks prints them)
@@ -1101,6 +1074,7 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
     uint32_t cnt = 0;                                // wave-uniform ring fill
     FoldStats st;
     const uint64_t groups = n / 4;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint64_t nvalid = 0, nkept = 0;
     // one wave round: 64 groups of 4 edges from g0 — filter, then ring or union in place
     auto wave_round = [&](const uint64_t g0) {
@@ -1156,22 +1130,8 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
         cnt += wtot;
         if (cnt >= 64) ring_flush<MARK, STATS>(f, ring, cnt, cnt - 64, st, gR);
     };
-    // Round assignment (a round = 64 groups of 4 edges, one wave load): the first R - T rounds go
-    // round-robin over the grid (workgroup-major, as a grid-stride loop), the last T = R x skew / 1024
-    // only to the even-numbered workgroups. Workgroups are dispatched round-robin over the 8 XCDs,
-    // and the odd XCDs' workgroups ran a steady launch's main loop 8-9 us slower in every window
-    // (profiles/r05_ring_clocks.txt: 178-180 vs 186-189 us mean end): the tail moves that share of
-    // work to the even XCDs without any shared counter (a grab counter cost ~60 ns per serialised
-    // grab, profiles/r05_dyn_ab.txt)
-    const uint64_t R = (groups + 63) / 64;
-    const uint64_t T = (G_SKEW_OK(gridDim.x) && hot.skew) ? (R * hot.skew) >> 10 : 0;
-    const uint64_t wave_id = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t r = wave_id; r < R - T; r += nwaves) wave_round(r * 64);
-    if (T && (blockIdx.x & 1u) == 0) {
-        const uint64_t ew = (uint64_t)(blockIdx.x >> 1) * (blockDim.x >> 6) + (threadIdx.x >> 6);
-        for (uint64_t t = ew; t < T; t += nwaves / 2) wave_round((R - T + t) * 64);
-    }
+    for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < groups; g0 += stride)
+        wave_round(g0);
     __shared__ uint32_t s_mcnt;
     __shared__ unsigned long long s_mbase;
     if (CLK) {
