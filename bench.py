@@ -104,8 +104,8 @@ def parse():
                          "RCCL at P > 1 (the one-GPU rank model's best: DESIGN.md section 6), else allgather")
     ap.add_argument("--share0", type=float, default=None,
                     help="prefilter, strong layout: rank 0's share of every global window (default "
-                         "(1 + 1/8) / P - 1/8: P=2 0.44, P=4 0.16, P=8 0 = 4 edges); "
-                         "the other ranks split the rest evenly")
+                         "(1 + 1/8) / P - 1/8 below P = 4 (P=2 0.44), 0 from P = 4 on: rank 0 then only "
+                         "merges); the other ranks split the rest evenly")
     ap.add_argument("--no-fold-timing", action="store_true",
                     help="no HIP events on the timed region's fold launches (value only; the roofline "
                          "figures are then omitted)")
@@ -125,9 +125,14 @@ def prefilter_share0(world: int) -> float:
     """Rank 0's default share of a window under --merge prefilter: its per-window work beyond its
     own slice (the survivors' fold, the close, the launch gaps) costs about as much as filtering 1/8
     of a window (tools/sim_ranks.py prefilter, profiles/r05_prefilter_sim_*), so the slices balance
-    at W1 = (1 + 1/8) W / P for the filtering ranks and W0 = W1 - W / 8 for rank 0. Below 1/32 of a
-    window rank 0's own fold is mostly its launch (24 us for 2^18 edges at P = 8): it then folds no
-    slice of its own (the filtering ranks take the whole window, layout())."""
+    at W1 = (1 + 1/8) W / P for the filtering ranks and W0 = W1 - W / 8 for rank 0. From P = 4 on rank
+    0 folds no slice of its own (the filtering ranks take the whole window, layout()): with the
+    senders filtering while rank 0 folds the previous window (round 6), rank 0's own fold of a small
+    slice is mostly launch and latency (~38 us per 2^20 edges against the senders' ~14 us), and the
+    round-6 rank model at P = 4 gives 1.79x with no slice, 1.70 / 1.66 / 1.57x with 5 / 10 / 15.6 %
+    (profiles/r06_g_sim_p4_*.txt); at P = 2 the formula's 0.44 stays best (1.22x vs 1.16x at 0.35)."""
+    if world >= 4:
+        return 0.0
     s = max(0.0, (1.0 + 0.125) / world - 0.125)
     return s if s >= 1.0 / 32 else 0.0
 

@@ -292,6 +292,12 @@ constexpr uint32_t kYoungSplitDiv = 16;
 // at 4 edges per thread filled 64 workgroups). Config 5: 3.94 -> 5.09 G edges/s, per-window latency
 // p50 29.9 -> 23.5 us; at 2^20 edges per launch config 2 +3 %, config 4 -1.5 % (profiles/r03_small)
 constexpr uint64_t kSmallFoldEdges = 1u << 18;
+// Pair / survivor folds (AOS: the prefilter Merger's survivors, exported partial summaries) take one
+// edge per thread up to this many pairs: a mature window's survivors (0.2-3.5 M at the 8-rank
+// RMAT-26 layout) are latency chains (gbits lookups, walks, a CAS), and four per thread ran them
+// four deep. One-GPU rank model at P = 8: the Merger's survivor folds 5.26 -> 4.33 ms per step,
+// window 5's 300 -> 141 us, the model 2.01 -> 2.20x (profiles/r06_f_sim_p8_*.txt)
+constexpr uint64_t kSmallPairFold = 1ull << 22;
 // list-mode closes: one-edge-per-thread folds log their first touches into one touch-log slot per
 // wave, up to kTlogSlots slots per window (2^18 edges; beyond: the close is a bitmap or full one)
 constexpr uint32_t kTlogSlots = 4096;
@@ -362,7 +368,8 @@ static void launch_warm_build(gs_cc_t* h, hipEvent_t stop, hipStream_t s);
 
 template <typename IdT, bool AOS>
 void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool young = false) {
-    const int ept = young ? kYoungEpt : (n <= dbg().small_fold ? dbg().small_ept : kEdgesPerThread);
+    const uint64_t small = AOS ? std::max<uint64_t>(kSmallPairFold, dbg().small_fold) : dbg().small_fold;
+    const int ept = young ? kYoungEpt : (n <= small ? dbg().small_ept : kEdgesPerThread);
     const bool persist = young && h->cus > 0;
     // The first young launch after reset folds into an EMPTY forest: every hub's first hooks and
     // the giant root's repeated re-hooks collide there, so it keeps at most ~1/16 of its edges in

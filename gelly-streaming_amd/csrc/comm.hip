@@ -132,6 +132,16 @@ struct gs_comm {
     std::vector<uint64_t> gslot;                   // gather: every sender's speculative slot (empty: exact round next)
     uint64_t win = 0;                              // prefilter: windows since the stream's start (broadcast schedule)
     uint32_t* bword = nullptr;                     // prefilter: the broadcast giant slot words (device, 2)
+    // prefilter, asynchronous filter-state broadcasts (after the first kBcastSync closes): their own
+    // communicator (RCCL: split from the main one at bind; in-process: the same group) and stream
+    ncclComm_t nccl_side = nullptr;
+    hipStream_t bside = nullptr;
+    uint32_t* bstage = nullptr;                    // rank 0: a snapshot [gbits | 2 giant words]; senders: 2 slots
+    uint64_t bslot_words = 0;                      // 32-bit words per slot
+    hipEvent_t ev_bmain = nullptr;                 // senders: a slot is free (its install ran); rank 0: the
+                                                   // last broadcast has read the snapshot
+    hipEvent_t ev_brecv[2] = {nullptr, nullptr};   // senders: slot k has arrived; rank 0 ([0]): snapshot taken
+    int64_t bpend[2] = {-1, -1};                   // senders: the window whose state slot k holds (-1: none)
     uint64_t bytes_sent = 0, bytes_recv = 0, exchanges = 0, overflows = 0;
 };
 
@@ -218,10 +228,11 @@ int recv(gs_comm_t* c, void* p, size_t bytes, int peer, hipStream_t s) {
     return GS_OK;
 }
 
-// rank 0's buffer into every rank's buffer of the same address role, in place
-int bcast(gs_comm_t* c, void* buf, size_t bytes, hipStream_t s) {
+// rank 0's buffer into every rank's buffer of the same address role, in place (side: on the
+// prefilter's broadcast communicator; the in-process group serves both, its host barriers order them)
+int bcast(gs_comm_t* c, void* buf, size_t bytes, hipStream_t s, bool side = false) {
     if (c->nccl) {
-        GS_NCCL(ncclBroadcast(buf, buf, bytes, ncclUint8, 0, c->nccl, s));
+        GS_NCCL(ncclBroadcast(buf, buf, bytes, ncclUint8, 0, side ? c->nccl_side : c->nccl, s));
         return GS_OK;
     }
     LocalGroup& g = *c->local;
@@ -701,13 +712,98 @@ int merge_gather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
 // The first kExactYoung windows of a stream are exact rounds (counts to the host first): their
 // survivors are large (a padded speculative slot would move twice their bytes), and rank 0 folds
 // them in one call through the young fold. Then speculative slots sized from each sender's last
-// count, verified lazily (settle_gather), as the gather. After rank 0's close of each of the first
-// kBcastYoung windows, then of every kBcastEvery-th, the bitmap and the giant words are broadcast
-// (8 MiB at 2^26 ids; a staler bitmap only lets more edges survive).
+// count, verified lazily (settle_gather), as the gather. The bitmap and the giant words go out
+// after rank 0's closes on the schedule below. A rank may fold no slice of its own (n == 0): every
+// rank still runs every window's exchange (the window count is agreed per call, gs_cc_fold_windows).
 constexpr uint64_t kExactYoung = 16;
-constexpr uint64_t kBcastYoung = 4;                // the giant forms in the first windows
-constexpr uint64_t kBcastEvery = 16;               // 8 MiB at 2^26 ids: ~130 us at 64 GB/s
-bool bcast_due(uint64_t win) { return win < kBcastYoung || win % kBcastEvery == kBcastEvery - 1; }
+// Filter-state broadcasts (round 6). After each of the first kBcastSync closes the broadcast is on
+// the critical path, as before: the next window's filter waits for it (window 1 has no bitmap at
+// all, window 2 needs the giant window 1 formed). After that they are asynchronous: rank 0 snapshots
+// [gbits | giant words] right after the close and broadcasts the snapshot on a side stream over a
+// communicator of their own, while it folds the next windows; a sender receives into one of two
+// staging slots on its side stream and installs the state before its filter two windows later
+// (a staler bitmap only lets more edges survive: components only merge until reset). While the
+// giant grows (windows < kBcastAsyncYoung) every window's state goes out, then every
+// kBcastAsyncEvery-th (8 MiB at 2^26 ids, ~130 us of link time at 64 GB/s).
+constexpr uint64_t kBcastSync = 2;
+constexpr uint64_t kBcastAsyncYoung = 16;
+constexpr uint64_t kBcastAsyncEvery = 4;
+constexpr uint64_t kBcastLag = 2;                  // installed before the filter of window j + kBcastLag
+bool bcast_sync(uint64_t win) { return win < kBcastSync; }
+bool bcast_async(uint64_t win) {
+    return win >= kBcastSync && (win < kBcastAsyncYoung || win % kBcastAsyncEvery == kBcastAsyncEvery - 1);
+}
+
+// side stream, events and staging of the asynchronous broadcasts (first use)
+int bside_init(gs_comm_t* c, uint64_t slot_words) {
+    if (c->bside) return GS_OK;
+    if (hipStreamCreateWithFlags(&c->bside, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_bmain, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_brecv[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_brecv[1], hipEventDisableTiming) != hipSuccess ||
+        hipMalloc(&c->bstage, (size_t)slot_words * 4 * (c->rank == 0 ? 1 : 2)) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(GS_ERR_NOMEM, "prefilter broadcast staging");
+    }
+    c->bslot_words = slot_words;
+    c->bpend[0] = c->bpend[1] = -1;
+    return GS_OK;
+}
+
+// rank 0, after close(win): the snapshot and its broadcast, off the handle's stream
+int bcast_async_send(gs_comm_t* c, gs_cc_t* h, hipStream_t s) {
+    uint32_t *gb = nullptr, *words = nullptr;
+    uint64_t gbytes = 0;
+    GS_TRY(cc_filter_state(h, &gb, &gbytes, &words));
+    GS_TRY(bside_init(c, gbytes / 4 + 2));
+    // the snapshot is taken on the handle's stream, right after the close: a copy on the side stream
+    // could overlap the next close, and a giant switch there (the bitmap rebuilt for another
+    // component) would mix two components' bits (8 MiB at 2^26 ids: a few us). The previous
+    // broadcast must have read the buffer first.
+    GS_HIP(hipStreamWaitEvent(s, c->ev_bmain, 0));
+    GS_HIP(hipMemcpyAsync(c->bstage, gb, gbytes, hipMemcpyDeviceToDevice, s));
+    GS_HIP(hipMemcpyAsync(c->bstage + gbytes / 4, words, 2 * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    GS_HIP(hipEventRecord(c->ev_brecv[0], s));                  // the snapshot is complete
+    GS_HIP(hipStreamWaitEvent(c->bside, c->ev_brecv[0], 0));
+    GS_TRY(bcast(c, c->bstage, gbytes + 8, c->bside, true));
+    GS_HIP(hipEventRecord(c->ev_bmain, c->bside));              // the buffer may be rewritten after this
+    c->bytes_sent += (gbytes + 8) * (c->world - 1);
+    return GS_OK;
+}
+
+// sender, in the call of window win: receive the state rank 0 broadcasts after close(win) into a slot
+int bcast_async_recv(gs_comm_t* c, gs_cc_t* h, uint64_t win) {
+    uint32_t *gb = nullptr, *words = nullptr;
+    uint64_t gbytes = 0;
+    GS_TRY(cc_filter_state(h, &gb, &gbytes, &words));
+    GS_TRY(bside_init(c, gbytes / 4 + 2));
+    const int k = (int)(win & 1);
+    // (the slot's last install was recorded in ev_bmain, which the side stream waits for)
+    GS_HIP(hipStreamWaitEvent(c->bside, c->ev_bmain, 0));
+    GS_TRY(bcast(c, c->bstage + (size_t)k * c->bslot_words, gbytes + 8, c->bside, true));
+    GS_HIP(hipEventRecord(c->ev_brecv[k], c->bside));
+    c->bpend[k] = (int64_t)win;
+    c->bytes_recv += gbytes + 8;
+    return GS_OK;
+}
+
+// sender, before the filter of window win: install the state of window win - kBcastLag if it was sent
+int bcast_async_install(gs_comm_t* c, gs_cc_t* h, uint64_t win, hipStream_t s) {
+    if (win < kBcastLag) return GS_OK;
+    const uint64_t j = win - kBcastLag;
+    const int k = (int)(j & 1);
+    if (c->bpend[k] != (int64_t)j) return GS_OK;
+    uint32_t *gb = nullptr, *words = nullptr;
+    uint64_t gbytes = 0;
+    GS_TRY(cc_filter_state(h, &gb, &gbytes, &words));
+    const uint32_t* slot = c->bstage + (size_t)k * c->bslot_words;
+    GS_HIP(hipStreamWaitEvent(s, c->ev_brecv[k], 0));
+    GS_HIP(hipMemcpyAsync(gb, slot, gbytes, hipMemcpyDeviceToDevice, s));
+    GS_TRY(cc_install_giant(h, slot + gbytes / 4));
+    GS_HIP(hipEventRecord(c->ev_bmain, s));                      // slot k free for the next receive
+    c->bpend[k] = -1;
+    return GS_OK;
+}
 
 int bcast_filter_state(gs_comm_t* c, gs_cc_t* h, hipStream_t s) {
     uint32_t *gb = nullptr, *words = nullptr;
@@ -740,6 +836,7 @@ int merge_prefilter(gs_comm_t* c, gs_cc_t* h, const CcInfo& in, const void* a, c
     if (c->gslot.empty()) c->gslot.assign(P, 0);
     if (c->rank != 0) {
         GS_TRY(ensure_send(c, m, s));
+        GS_TRY(bcast_async_install(c, h, win, s));
         if (exact) {
             GS_TRY(cc_filter_async(h, a, b, m, c->sendbuf + 2, c->send_pairs - 1, reinterpret_cast<unsigned long long*>(c->sendbuf)));
             GS_HIP(hipMemcpyAsync(c->hcnt + P, c->sendbuf, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
@@ -767,7 +864,8 @@ int merge_prefilter(gs_comm_t* c, gs_cc_t* h, const CcInfo& in, const void* a, c
             c->pend_buf = send_buf;
             cc_set_settle(h, settle_cb, c);
         }
-        if (bcast_due(win)) GS_TRY(bcast_filter_state(c, h, s));
+        if (bcast_sync(win)) GS_TRY(bcast_filter_state(c, h, s));
+        if (bcast_async(win)) GS_TRY(bcast_async_recv(c, h, win));
         return GS_OK;
     }
     if (!c->root_marking_off) {                    // the Merger never exports
@@ -830,7 +928,8 @@ int merge_prefilter(gs_comm_t* c, gs_cc_t* h, const CcInfo& in, const void* a, c
         c->pending = true;
         cc_set_settle(h, settle_cb, c);
     }
-    if (bcast_due(win)) GS_TRY(bcast_filter_state(c, h, s));
+    if (bcast_sync(win)) GS_TRY(bcast_filter_state(c, h, s));
+    if (bcast_async(win)) GS_TRY(bcast_async_send(c, h, s));
     return GS_OK;
 }
 
@@ -954,7 +1053,13 @@ int gs_comm_destroy(gs_comm_t* c) {
         if (!c->broken) (void)settle_cb(c);
     }
     (void)hipDeviceSynchronize();
+    if (c->nccl_side) (void)ncclCommDestroy(c->nccl_side);
     if (c->nccl) (void)ncclCommDestroy(c->nccl);
+    if (c->bside) (void)hipStreamDestroy(c->bside);
+    if (c->ev_bmain) (void)hipEventDestroy(c->ev_bmain);
+    for (hipEvent_t e : c->ev_brecv)
+        if (e) (void)hipEventDestroy(e);
+    if (c->bstage) (void)hipFree(c->bstage);
     if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->ev_counts) (void)hipEventDestroy(c->ev_counts);
@@ -991,6 +1096,10 @@ namespace {
 int abort_exchange(gs_comm_t* c, int rc) {
     const std::string msg = last_error();
     c->broken = true;
+    if (c->nccl_side) {
+        (void)ncclCommAbort(c->nccl_side);
+        c->nccl_side = nullptr;
+    }
     if (c->nccl) {
         (void)ncclCommAbort(c->nccl);
         c->nccl = nullptr;
@@ -1026,6 +1135,8 @@ int merge_window(gs_cc_t* h, gs_comm_t* c, int mode, const void* a = nullptr, co
                             "buffers, rank %d's %llu / %llu: every rank needs the same vertex capacity and id mode",
                             q, c->hcnt[q] >> 8, c->hcnt[q] & 0xFF, c->rank, (unsigned long long)c->cap_pairs,
                             (unsigned long long)c->pair_bytes);
+        if (mode == GS_MERGE_PREFILTER && c->nccl && !c->nccl_side)   // (collective: every rank binds here)
+            GS_NCCL(ncclCommSplit(c->nccl, 0, c->rank, &c->nccl_side, nullptr));
         c->bound = h;
         c->mode = mode;
         c->reset_gen = in.reset_gen;
@@ -1036,6 +1147,7 @@ int merge_window(gs_cc_t* h, gs_comm_t* c, int mode, const void* a = nullptr, co
         c->spec_slot = 0;                            // its first window runs the exact round again
         c->gslot.clear();
         c->win = 0;
+        c->bpend[0] = c->bpend[1] = -1;              // (broadcasts in flight land, unused)
     }
     DeviceGuard g(in.device);
     switch (mode) {

@@ -67,6 +67,27 @@ def _cuda_tensors(objs):
     return [o for o in objs if _is_torch(o) and o.is_cuda]
 
 
+_MODES = {"allgather": _abi.GS_MERGE_ALLGATHER, "gather": _abi.GS_MERGE_GATHER, "tree": _abi.GS_MERGE_TREE,
+          "prefilter": _abi.GS_MERGE_PREFILTER}
+
+
+def _first_cuda_tensor(objs):
+    for o in objs:
+        if _is_torch(o) and o.is_cuda:
+            return o
+    return None
+
+
+def _current_raw_stream(t) -> int:
+    """torch's current stream on t's device as a raw pointer (torch.cuda.current_stream builds a
+    Stream object per call: a few us, the order of a small window's GPU time)."""
+    import torch
+    f = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    if f is not None:
+        return int(f(t.device.index if t.device.index is not None else torch.cuda.current_device()))
+    return int(torch.cuda.current_stream(t.device).cuda_stream)
+
+
 class DisjointSet:
     """GPU union-find summary (DisjointSet<K>), K = int32 or int64 vertex ids in [0, capacity);
     ``sparse=True`` (64-bit ids only): ANY Java long ids, at most ``vertex_capacity`` distinct."""
@@ -112,42 +133,49 @@ class DisjointSet:
 
     def set_stream(self, stream) -> None:
         call("gs_cc_set_stream", self.handle, _stream_ptr(stream))
+        self._hs = None                             # re-read by _stream()
 
     def _stream(self) -> int:
-        s = ctypes.c_void_p()
-        call("gs_cc_get_stream", self.handle, ctypes.byref(s))
-        return int(s.value or 0)
+        """The handle's HIP stream (cached: it changes only through set_stream)."""
+        hs = getattr(self, "_hs", None)
+        if hs is None:
+            s = ctypes.c_void_p()
+            call("gs_cc_get_stream", self.handle, ctypes.byref(s))
+            hs = self._hs = int(s.value or 0)
+        return hs
 
     def _after_torch(self, *objs) -> None:
         """Device tensors a call reads were produced in torch's stream order: the handle's stream
         waits for torch's current stream first (an event, no host wait). Without it a handle on
         its own stream could read a tensor torch is still writing (e.g. the torch.stack of a
         fold_pairs input; round 4's list-close diagnostic failed that way)."""
-        ts = _cuda_tensors(objs)
-        if not ts:
+        # (per-call host cost matters: config 5 calls this once per 2^16-edge window, ~25 us of work;
+        # the handle's stream is cached and torch's current stream read raw, round 6)
+        t = _first_cuda_tensor(objs)
+        if t is None:
+            return
+        hs = self._stream()
+        if hs == 0 or hs == _current_raw_stream(t):  # same stream (or the null stream: ordered anyway)
             return
         import torch
-        cur = torch.cuda.current_stream(ts[0].device)
-        hs = self._stream()
-        if hs == 0 or hs == cur.cuda_stream:         # same stream (or the null stream: ordered anyway)
-            return
+        cur = torch.cuda.current_stream(t.device)
         ev = torch.cuda.Event()
         ev.record(cur)
-        torch.cuda.ExternalStream(hs, device=ts[0].device).wait_event(ev)
+        torch.cuda.ExternalStream(hs, device=t.device).wait_event(ev)
 
     def _torch_after(self, *objs) -> None:
         """The reverse: torch's current stream waits for what this handle enqueued into device
         tensors without a host wait (async exports)."""
-        ts = _cuda_tensors(objs)
-        if not ts:
+        t = _first_cuda_tensor(objs)
+        if t is None:
+            return
+        hs = self._stream()
+        if hs == 0 or hs == _current_raw_stream(t):
             return
         import torch
-        cur = torch.cuda.current_stream(ts[0].device)
-        hs = self._stream()
-        if hs == 0 or hs == cur.cuda_stream:
-            return
+        cur = torch.cuda.current_stream(t.device)
         ev = torch.cuda.Event()
-        ev.record(torch.cuda.ExternalStream(hs, device=ts[0].device))
+        ev.record(torch.cuda.ExternalStream(hs, device=t.device))
         cur.wait_event(ev)
 
     def sync(self) -> None:
@@ -246,7 +274,6 @@ class DisjointSet:
     def fold_windows(self, src, dst, window_edges: int, comm=None, mode: str = "allgather") -> int:
         """A batch of count windows in one call (gs_cc_fold_windows): fold each window of
         ``window_edges`` edges, then close it (or merge it over ``comm``). Returns the windows."""
-        from .comm import MODES
         ps, ks, n = _buf(src, self.id_bits, "src")
         pd, kd, m = _buf(dst, self.id_bits, "dst")
         if n != m:
@@ -254,7 +281,7 @@ class DisjointSet:
         w = U64()
         self._after_torch(ks, kd)
         call("gs_cc_fold_windows", self.handle, comm.handle if comm is not None else None,
-             MODES[mode], ps, pd, n, int(window_edges), ctypes.byref(w))
+             _MODES[mode], ps, pd, n, int(window_edges), ctypes.byref(w))
         return int(w.value)
 
     def fold_text(self, text, window_edges: int, chunk_bytes: int = 0, on_window=None) -> Tuple[int, int]:

@@ -4,7 +4,7 @@ step is timed with HIP events. Measures what a multi-GPU run cannot show from a 
 payload (pairs) each exchange moves per window and the merge folds on the receiving ranks; the
 xGMI transfer time is modelled as bytes / 150 GB/s per link.
 
-usage (GPU box): python tools/sim_ranks.py P windows [scheme ...]   schemes: gather tree allgather prefilter
+usage (GPU box): python tools/sim_ranks.py P windows [scheme ...]   schemes: gather tree allgather prefilter prefilter_r05 prefilter_forest
 (allgather: every rank keeps the global summary; per window each rank's delta goes to every other
 rank over its own link and every rank folds the others' deltas with marking paused)
 """
@@ -78,78 +78,232 @@ def one_gpu_base(P, NW):
     return base
 
 
-def sim_prefilter(P, NW):
-    """GS_MERGE_PREFILTER: the global window (P x the per-rank W) split into rank 0's share
-    (SIM_SHARE0) and P - 1 equal sender slices. Rank 0 folds its share; each sender slice is
-    filtered (gs_cc_filter_edges, against rank 0's own current filter state: the broadcast is not
-    stale here, so survivors are a lower bound) and its survivors folded by rank 0; rank 0 closes.
-    Per window: with a broadcast due (each of the first 4 windows, then every 16th: 8 MiB at
-    BCAST_BW) the chain is serial — sender filters, transfer, rank 0's survivor fold + close, the
-    broadcast; otherwise senders (filtering window w + 1) and rank 0 (its fold, the survivors and
-    the close of window w) overlap and the window costs the longer of the two."""
+def _bench_layout(P):
+    """bench.py's per-rank slices of a global window under --merge prefilter (strong layout)."""
+    import importlib
+    sys.argv = sys.argv[:1]
+    sys.path.insert(0, ROOT)
+    bench = importlib.import_module("bench")
+
+    class _L:
+        edge_factor, scale, window_log2, scaling, share0, merge = 16, 26, 0, "strong", None, "prefilter"
+    _L.scale = scale
+    if os.environ.get("SIM_SHARE0"):                  # (bench.py --share0)
+        _L.share0 = float(os.environ["SIM_SHARE0"])
+    _L.window_log2 = (W * P).bit_length() - 1
+    return [bench.layout(_L, P, r)[1] for r in range(P)]
+
+
+# the round-6 broadcast schedule (csrc/comm.hip merge_prefilter): synchronous after the first
+# kBcastSync closes, then asynchronous (installed by the senders kBcastLag windows later) after every
+# close while w < 16, then after every 4th
+SYNC, LAG = 2, 2
+
+
+def bcast_async(w):
+    return w >= SYNC and (w < 16 or w % 4 == 3)
+
+
+def sim_prefilter(P, NW, r05=False):
+    """GS_MERGE_PREFILTER, the round-6 protocol (r05=True: round 5's accounting, kept for the record).
+    The global window (P x the per-rank W) is split as bench.py splits it (rank 0 no slice at P = 8).
+    Each sender slice is filtered against the Merger's giant state AS THE SENDER HAS IT — the state
+    after the last close whose broadcast it has installed (a second summary replays the Merger's
+    folds and closes that many windows behind, so the survivors include the stale bitmap's extra
+    edges) — and rank 0 folds every survivor and closes. Per window: the senders' filters run while
+    rank 0 folds and closes the previous window (the senders' send of window w waits for rank 0's
+    receive, posted after its close of w - 1), so a window costs the longer of the two chains; a
+    synchronous broadcast (after closes 0 and 1) serialises them. Asynchronous broadcasts cost rank 0
+    a snapshot copy (8 MiB) and the senders an install copy, on their chains."""
     s0 = max(0.0, 1.125 / P - 0.125)                                                   # bench.py prefilter_share0
-    share0 = float(os.environ.get("SIM_SHARE0", str(s0 if s0 >= 1.0 / 32 else 0.0)))
     BCAST_BW = 64e9
+    COPY_BW = 4.0e12                                  # D2D copy (read + write), snapshot / install
     base = one_gpu_base(P, NW)
     Wg = W * P
-    W0 = max(4, int(Wg * share0) // 4 * 4)
-    W1 = (Wg - W0) // (P - 1) // 4 * 4
-    W0 = Wg - W1 * (P - 1)
+    if r05:
+        share0 = float(os.environ.get("SIM_SHARE0", str(s0 if s0 >= 1.0 / 32 else 0.0)))
+        W0 = max(4, int(Wg * share0) // 4 * 4)
+        W1 = (Wg - W0) // (P - 1) // 4 * 4
+        W0 = Wg - W1 * (P - 1)
+        sizes = [W0] + [W1] * (P - 1)
+    else:
+        sizes = _bench_layout(P)
+    W0 = sizes[0]
     m0 = gsgpu.DisjointSet(V, id_bits=32, stream=torch.cuda.current_stream())
-    ss = torch.empty(max(W0, W1), dtype=torch.int32, device="cuda")
-    sd = torch.empty(max(W0, W1), dtype=torch.int32, device="cuda")
-    outs = [torch.empty(2 * W1, dtype=torch.int32, device="cuda") for _ in range(P - 1)]
+    lag = None if r05 else gsgpu.DisjointSet(V, id_bits=32, stream=torch.cuda.current_stream())
+    mx = max(sizes)
+    ss = torch.empty(mx, dtype=torch.int32, device="cuda")
+    sd = torch.empty(mx, dtype=torch.int32, device="cuda")
+    outs = [torch.empty(2 * sizes[r], dtype=torch.int32, device="cuda") for r in range(1, P)]
     gbytes = V // 8
-    m0.timing(True)                                   # kernel time of every launch (HIP events)
+    m0.timing(True)
+    if lag is not None:
+        lag.timing(True)
 
-    def ktime():
-        return sum(m0.kernel_time(k)[0] for k in range(6)) * 1e3        # us, cumulative
+    def ktime(h):
+        return sum(h.kernel_time(k)[0] for k in range(6)) * 1e3        # us, cumulative
 
-    def ktimed(fn):                                   # (result, kernel-only us of the launches fn made)
-        k0 = ktime()
+    def ktimed(h, fn):                                # (result, kernel-only us of the launches fn made)
+        k0 = ktime(h)
         r = fn()
         torch.cuda.synchronize()
-        return r, ktime() - k0
-    kt = dict(crit=0.0)
-    print("== prefilter P=%d scale=%d global window 2^%d: rank 0 %d edges, senders %d each" %
-          (P, scale, Wg.bit_length() - 1, W0, W1), flush=True)
+        return r, ktime(h) - k0
+    print("== prefilter%s P=%d scale=%d global window 2^%d: rank 0 %d edges, senders %s each" %
+          ("_r05" if r05 else "", P, scale, Wg.bit_length() - 1, W0, sorted(set(sizes[1:]))), flush=True)
     tot = dict(crit=0.0, filt=0.0, merge=0.0, close=0.0, own=0.0, surv=0)
+    history = []                                      # per window: (own slice, all survivors) as folded by rank 0
+    lag_at = -1                                       # lag summary = the Merger after close(lag_at)
+    prev_r0 = 0.0                                     # rank 0's chain of the previous window (overlaps this filter)
     for w in range(NW):
-        gen.rmat(ss[:W0], sd[:W0], w * Wg, scale, 1)
-        _, k0 = ktimed(lambda: m0.fold(ss[:W0], sd[:W0]))
-        ns, kf = [], []
+        filt_h = m0
+        if lag is not None:
+            # the state the senders filter window w with: the last installed broadcast
+            avail = [j for j in range(w) if (j < SYNC and j <= w - 1) or (bcast_async(j) and j + LAG <= w)]
+            target = max(avail) if avail else -1
+            while lag_at < target:
+                lag_at += 1
+                o, sv = history[lag_at]
+                if o is not None:
+                    lag.fold(o[0], o[1])
+                if sv is not None and sv.numel():
+                    lag.fold_pairs(sv, sv.numel() // 2, id_bits=32)
+                lag.close_window()
+            torch.cuda.synchronize()
+            filt_h = lag
+        own = None
+        t0 = 0.0
+        off = w * Wg
+        if W0:
+            gen.rmat(ss[:W0], sd[:W0], off, scale, 1)
+            own = (ss[:W0].clone(), sd[:W0].clone())
+            _, t0 = ktimed(m0, lambda: m0.fold(ss[:W0], sd[:W0]))
+        off += W0
+        ns, tf = [], []
         for r in range(1, P):
-            gen.rmat(ss[:W1], sd[:W1], w * Wg + W0 + (r - 1) * W1, scale, 1)
-            n, k = ktimed(lambda: m0.filter_edges(ss[:W1], sd[:W1], outs[r - 1]))
-            ns.append(n); kf.append(k)
+            n_r = sizes[r]
+            gen.rmat(ss[:n_r], sd[:n_r], off, scale, 1)
+            off += n_r
+            n, k = ktimed(filt_h, lambda: filt_h.filter_edges(ss[:n_r], sd[:n_r], outs[r - 1]))
+            ns.append(n); tf.append(k)
         allp = torch.cat([outs[r - 1][:2 * ns[r - 1]] for r in range(1, P)])     # every survivor, one fold
-        _, km = ktimed(lambda: m0.fold_pairs(allp, allp.numel() // 2, id_bits=32) if allp.numel() else None)
-        _, kc = ktimed(lambda: m0.close_window())
-        t0, tf, tm, tc = k0, kf, km, kc              # kernel time only (HIP events on the launches)
+        _, tm = ktimed(m0, lambda: m0.fold_pairs(allp, allp.numel() // 2, id_bits=32) if allp.numel() else None)
+        _, tc = ktimed(m0, lambda: m0.close_window())
+        if lag is not None:
+            history.append((own, allp.clone()))
         xfer = max(8 * n / LINK * 1e6 for n in ns)
-        due = w < 4 or w % 16 == 15
-        bc = gbytes / BCAST_BW * 1e6 if due else 0.0
-        if due:
-            crit = max(max(tf) + xfer, t0) + tm + tc + bc
+        if r05:
+            due = w < 4 or w % 16 == 15
+            bc = gbytes / BCAST_BW * 1e6 if due else 0.0
+            crit = (max(max(tf) + xfer, t0) + tm + tc + bc) if due else max(max(tf) + xfer, t0 + tm + tc)
+            crit += GAP * 4
         else:
-            crit = max(max(tf) + xfer, t0 + tm + tc)
-        crit += GAP * 4                               # rank 0's chain: own fold, receive, fold, close
+            sync = w < SYNC
+            bc = gbytes / BCAST_BW * 1e6 if sync else 0.0
+            snap = 2 * gbytes / COPY_BW * 1e6 if bcast_async(w) else 0.0
+            inst = 2 * gbytes / COPY_BW * 1e6 if (w >= LAG and bcast_async(w - LAG)) else 0.0
+            chain_s = max(tf) + inst + xfer                            # senders: filter, send
+            chain_r = (t0 + GAP if W0 else 0.0) + tm + tc + snap + 2 * GAP   # rank 0: (own,) fold, close
+            if w == 0 or w - 1 < SYNC:
+                # the filter of w waited for the broadcast after close(w - 1): nothing overlapped
+                crit = chain_s + chain_r + bc
+            else:
+                crit = max(chain_s, chain_r) + bc
         tot["crit"] += crit; tot["filt"] += max(tf); tot["merge"] += tm; tot["close"] += tc; tot["own"] += t0
         tot["surv"] += sum(ns)
         print("w%3d own fold %6.0f us  sender filter max %6.0f us  survivors %8d (max %7d)  xfer %5.0f  "
               "merge folds %6.0f  close %5.0f  bcast %5.0f  critical %6.0f us" %
               (w + 1, t0, max(tf), sum(ns), max(ns), xfer, tm, tc, bc, crit), flush=True)
-    print("TOTAL prefilter: own %.2f ms, sender filter %.2f, merge %.2f, close %.2f, critical %.2f ms, survivors %d; "
+    print("TOTAL prefilter%s: own %.2f ms, sender filter %.2f, merge %.2f, close %.2f, critical %.2f ms, survivors %d; "
           "one GPU %.2f ms -> model speedup %.2fx at P=%d"
-          % (tot["own"] / 1e3, tot["filt"] / 1e3, tot["merge"] / 1e3, tot["close"] / 1e3, tot["crit"] / 1e3,
-             tot["surv"], base / 1e3, base / tot["crit"], P), flush=True)
+          % ("_r05" if r05 else "", tot["own"] / 1e3, tot["filt"] / 1e3, tot["merge"] / 1e3, tot["close"] / 1e3,
+             tot["crit"] / 1e3, tot["surv"], base / 1e3, base / tot["crit"], P), flush=True)
     m0.close()
+    if lag is not None:
+        lag.close()
+    torch.cuda.synchronize()
+
+
+def sim_prefilter_forest(P, NW):
+    """Round-6 prototype: GS_MERGE_PREFILTER whose senders keep a partition forest. Each sender
+    filters its slice against the Merger's giant state (as sim_prefilter), folds the survivors into
+    its OWN cumulative forest (UpdateCC per partition, hook log on) and sends the forest's delta —
+    (v, root) pairs of the roots it hooked — instead of the raw survivors; the Merger folds the pairs
+    (DisjointSet.merge) and closes. Same per-window accounting as sim_prefilter, with rank 0 folding
+    no slice of its own (bench.py's layout at P = 8) and the sender chain = filter + forest fold +
+    export."""
+    BCAST_BW = 64e9
+    base = one_gpu_base(P, NW)
+    Wg = W * P
+    W1 = Wg // (P - 1) // 4 * 4
+    sizes = [W1] * (P - 1)
+    for r in range((Wg - W1 * (P - 1)) // 4):
+        sizes[r % (P - 1)] += 4
+    m0 = gsgpu.DisjointSet(V, id_bits=32, stream=torch.cuda.current_stream())
+    snd = [gsgpu.DisjointSet(V, id_bits=32, track_marks=True, stream=torch.cuda.current_stream()) for _ in range(P - 1)]
+    mx = max(sizes)
+    ss = torch.empty(mx, dtype=torch.int32, device="cuda")
+    sd = torch.empty(mx, dtype=torch.int32, device="cuda")
+    surv = torch.empty(2 * mx, dtype=torch.int32, device="cuda")
+    pbuf = [torch.empty(4 * V, dtype=torch.int32, device="cuda") for _ in range(P - 1)]
+    gbytes = V // 8
+    for h in [m0] + snd:
+        h.timing(True)
+
+    def kt(h):
+        return sum(h.kernel_time(k)[0] for k in range(6)) * 1e3
+
+    def ktimed(h, fn):
+        k0 = kt(h)
+        r = fn()
+        torch.cuda.synchronize()
+        return r, kt(h) - k0
+    print("== prefilter_forest P=%d scale=%d global window 2^%d: rank 0 no slice, senders %d edges each" %
+          (P, scale, Wg.bit_length() - 1, mx), flush=True)
+    tot = dict(crit=0.0, snd=0.0, merge=0.0, close=0.0, surv=0, pairs=0)
+    for w in range(NW):
+        chain, ns, npairs = [], [], []
+        off = w * Wg
+        for r in range(P - 1):
+            n_r = sizes[r]
+            gen.rmat(ss[:n_r], sd[:n_r], off, scale, 1)
+            off += n_r
+            n, tf = ktimed(m0, lambda: m0.filter_edges(ss[:n_r], sd[:n_r], surv))
+            _, tl = ktimed(snd[r], lambda: snd[r].fold_pairs(surv, n, id_bits=32) if n else None)
+            npr, te = ktimed(snd[r], lambda: snd[r].export_marks(pbuf[r]))
+            chain.append(tf + tl + te + 2 * GAP)
+            ns.append(n)
+            npairs.append(npr)
+        allp = torch.cat([pbuf[r][:2 * npairs[r]] for r in range(P - 1)])
+        _, tm = ktimed(m0, lambda: m0.fold_pairs(allp, allp.numel() // 2, id_bits=32) if allp.numel() else None)
+        _, tc = ktimed(m0, lambda: m0.close_window())
+        xfer = max(8 * n / LINK * 1e6 for n in npairs)
+        due = w < 4 or w % 16 == 15
+        bc = gbytes / BCAST_BW * 1e6 if due else 0.0
+        if due:
+            crit = max(chain) + xfer + tm + tc + bc
+        else:
+            crit = max(max(chain) + xfer, tm + tc)
+        crit += GAP * 3                               # rank 0's chain: receive, fold, close
+        tot["crit"] += crit; tot["snd"] += max(chain); tot["merge"] += tm; tot["close"] += tc
+        tot["surv"] += sum(ns); tot["pairs"] += sum(npairs)
+        print("w%3d sender chain max %6.0f us  survivors %8d  pairs %8d (max %7d)  xfer %5.0f  merge folds %6.0f  "
+              "close %5.0f  bcast %5.0f  critical %6.0f us" % (w + 1, max(chain), sum(ns), sum(npairs), max(npairs), xfer,
+                                                               tm, tc, bc, crit), flush=True)
+    print("TOTAL prefilter_forest: sender chain %.2f ms, merge %.2f, close %.2f, critical %.2f ms, survivors %d, pairs %d; "
+          "one GPU %.2f ms -> model speedup %.2fx at P=%d"
+          % (tot["snd"] / 1e3, tot["merge"] / 1e3, tot["close"] / 1e3, tot["crit"] / 1e3, tot["surv"], tot["pairs"],
+             base / 1e3, base / tot["crit"], P), flush=True)
+    for h in [m0] + snd:
+        h.close()
     torch.cuda.synchronize()
 
 
 for scheme in schemes:
-    if scheme == "prefilter":
-        sim_prefilter(P, NW)
+    if scheme in ("prefilter", "prefilter_r05"):
+        sim_prefilter(P, NW, r05=scheme == "prefilter_r05")
+        continue
+    if scheme == "prefilter_forest":
+        sim_prefilter_forest(P, NW)
         continue
     ag = scheme == "allgather"       # replicated summaries: every rank folds every other rank's delta
     base = one_gpu_base(P, NW)
