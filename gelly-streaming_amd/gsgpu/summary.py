@@ -32,13 +32,25 @@ def _is_torch(x) -> bool:
     return type(x).__module__.startswith("torch")
 
 
+# torch.Tensor and the dtypes a buffer may have, once torch is loaded (the per-call checks below
+# run once per window of a per-window caller: config 5's 2^16-edge windows cost ~25 us each)
+_TORCH = None
+
+
+def _torch_kinds():
+    global _TORCH
+    if _TORCH is None:
+        import torch
+        _TORCH = (torch.Tensor, (torch.int32, torch.uint32), (torch.int64,))
+    return _TORCH
+
+
 def _buf(x, id_bits: int, name: str):
     """(pointer, keepalive, length) for a 1-D id buffer of the handle's width."""
-    if _is_torch(x):
-        import torch
-        want = torch.int32 if id_bits == 32 else torch.int64
-        if x.dtype not in ((torch.int32, torch.uint32) if id_bits == 32 else (torch.int64,)):
-            raise TypeError("%s: torch dtype %s, expected %s" % (name, x.dtype, want))
+    if _TORCH is not None and isinstance(x, _TORCH[0]) or _TORCH is None and _is_torch(x):
+        tensor, d32, d64 = _torch_kinds()
+        if x.dtype not in (d32 if id_bits == 32 else d64):
+            raise TypeError("%s: torch dtype %s, expected %s" % (name, x.dtype, (d32 if id_bits == 32 else d64)[0]))
         if not x.is_contiguous():
             raise ValueError("%s: tensor must be contiguous" % name)
         return ctypes.c_void_p(x.data_ptr()), x, x.numel()
@@ -72,8 +84,9 @@ _MODES = {"allgather": _abi.GS_MERGE_ALLGATHER, "gather": _abi.GS_MERGE_GATHER, 
 
 
 def _first_cuda_tensor(objs):
+    tensor = _torch_kinds()[0] if _TORCH is not None else None
     for o in objs:
-        if _is_torch(o) and o.is_cuda:
+        if (isinstance(o, tensor) if tensor is not None else _is_torch(o)) and o.is_cuda:
             return o
     return None
 
