@@ -20,6 +20,9 @@ Checks (BASELINE.json configs[2] on one GPU; tests/test_gpu_variants.py runs thi
   * --id-bits 64: the reference's Long ids (ConnectedComponentsExample.java:61);
   * after the last window the dense canonical labels equal an independent torch CC of the whole
     stream (hook-to-min + pointer jumping: bench.py torch_min_labels) and are minimal/idempotent;
+  * --label-windows (default 1, 2, 5, 16): the WHOLE emission of those windows — every vertex's
+    canonical label, not only the checksum — equals the torch CC of the stream up to them (window 1
+    the young forest, 5 the giant-root change, 16 past the warm-set build);
   * --fold-windows: bench.py's timed call itself, gs_cc_fold_windows (the per-window loop inside the
     library), from a reset over the whole stream in one call, then the last window's emission
     checksum against the fixture; again in calls of --chunk windows, each call's last window
@@ -64,6 +67,9 @@ def main():
     ap.add_argument("--variant", action="store_true", help="allow GSGPU_* variables (a named fold variant)")
     ap.add_argument("--fold-windows", action="store_true", help="also the gs_cc_fold_windows path (bench.py's timed call)")
     ap.add_argument("--chunk", type=int, default=8, help="windows per gs_cc_fold_windows call in the chunked pass")
+    ap.add_argument("--label-windows", default="1,2,5,16",
+                    help="windows (1-based) whose whole label array is compared with an independent torch CC of "
+                         "the stream up to them (first pass; '' = none; skipped with --no-torch)")
     a = ap.parse_args()
     path, a.scale, a.edge_factor, a.window_log2, a.seed = FIXTURES[a.fixture]
     import torch
@@ -84,6 +90,8 @@ def main():
     torch.cuda.synchronize()
     ds = gsgpu.DisjointSet(V, id_bits=a.id_bits, stream=torch.cuda.current_stream())
     passes = []
+    label_windows = [] if a.no_torch else [int(x) for x in a.label_windows.split(",") if x.strip()]
+    saved = {}                             # window -> its emission's dense labels (first pass)
     for step in range(a.steps):
         if step:
             ds.reset()
@@ -92,6 +100,9 @@ def main():
             ds.fold(src[lo:lo + W], dst[lo:lo + W])
             ds.close_window()
             got.append(ds.checksum())
+            if step == 0 and len(got) in label_windows:
+                saved[len(got)] = torch.empty(V, dtype=dt, device="cuda")
+                ds.dense(out=saved[len(got)])
         passes.append(got)
         print("pass %d: %d windows, first bad %s (%.1f s)" % (step, len(got), first_bad(got, want), time.time() - t0),
               file=sys.stderr, flush=True)
@@ -127,15 +138,24 @@ def main():
     if not a.no_torch:
         ref = torch_min_labels(src, dst, V)
         torch_ok = bool(torch.equal(lab, ref))
+        del ref
+    # whole emissions of chosen windows (not only their checksums) vs torch CC of the stream prefix
+    window_labels = {}
+    for w, got_lab in sorted(saved.items()):
+        ref = torch_min_labels(src[:w * W], dst[:w * W], V)
+        window_labels[w] = bool(torch.equal(got_lab.long(), ref))
+        del ref
     nv, nc = ds.stats()
     out = {"fixture": a.fixture, "scale": a.scale, "edges": E, "window_edges": W, "windows": len(want), "id_bits": a.id_bits,
            "steps": a.steps, "fixture_windows_equal": ok_windows,
            "first_bad": [first_bad(g, want) for g in passes],
            "fold_windows": fw, "final_equals_torch_cc": torch_ok, "labels_minimal_idempotent": minimal,
+           "window_labels_equal_torch_cc": window_labels,
            "final_vertices": nv, "final_components": nc,
            "fixture_final": list(want[-1][1:]),
            "seconds": {"gpu": round(t_gpu, 1), "total": round(time.time() - t0, 1)}}
     out["ok"] = ok_windows and torch_ok is not False and minimal and (nv, nc) == tuple(want[-1][1:]) and \
+        all(window_labels.values()) and \
         (fw is None or (fw["whole_ok"] and fw["chunked_ok"]))
     ds.close()
     print(json.dumps(out), flush=True)

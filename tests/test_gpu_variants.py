@@ -64,6 +64,19 @@ def test_c5_config_production(args):
     assert r["ok"], r
 
 
+def test_c5_latency_at_the_c_abi():
+    """csrc/host/cc_latency (config 5 driven window by window from C++, no Python: what a Java FFM /
+    JNI caller sees): the last window's emission equals the C oracle's fixture (window 4,096)."""
+    exe = os.path.join(ROOT, "gelly-streaming_amd", "gsgpu", "lib", "cc_latency")
+    out = subprocess.check_output([exe], env=_env({}), timeout=600)
+    r = _last_json(out)
+    print(r)
+    fx = json.load(open(os.path.join(HERE, "golden", "c5_rmat24.json")))
+    assert r["windows"] == 4096
+    assert (int(r["final_checksum"]), r["final_vertices"], r["final_components"]) == \
+        (int(fx["checksums"][-1]), int(fx["vertices"][-1]), int(fx["components"][-1]))
+
+
 @pytest.mark.parametrize("mode", ["allgather", "gather", "tree", "prefilter"])
 def test_headline_config_eight_ranks_one_gpu(mode):
     """BASELINE config 3's 8-rank strong layout at full scale through the C-ABI exchange
