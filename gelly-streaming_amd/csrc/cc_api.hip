@@ -119,8 +119,6 @@ struct gs_cc {
     uint2* hot = nullptr;                // LDS hot set master copy (kHotBuckets uint2), steady folds
     uint32_t hot_bits = 0;               // ids < 2^hot_bits
     uint32_t* hot_cand = nullptr;        // hot-set admission candidates (2^kHotCandBits ids)
-    uint32_t* ring_tails = nullptr;      // k_fold_ring's dynamic-tail heads (HotArgs::tails), zeroed
-    uint64_t tail_launches = 0;          // ring launches since create: the heads' set parity
     uint32_t* warm = nullptr;            // warm set (2^warm_bits words, L2-resident), steady folds
     uint32_t warm_bits = 0;
     uint32_t* wkeys = nullptr;           // warm build: sampled endpoint key slots
@@ -323,8 +321,6 @@ struct DebugEnv {
     uint64_t young_first_min = kYoungFirstMinWg;    // GSGPU_YOUNG_FIRST_MIN: workgroup floor of the first young launch
     bool list_close = true;                         // GSGPU_LIST_CLOSE=0: no list-mode closes (A/B)
     bool small_claim = true;                        // GSGPU_SMALL_CLAIM=0: small k_fold launches without claims (A/B)
-    uint32_t ring_tail_rounds = 0;                  // GSGPU_RING_TAIL=R[,C]: k_fold_ring's dynamic tail (R rounds,
-    uint32_t ring_tail_chunk = 8;                   //   C wave rounds per grab)
     DebugEnv() {
         const char* e = getenv("GSGPU_FOLD_STATS");
         fold_stats = e && atoi(e) != 0;
@@ -347,12 +343,6 @@ struct DebugEnv {
         if (e && *e) list_close = atoi(e) != 0;
         e = getenv("GSGPU_SMALL_CLAIM");
         if (e && *e) small_claim = atoi(e) != 0;
-        e = getenv("GSGPU_RING_TAIL");
-        if (e && *e) {
-            ring_tail_rounds = (uint32_t)strtoul(e, nullptr, 0);
-            const char* c = strchr(e, ',');
-            if (c) ring_tail_chunk = std::max<uint32_t>(1, (uint32_t)strtoul(c + 1, nullptr, 0));
-        }
 
     }
 };
@@ -499,7 +489,7 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     // kWarmAt after reset and every kWarmEvery-th after it, each time only if the set is not valid
     // for the current giant (device-gated)
     bool build = false;
-    const HotArgs hot0 = ring_hot_args(h, &build);
+    const HotArgs hot = ring_hot_args(h, &build);
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
     f.mark_len = h->mark_ctr;
     f.cbits = kUseCbits ? h->cbits : nullptr;
@@ -509,13 +499,6 @@ void launch_fold_ring(gs_cc_t* h, const IdT* a, const IdT* b, uint64_t n) {
     KTimer t(h, h->fold_timer == GS_K_FOLD ? GS_K_RING : h->fold_timer, n);
     const bool st = h->dstats != nullptr;
     const dim3 grid(grid_for(n / 4, kHotThreads, (unsigned)std::max(h->cus, 1)));
-    HotArgs hot = hot0;
-    if (h->ring_tails && dbg().ring_tail_rounds && grid.x >= 8) {
-        hot.tails = h->ring_tails;
-        hot.tpar = (uint32_t)(h->tail_launches++ & 1);
-        hot.tail_rounds = dbg().ring_tail_rounds;
-        hot.tail_chunk = dbg().ring_tail_chunk;
-    }
     hipEvent_t stop = build ? nullptr : t.stop();
     hipEvent_t start = t.start();
     if (hot.clocks) {                                // GSGPU_RING_CLOCKS: the instrumented instance
@@ -1219,15 +1202,6 @@ int gs_cc_create(gs_cc_t** out, const gs_cc_config* cfg) {
                 h->hot = nullptr;
                 h->hot_cand = nullptr;
             }
-            if (h->hot && hipMalloc(&h->ring_tails, 2 * 8 * kTailLineWords * sizeof(uint32_t)) == hipSuccess) {
-                if (hipMemset(h->ring_tails, 0, 2 * 8 * kTailLineWords * sizeof(uint32_t)) != hipSuccess) {
-                    (void)hipFree(h->ring_tails);
-                    h->ring_tails = nullptr;
-                }
-            } else {
-                (void)hipGetLastError();
-                h->ring_tails = nullptr;
-            }
             h->hot_bits = bits;
             // warm set: only where gbits outgrows an XCD's 4 MiB L2 (with the ring fold), its table
             // L2-resident and at most 1/8 of gbits (8-bit slots need at least 2^(B-8) buckets)
@@ -1292,7 +1266,6 @@ int gs_cc_destroy(gs_cc_t* h) {
     if (h->fstage) (void)hipFree(h->fstage);
     if (h->hot) (void)hipFree(h->hot);
     if (h->hot_cand) (void)hipFree(h->hot_cand);
-    if (h->ring_tails) (void)hipFree(h->ring_tails);
     if (h->warm) (void)hipFree(h->warm);
     if (h->wkeys) (void)hipFree(h->wkeys);
     if (h->wpart) (void)hipFree(h->wpart);

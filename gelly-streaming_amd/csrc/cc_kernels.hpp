@@ -445,15 +445,7 @@ struct HotArgs {
     unsigned long long* wctl = nullptr;        // warm build: edges counted (written by count launches)
     uint64_t count_edges = 0;                  // count this launch's first edges (if !*warm_valid)
     uint32_t clocks = 0;                       // GSGPU_RING_CLOCKS: launch k_fold_ring's CLK instance
-    // k_fold_ring's dynamic tail (below): the last tail_rounds grid-stride rounds go to 8 per-XCD
-    // pools, grabbed tail_chunk wave rounds at a time; tails = 2 sets x 8 heads, one per 128-B line
-    // (set tpar is this launch's, zeroed by the launch before; this launch zeroes the other)
-    uint32_t* tails = nullptr;
-    uint32_t tpar = 0;
-    uint32_t tail_rounds = 0;
-    uint32_t tail_chunk = 8;
 };
-constexpr uint32_t kTailLineWords = 32;
 
 // ---- warm set (L2-resident second tier) ----
 // Ids ranked ~80K..2M by frequency answer ~45 % of an RMAT-26 window's lookups (top 80K: 38 %,
@@ -1138,57 +1130,8 @@ __global__ __launch_bounds__(kHotThreads) void k_fold_ring(const IdT* __restrict
         cnt += wtot;
         if (cnt >= 64) ring_flush<MARK, STATS>(f, ring, cnt, cnt - 64, st, gR);
     };
-    if (!hot.tails || hot.tail_rounds == 0) {
-        for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < groups; g0 += stride)
-            wave_round(g0);
-    } else {
-        // Static grid-stride wave rounds, then a dynamic tail. Workgroups on odd XCDs end a steady
-        // launch ~4 % later than those on even ones (profiles/r06_lazy_skew_ab.txt): the last
-        // tail_rounds rounds form 8 pools, one per XCD (workgroups are dispatched round-robin over the
-        // XCDs: blockIdx % 8); a wave grabs tail_chunk wave rounds from its own XCD's pool, then from
-        // the others'. Drained heads are read (all 8 in one load), not incremented again.
-        constexpr uint32_t kWaves = kHotThreads / 64;
-        const uint32_t nw = gridDim.x * kWaves;
-        const uint32_t gw = blockIdx.x * kWaves + (threadIdx.x >> 6);
-        const uint32_t W = (uint32_t)((groups + 63) / 64);            // wave rounds of 64 groups
-        const uint32_t R = (W + nw - 1) / nw;
-        const uint32_t ks = R > hot.tail_rounds ? R - hot.tail_rounds : 0u;
-        const uint32_t t0 = ks * nw < W ? ks * nw : W;
-        const uint32_t tp = (W - t0 + 7) / 8;                           // wave rounds per pool
-        const uint32_t xcd = blockIdx.x & 7u;
-        if (blockIdx.x == 0 && threadIdx.x < 8)
-            hot.tails[((hot.tpar ^ 1u) * 8 + threadIdx.x) * kTailLineWords] = 0u;
-        uint32_t k = 0, pj = 0, ci = 0, cend = 0;                     // pj: the pool being drained
-        for (;;) {
-            uint32_t q;
-            if (k < ks) {
-                q = gw + k * nw;
-                ++k;
-            } else if (ci < cend) {
-                q = t0 + ((xcd + pj) & 7u) * tp + ci;
-                ++ci;
-            } else {
-                // lanes 0-7 read the 8 heads at once; the wave grabs from the first pool with work
-                // left, its own XCD's first
-                uint32_t* const heads = hot.tails + hot.tpar * 8 * kTailLineWords;
-                uint32_t v = tp;
-                if (lane < 8) v = __hip_atomic_load(heads + lane * kTailLineWords, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t open = (uint32_t)__ballot(lane < 8 && v < tp) & 0xFFu;
-                if (open == 0) break;                                   // uniform: every pool drained
-                const uint32_t rot = ((open >> xcd) | (open << (8 - xcd))) & 0xFFu;
-                pj = (uint32_t)(__ffs(rot) - 1);
-                uint32_t i = 0;
-                if (lane == 0) i = atomicAdd(heads + ((xcd + pj) & 7u) * kTailLineWords, hot.tail_chunk);
-                i = __shfl(i, 0, 64);
-                if (i < tp) {
-                    ci = i;
-                    cend = min(i + hot.tail_chunk, tp);
-                }
-                continue;
-            }
-            if (q < W) wave_round((uint64_t)q * 64);
-        }
-    }
+    for (uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); g0 < groups; g0 += stride)
+        wave_round(g0);
     __shared__ uint32_t s_mcnt;
     __shared__ unsigned long long s_mbase;
     if (CLK) {

@@ -103,10 +103,6 @@ VARIANTS = {
     # no list-mode closes: every close after a logging fold is a bitmap or full one (the A/B knob
     # the round-4 list-close measurements ran against)
     "list_close_off": {"GSGPU_LIST_CLOSE": "0"},
-    # k_fold_ring's per-XCD dynamic tail (GSGPU_RING_TAIL=rounds,chunk): the last 2 grid-stride rounds
-    # from per-XCD pools, and every wave round from them one at a time (no static part)
-    "ring_tail_2x8": {"GSGPU_RING_MIN_BITS": "20", "GSGPU_RING_TAIL": "2,8"},
-    "ring_tail_all": {"GSGPU_RING_MIN_BITS": "20", "GSGPU_RING_TAIL": "100000,1"},
 }
 
 
