@@ -97,7 +97,7 @@ def _bench_layout(P):
 # the round-6 broadcast schedule (csrc/comm.hip merge_prefilter): synchronous after the first
 # kBcastSync closes, then asynchronous (installed by the senders kBcastLag windows later) after every
 # close while w < 16, then after every 4th
-SYNC, LAG = 2, 2
+SYNC, LAG = int(os.environ.get("SIM_SYNC", "2")), 2      # SIM_SYNC: another synchronous prefix (A/B)
 
 
 def bcast_async(w):
