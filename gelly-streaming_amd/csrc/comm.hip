@@ -716,16 +716,19 @@ int merge_gather(gs_comm_t* c, gs_cc_t* h, const CcInfo& in) {
 // after rank 0's closes on the schedule below. A rank may fold no slice of its own (n == 0): every
 // rank still runs every window's exchange (the window count is agreed per call, gs_cc_fold_windows).
 constexpr uint64_t kExactYoung = 16;
-// Filter-state broadcasts (round 6). After each of the first kBcastSync closes the broadcast is on
-// the critical path, as before: the next window's filter waits for it (window 1 has no bitmap at
-// all, window 2 needs the giant window 1 formed). After that they are asynchronous: rank 0 snapshots
+// Filter-state broadcasts (round 6). After the first kBcastSync closes the broadcast is on the
+// critical path, as before: the next window's filter waits for it (window 2 needs the giant window 1
+// formed; with no bitmap at all every edge of window 2 would go to rank 0). After that they are
+// asynchronous (window 3 filters against close 0's bitmap: 3.5 M survivors at the 8-rank RMAT-26
+// layout instead of 2.3 M, but its filter overlaps rank 0's window 2; rank model P = 8 2.23 -> 2.27x,
+// P = 4 1.77 -> 1.84x with one synchronous broadcast instead of two, profiles/r06_k_sim_ab.txt): rank 0 snapshots
 // [gbits | giant words] right after the close and broadcasts the snapshot on a side stream over a
 // communicator of their own, while it folds the next windows; a sender receives into one of two
 // staging slots on its side stream and installs the state before its filter two windows later
 // (a staler bitmap only lets more edges survive: components only merge until reset). While the
 // giant grows (windows < kBcastAsyncYoung) every window's state goes out, then every
 // kBcastAsyncEvery-th (8 MiB at 2^26 ids, ~130 us of link time at 64 GB/s).
-constexpr uint64_t kBcastSync = 2;
+constexpr uint64_t kBcastSync = 1;
 constexpr uint64_t kBcastAsyncYoung = 16;
 constexpr uint64_t kBcastAsyncEvery = 4;
 constexpr uint64_t kBcastLag = 2;                  // installed before the filter of window j + kBcastLag

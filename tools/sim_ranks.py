@@ -97,7 +97,7 @@ def _bench_layout(P):
 # the round-6 broadcast schedule (csrc/comm.hip merge_prefilter): synchronous after the first
 # kBcastSync closes, then asynchronous (installed by the senders kBcastLag windows later) after every
 # close while w < 16, then after every 4th
-SYNC, LAG = int(os.environ.get("SIM_SYNC", "2")), 2      # SIM_SYNC: another synchronous prefix (A/B)
+SYNC, LAG = int(os.environ.get("SIM_SYNC", "1")), 2      # SIM_SYNC: another synchronous prefix (A/B)
 
 
 def bcast_async(w):
@@ -113,7 +113,7 @@ def sim_prefilter(P, NW, r05=False):
     edges) — and rank 0 folds every survivor and closes. Per window: the senders' filters run while
     rank 0 folds and closes the previous window (the senders' send of window w waits for rank 0's
     receive, posted after its close of w - 1), so a window costs the longer of the two chains; a
-    synchronous broadcast (after closes 0 and 1) serialises them. Asynchronous broadcasts cost rank 0
+    synchronous broadcast (after close 0; round 6's first protocol: 0 and 1) serialises them. Asynchronous broadcasts cost rank 0
     a snapshot copy (8 MiB) and the senders an install copy, on their chains."""
     s0 = max(0.0, 1.125 / P - 0.125)                                                   # bench.py prefilter_share0
     BCAST_BW = 64e9
