@@ -101,6 +101,13 @@ def _current_raw_stream(t) -> int:
     return int(torch.cuda.current_stream(t.device).cuda_stream)
 
 
+def _as_torch_stream(hs: int, device):
+    """The handle's stream as a torch stream object (0: the null stream, which a non-blocking torch
+    stream is NOT ordered with, so it gets the event wait like any other)."""
+    import torch
+    return torch.cuda.ExternalStream(hs, device=device) if hs else torch.cuda.default_stream(device)
+
+
 class DisjointSet:
     """GPU union-find summary (DisjointSet<K>), K = int32 or int64 vertex ids in [0, capacity);
     ``sparse=True`` (64-bit ids only): ANY Java long ids, at most ``vertex_capacity`` distinct."""
@@ -168,13 +175,13 @@ class DisjointSet:
         if t is None:
             return
         hs = self._stream()
-        if hs == 0 or hs == _current_raw_stream(t):  # same stream (or the null stream: ordered anyway)
+        if hs == _current_raw_stream(t):                 # same stream: ordered anyway
             return
         import torch
         cur = torch.cuda.current_stream(t.device)
         ev = torch.cuda.Event()
         ev.record(cur)
-        torch.cuda.ExternalStream(hs, device=t.device).wait_event(ev)
+        _as_torch_stream(hs, t.device).wait_event(ev)
 
     def _torch_after(self, *objs) -> None:
         """The reverse: torch's current stream waits for what this handle enqueued into device
@@ -183,12 +190,12 @@ class DisjointSet:
         if t is None:
             return
         hs = self._stream()
-        if hs == 0 or hs == _current_raw_stream(t):
+        if hs == _current_raw_stream(t):
             return
         import torch
         cur = torch.cuda.current_stream(t.device)
         ev = torch.cuda.Event()
-        ev.record(torch.cuda.ExternalStream(hs, device=t.device))
+        ev.record(_as_torch_stream(hs, t.device))
         cur.wait_event(ev)
 
     def sync(self) -> None:

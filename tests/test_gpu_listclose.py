@@ -121,6 +121,33 @@ def test_handle_on_its_own_stream_reads_torch_inputs_in_order(oracle, torch_cuda
         assert ds.checksum()[0] == int(want["checksums"][w]), "window %d" % w
 
 
+def test_handle_on_the_null_stream_reads_a_torch_side_stream_in_order(oracle, torch_cuda):
+    """The handle on the HIP null stream (set_stream(0)), the inputs produced on a torch side stream:
+    torch's pool streams are non-blocking, so the null stream is not ordered with them — gsgpu makes
+    the null stream wait for torch's current stream like any other (summary.py _as_torch_stream)."""
+    torch = torch_cuda
+    scale, n, W = 16, 1 << 18, 4096
+    cap = 1 << scale
+    s, d = oracle.gen_rmat(0, n, scale, 12)
+    want = oracle.run(s, d, W, partitions=4, threads=4, emit=EMIT_CHECKSUM, label_cap=cap)
+    ts = torch.from_numpy(s.astype(np.int32)).cuda()
+    td = torch.from_numpy(d.astype(np.int32)).cuda()
+    ds = DisjointSet(cap, id_bits=32)
+    ds.set_stream(0)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for w, lo in enumerate(range(0, n, W)):
+            junk = torch.empty(1 << 24, device="cuda").uniform_()
+            pairs = torch.stack([ts[lo:lo + W], td[lo:lo + W]], dim=1).contiguous().view(-1)
+            ds.fold_pairs(pairs)
+            ds.close_window()
+            del junk
+            assert ds.checksum()[0] == int(want["checksums"][w]), "window %d" % w
+    torch.cuda.synchronize()
+    ds.close()
+
+
 @pytest.mark.parametrize("W", [4096, 1 << 15])
 def test_giant_root_changes_every_window(oracle, torch_cuda, W):
     """The giant's root (its minimum id) drops in every window: a smaller id joins it each time, so
