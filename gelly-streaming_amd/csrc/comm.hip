@@ -739,13 +739,15 @@ bool bcast_async(uint64_t win) {
 
 // side stream, events and staging of the asynchronous broadcasts (first use)
 int bside_init(gs_comm_t* c, uint64_t slot_words) {
-    if (c->bside) return GS_OK;
-    if (hipStreamCreateWithFlags(&c->bside, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_bmain, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_brecv[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_brecv[1], hipEventDisableTiming) != hipSuccess ||
+    if (c->bstage) return GS_OK;                     // (the last piece: everything before it exists)
+    // a failed attempt keeps what it created (gs_comm_destroy frees it) and the next one goes on
+    if ((!c->bside && hipStreamCreateWithFlags(&c->bside, hipStreamNonBlocking) != hipSuccess) ||
+        (!c->ev_bmain && hipEventCreateWithFlags(&c->ev_bmain, hipEventDisableTiming) != hipSuccess) ||
+        (!c->ev_brecv[0] && hipEventCreateWithFlags(&c->ev_brecv[0], hipEventDisableTiming) != hipSuccess) ||
+        (!c->ev_brecv[1] && hipEventCreateWithFlags(&c->ev_brecv[1], hipEventDisableTiming) != hipSuccess) ||
         hipMalloc(&c->bstage, (size_t)slot_words * 4 * (c->rank == 0 ? 1 : 2)) != hipSuccess) {
         (void)hipGetLastError();
+        c->bstage = nullptr;
         return fail(GS_ERR_NOMEM, "prefilter broadcast staging");
     }
     c->bslot_words = slot_words;

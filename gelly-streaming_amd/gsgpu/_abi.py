@@ -178,11 +178,16 @@ def lib() -> ctypes.CDLL:
     return L
 
 
+_FN = {}                                          # name -> ctypes function (a per-call getattr costs)
+
+
 def call(name: str, *args) -> None:
-    L = lib()
-    rc = getattr(L, name)(*args)
+    f = _FN.get(name)
+    if f is None:
+        f = _FN[name] = getattr(lib(), name)
+    rc = f(*args)
     if rc != GS_OK:
-        msg = L.gs_last_error()
+        msg = lib().gs_last_error()
         raise GsError(rc, name, msg.decode() if msg else "")
 
 

@@ -91,13 +91,20 @@ def _first_cuda_tensor(objs):
     return None
 
 
+_RAW_STREAM = []                                  # [torch._C._cuda_getCurrentRawStream or None], first use
+
+
 def _current_raw_stream(t) -> int:
     """torch's current stream on t's device as a raw pointer (torch.cuda.current_stream builds a
     Stream object per call: a few us, the order of a small window's GPU time)."""
-    import torch
-    f = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    if not _RAW_STREAM:
+        import torch
+        _RAW_STREAM.append(getattr(torch._C, "_cuda_getCurrentRawStream", None))
+    f = _RAW_STREAM[0]
     if f is not None:
-        return int(f(t.device.index if t.device.index is not None else torch.cuda.current_device()))
+        i = t.get_device()                             # (an int: t.device builds a torch.device)
+        return int(f(i))
+    import torch
     return int(torch.cuda.current_stream(t.device).cuda_stream)
 
 
