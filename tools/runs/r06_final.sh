@@ -12,14 +12,17 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 if [ "$PART" = evidence ]; then
+# the PMC passes first: their traffic.json becomes this tree's profiles/fold_traffic.json, so the bench
+# line below carries roofline.traffic of these very sources (copy it into the repo afterwards)
+bash tools/pmc_traffic.sh "$TAG" > "$OUT/pmc.out" 2>&1 || { echo "pmc failed"; tail -5 "$OUT/pmc.out"; exit 3; }
+cp "$OUT/pmc/traffic.json" profiles/fold_traffic.json
+echo "pmc ok"
 timeout -k 10 400 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; echo "bench rc=$rc $(cut -c1-200 $OUT/bench.json)"; [ $rc -eq 0 ] || { tail -5 "$OUT/bench.err"; exit 3; }
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- \
   python3 "$GRAFT_REPO_ROOT/bench.py" --steps 1 --warmup 1 --no-cpu-baseline > "$GRAFT_REPO_ROOT/$OUT/prof.log" 2>&1
 rc=$?; cd "$GRAFT_REPO_ROOT"; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$OUT/prof.log"; exit 3; }
-bash tools/pmc_traffic.sh "$TAG" > "$OUT/pmc.out" 2>&1 || { echo "pmc failed"; tail -5 "$OUT/pmc.out"; exit 3; }
-echo "pmc ok"
 timeout -k 10 300 python -u tools/window_profile.py > "$OUT/window_profile.txt" 2> "$OUT/window_profile.err"
 rc=$?; echo "wprof rc=$rc $(tail -1 $OUT/window_profile.txt)"; [ $rc -eq 0 ] || exit 3
 for w in c2 c4 c5 c5; do
