@@ -321,7 +321,6 @@ struct DebugEnv {
     uint64_t young_first_min = kYoungFirstMinWg;    // GSGPU_YOUNG_FIRST_MIN: workgroup floor of the first young launch
     bool list_close = true;                         // GSGPU_LIST_CLOSE=0: no list-mode closes (A/B)
     bool small_claim = true;                        // GSGPU_SMALL_CLAIM=0: small k_fold launches without claims (A/B)
-    uint32_t young_chunks = 1;                      // GSGPU_YOUNG_CHUNKS=K: young-fold chunks per counter grab (A/B)
     DebugEnv() {
         const char* e = getenv("GSGPU_FOLD_STATS");
         fold_stats = e && atoi(e) != 0;
@@ -344,8 +343,6 @@ struct DebugEnv {
         if (e && *e) list_close = atoi(e) != 0;
         e = getenv("GSGPU_SMALL_CLAIM");
         if (e && *e) small_claim = atoi(e) != 0;
-        e = getenv("GSGPU_YOUNG_CHUNKS");
-        if (e && *e) young_chunks = (uint32_t)std::max(1, std::min(64, atoi(e)));
 
     }
 };
@@ -412,7 +409,6 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
     }
     if (persist) {
         f.work = reinterpret_cast<unsigned long long*>(h->derr + kWorkWord);
-        f.work_chunks = dbg().young_chunks;
         (void)hipMemsetAsync(f.work, 0, sizeof(unsigned long long), h->stream);
     }
     const bool vec = std::is_same<IdT, uint32_t>::value && !AOS &&

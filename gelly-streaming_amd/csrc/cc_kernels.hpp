@@ -294,7 +294,6 @@ struct FoldArgs {
     unsigned long long* stats;   // STATS: [valid, filtered, early, hooks, casfail, inits]
     uint32_t halve = 1;          // path halving in root walks (find_root)
     unsigned long long* work = nullptr;   // k_fold: dynamic chunk counter (young forest), or null
-    uint32_t work_chunks = 1;             // ... blockDim-group chunks taken per grab
     unsigned long long* mark_len = nullptr;   // MARK: the hook log's length word (mark = the log)
     uint32_t* cbits = nullptr;   // ring folds: vertices claimed straight under the giant root (k_compress)
     uint32_t* hbits = nullptr;   // hooked-root bitmap, used by the kernel only while no giant exists
@@ -871,17 +870,14 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold(const IdT* __restrict__ a
     const uint64_t groups = (n + EPT - 1) / EPT;
     if (f.work) {
         __shared__ unsigned long long s_base;
-        const uint32_t kc = f.work_chunks;
         for (;;) {
-            if (threadIdx.x == 0) s_base = atomicAdd(f.work, (unsigned long long)blockDim.x * kc);
+            if (threadIdx.x == 0) s_base = atomicAdd(f.work, (unsigned long long)blockDim.x);
             __syncthreads();
             const uint64_t base = s_base;
             __syncthreads();
             if (base >= groups) break;
-            for (uint32_t c = 0; c < kc; ++c) {
-                const uint64_t g = base + (uint64_t)c * blockDim.x + threadIdx.x;
-                if (g < groups) fold_edges_at<IdT, AOS, MARK, VEC, EPT, STATS>(a, b, f, filt, g, st, claim_gR);
-            }
+            const uint64_t g = base + threadIdx.x;
+            if (g < groups) fold_edges_at<IdT, AOS, MARK, VEC, EPT, STATS>(a, b, f, filt, g, st, claim_gR);
         }
     } else {
         const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
