@@ -108,7 +108,7 @@ def sim_prefilter(P, NW, r05=False):
     """GS_MERGE_PREFILTER, the round-6 protocol (r05=True: round 5's accounting, kept for the record).
     The global window (P x the per-rank W) is split as bench.py splits it (rank 0 no slice at P = 8).
     Each sender slice is filtered against the Merger's giant state AS THE SENDER HAS IT — the state
-    after the last close whose broadcast it has installed (a second summary replays the Merger's
+    after the last close whose broadcast it has installed (a summary per sender replays the Merger's
     folds and closes that many windows behind, so the survivors include the stale bitmap's extra
     edges) — and rank 0 folds every survivor and closes. Per window: the senders' filters run while
     rank 0 folds and closes the previous window (the senders' send of window w waits for rank 0's
@@ -130,15 +130,20 @@ def sim_prefilter(P, NW, r05=False):
         sizes = _bench_layout(P)
     W0 = sizes[0]
     m0 = gsgpu.DisjointSet(V, id_bits=32, stream=torch.cuda.current_stream())
-    lag = None if r05 else gsgpu.DisjointSet(V, id_bits=32, stream=torch.cuda.current_stream())
+    # one lagging summary per sender (SIM_SHARED_LAG=1: one for all, as the first round-6 model ran it):
+    # each sender's hot set is admitted by its own filter launches (one per window, the protocol's
+    # cadence); one handle running all P - 1 filters admitted P - 1 times as often
+    nlag = 0 if r05 else (1 if os.environ.get("SIM_SHARED_LAG") else P - 1)
+    lags = [gsgpu.DisjointSet(V, id_bits=32, stream=torch.cuda.current_stream()) for _ in range(nlag)]
+    lag = lags[0] if lags else None
     mx = max(sizes)
     ss = torch.empty(mx, dtype=torch.int32, device="cuda")
     sd = torch.empty(mx, dtype=torch.int32, device="cuda")
     outs = [torch.empty(2 * sizes[r], dtype=torch.int32, device="cuda") for r in range(1, P)]
     gbytes = V // 8
     m0.timing(True)
-    if lag is not None:
-        lag.timing(True)
+    for h in lags:
+        h.timing(True)
 
     def ktime(h):
         return sum(h.kernel_time(k)[0] for k in range(6)) * 1e3        # us, cumulative
@@ -163,11 +168,12 @@ def sim_prefilter(P, NW, r05=False):
             while lag_at < target:
                 lag_at += 1
                 o, sv = history[lag_at]
-                if o is not None:
-                    lag.fold(o[0], o[1])
-                if sv is not None and sv.numel():
-                    lag.fold_pairs(sv, sv.numel() // 2, id_bits=32)
-                lag.close_window()
+                for h in lags:
+                    if o is not None:
+                        h.fold(o[0], o[1])
+                    if sv is not None and sv.numel():
+                        h.fold_pairs(sv, sv.numel() // 2, id_bits=32)
+                    h.close_window()
             torch.cuda.synchronize()
             filt_h = lag
         own = None
@@ -183,7 +189,8 @@ def sim_prefilter(P, NW, r05=False):
             n_r = sizes[r]
             gen.rmat(ss[:n_r], sd[:n_r], off, scale, 1)
             off += n_r
-            n, k = ktimed(filt_h, lambda: filt_h.filter_edges(ss[:n_r], sd[:n_r], outs[r - 1]))
+            fh = lags[(r - 1) % len(lags)] if lags else filt_h
+            n, k = ktimed(fh, lambda: fh.filter_edges(ss[:n_r], sd[:n_r], outs[r - 1]))
             ns.append(n); tf.append(k)
         allp = torch.cat([outs[r - 1][:2 * ns[r - 1]] for r in range(1, P)])     # every survivor, one fold
         _, tm = ktimed(m0, lambda: m0.fold_pairs(allp, allp.numel() // 2, id_bits=32) if allp.numel() else None)
@@ -218,8 +225,8 @@ def sim_prefilter(P, NW, r05=False):
           % ("_r05" if r05 else "", tot["own"] / 1e3, tot["filt"] / 1e3, tot["merge"] / 1e3, tot["close"] / 1e3,
              tot["crit"] / 1e3, tot["surv"], base / 1e3, base / tot["crit"], P), flush=True)
     m0.close()
-    if lag is not None:
-        lag.close()
+    for h in lags:
+        h.close()
     torch.cuda.synchronize()
 
 
