@@ -319,8 +319,6 @@ struct DebugEnv {
     uint64_t small_fold = kSmallFoldEdges;          // GSGPU_SMALL_FOLD: plain folds of at most this many edges...
     int small_ept = kSmallEpt;                      // GSGPU_SMALL_EPT: ...take this many edges per thread
     uint64_t young_first_min = kYoungFirstMinWg;    // GSGPU_YOUNG_FIRST_MIN: workgroup floor of the first young launch
-    int young_ept = kYoungEpt;                      // GSGPU_YOUNG_EPT=1|2|4: young-fold edges per thread (A/B)
-    uint64_t young_bpc = kYoungBlocksPerCu;         // GSGPU_YOUNG_BPC=B: young-fold workgroups per CU (A/B)
     bool list_close = true;                         // GSGPU_LIST_CLOSE=0: no list-mode closes (A/B)
     bool small_claim = true;                        // GSGPU_SMALL_CLAIM=0: small k_fold launches without claims (A/B)
     DebugEnv() {
@@ -339,10 +337,6 @@ struct DebugEnv {
         if (e && *e) small_fold = strtoull(e, nullptr, 0);
         e = getenv("GSGPU_YOUNG_FIRST_MIN");
         if (e && *e) young_first_min = std::max<uint64_t>(1, strtoull(e, nullptr, 0));
-        e = getenv("GSGPU_YOUNG_EPT");
-        if (e && *e) young_ept = atoi(e) == 1 ? 1 : (atoi(e) == 4 ? 4 : 2);
-        e = getenv("GSGPU_YOUNG_BPC");
-        if (e && *e) young_bpc = std::max<uint64_t>(1, std::min<uint64_t>(8, strtoull(e, nullptr, 0)));
         e = getenv("GSGPU_SMALL_EPT");
         if (e && *e) small_ept = atoi(e) == 1 ? 1 : (atoi(e) == 2 ? 2 : 4);
         e = getenv("GSGPU_LIST_CLOSE");
@@ -375,15 +369,15 @@ static void launch_warm_build(gs_cc_t* h, hipEvent_t stop, hipStream_t s);
 template <typename IdT, bool AOS>
 void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool young = false) {
     const uint64_t small = AOS ? std::max<uint64_t>(kSmallPairFold, dbg().small_fold) : dbg().small_fold;
-    const int ept = young ? dbg().young_ept : (n <= small ? dbg().small_ept : kEdgesPerThread);
+    const int ept = young ? kYoungEpt : (n <= small ? dbg().small_ept : kEdgesPerThread);
     const bool persist = young && h->cus > 0;
     // The first young launch after reset folds into an EMPTY forest: every hub's first hooks and
     // the giant root's repeated re-hooks collide there, so it keeps at most ~1/16 of its edges in
     // flight (>= 32 workgroups). BASELINE config 2 (RMAT-20, the whole 2^18-edge launch in flight
     // at 2/CU): 0.97 -> 0.64 ms per step; configs 3-5 unchanged (profiles/r03_ygrid2).
     const uint64_t ycap = h->edges_since_reset ? ~0ull
-                                               : std::max<uint64_t>(dbg().young_first_min, n / (kYoungFirstDiv * kFoldThreads * ept));
-    const unsigned grid = persist ? (unsigned)std::min<uint64_t>(std::min<uint64_t>((uint64_t)h->cus * dbg().young_bpc, ycap),
+                                               : std::max<uint64_t>(dbg().young_first_min, n / (kYoungFirstDiv * kFoldThreads * kYoungEpt));
+    const unsigned grid = persist ? (unsigned)std::min<uint64_t>(std::min<uint64_t>((uint64_t)h->cus * kYoungBlocksPerCu, ycap),
                                                                   grid_for((n + ept - 1) / ept, kFoldThreads, 1u << 20))
                                   : grid_for((n + ept - 1) / ept, kFoldThreads, 16384);
     ensure_stats(h);
