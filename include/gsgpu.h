@@ -196,7 +196,12 @@ int gs_cc_set_marking(gs_cc_t* h, int on);
  *                         1..P-1 keep no forest — each filters its slice of a window against the
  *                         giant bitmap rank 0 broadcasts and sends the surviving edges to rank 0,
  *                         which folds its own slice and every survivor, closes and emits (dense
- *                         ids; GS_CC_TRACK_MARKS not needed). Slices may differ in size per rank.
+ *                         ids; GS_CC_TRACK_MARKS not needed). Slices may differ in size per rank
+ *                         and may be empty. The bitmap goes out after close 0 on the call's stream
+ *                         (window 2's filter waits for it), later ones on a side stream over a
+ *                         communicator split from this one when a handle is first bound in this
+ *                         mode (collective), installed two windows later: a stale bitmap only lets
+ *                         more edges through.
  *   Every rank must call it once per window with the same mode. In GATHER / TREE only rank 0's
  *   emission is the job's, and the call waits for the delta sizes. In ALLGATHER it does not wait:
  *   the sizes are checked lazily (an outgrown slot's tail round) by the next merge_window, or first
@@ -222,8 +227,9 @@ int gs_cc_merge_window(gs_cc_t* h, gs_comm_t* comm, int mode);
  * else gs_cc_close_window — the per-window host loop run inside the library (one ABI call per batch
  * instead of two per window). After it returns, the labels are those of the last window's
  * emission; *windows_out (may be NULL) = windows folded. Stops at the first failure. With
- * GS_MERGE_PREFILTER only rank 0 folds (the others filter their slices for it); every rank must
- * pass the same number of windows (n / window_edges rounded up), window_edges may differ. */
+ * GS_MERGE_PREFILTER only rank 0 folds (the others filter their slices for it); the ranks agree on
+ * the call's window count (the most any rank passes, n / window_edges rounded up; one collective per
+ * call) and a rank with fewer windows, or none (n == 0), runs empty ones; window_edges may differ. */
 int gs_cc_fold_windows(gs_cc_t* h, gs_comm_t* comm, int mode, const void* src, const void* dst, uint64_t n,
                        uint64_t window_edges, uint64_t* windows_out);
 
