@@ -24,6 +24,7 @@
 // agree on it), a walk treats a word that is not below its index (a stale kInvalid) as a root.
 #include <algorithm>
 #include <cstring>
+#include <unordered_map>
 #include <vector>
 
 #include <hipcub/hipcub.hpp>
@@ -302,6 +303,15 @@ __global__ __launch_bounds__(kLitThreads) void k_bipl_merge(lit::State S, lit::S
     __shared__ uint32_t scan[kLitThreads];
     LitX x{scan};
     lit::merge_summaries(x, S, sh, F);
+}
+
+// restoreState: the snapshot's components, one run after another (lit::load_components)
+__global__ __launch_bounds__(kLitThreads) void k_bipl_load(lit::State S, const uint32_t* rk, const uint64_t* ro,
+                                                           uint32_t runs, const uint32_t* rv, const uint8_t* rs) {
+    __shared__ lit::Shared sh;
+    __shared__ uint32_t scan[kLitThreads];
+    LitX x{scan};
+    lit::load_components(x, S, sh, rk, ro, runs, rv, rs);
 }
 
 // the live (component, vertex, sign) entries: sort keys vertex << 32 | key (emission order: by
@@ -821,6 +831,133 @@ int gs_bip_emit_pairs(gs_bip_t* h, void* vertices, void* keys, uint8_t* signs, u
     if (total > cap) return fail(GS_ERR_CAPACITY, "gs_bip_emit_pairs: %llu vertices, capacity %llu",
                                  (unsigned long long)total, (unsigned long long)cap);
     return GS_OK;
+}
+
+// restoreState (the Merger's ListCheckpointed state, SummaryAggregation.java:121-135): the summary
+// becomes the snapshot's. A literal summary is loaded entry by entry (its components may share
+// vertices, so no set of edges rebuilds it); an intended one is rebuilt from one parity edge per
+// vertex, relative to its component key's own sign (a reversed merge can leave a key signed false,
+// Candidates.java:155-182): a vertex signed unlike its key gets (v, key), one signed like it (other
+// than the key) an edge to a vertex of the component signed the other way, a lone key its
+// self-loop; a failed snapshot is the odd cycle 0-1-2 there (Candidates.fail(): empty, f0 false).
+int gs_bip_restore(gs_bip_t* h, int bipartite, const void* vertices, const void* keys, const uint8_t* signs, uint64_t n) {
+    GS_TRY(bcheck(h));
+    if (n && (!vertices || !keys || !signs)) return fail(GS_ERR_INVALID, "gs_bip_restore: null entry array");
+    DeviceGuard g(h->device);
+    const size_t esz = h->id_bits / 8;
+    std::vector<int64_t> v(n), k(n);
+    std::vector<uint8_t> sg(n);
+    if (n) {
+        std::vector<char> raw(n * esz);
+        auto get = [&](const void* src, size_t bytes, void* dst) -> int {
+            if (is_device_pointer(src)) GS_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+            else std::memcpy(dst, src, bytes);
+            return GS_OK;
+        };
+        for (int which = 0; which < 2; ++which) {
+            GS_TRY(get(which ? keys : vertices, n * esz, raw.data()));
+            std::vector<int64_t>& o = which ? k : v;
+            for (uint64_t i = 0; i < n; ++i) {
+                if (esz == 4) { uint32_t x; std::memcpy(&x, raw.data() + 4 * i, 4); o[i] = x; }
+                else std::memcpy(&o[i], raw.data() + 8 * i, 8);
+            }
+        }
+        GS_TRY(get(signs, n, sg.data()));
+        for (uint64_t i = 0; i < n; ++i) {
+            if (v[i] < 0 || v[i] >= (int64_t)h->cap || k[i] < 0 || k[i] >= (int64_t)h->cap)
+                return fail(GS_ERR_INVALID, "gs_bip_restore: entry %llu (vertex %lld, key %lld) outside [0, %u)",
+                            (unsigned long long)i, (long long)v[i], (long long)k[i], h->cap);
+            sg[i] = sg[i] ? 1 : 0;
+        }
+    }
+    GS_TRY(gs_bip_reset(h));
+    if (h->lit) {
+        if (!bipartite) {                              // Candidates.fail(): no component, f0 false
+            lit::Ctl c = *h->lit->hctl;
+            c.ok = 0;
+            *h->lit->hctl = c;
+            GS_HIP(hipMemcpyAsync(h->lit->S.ctl, h->lit->hctl, sizeof(c), hipMemcpyHostToDevice, h->stream));
+            GS_HIP(hipStreamSynchronize(h->stream));
+            return GS_OK;
+        }
+        if (n == 0) return GS_OK;
+        std::vector<uint64_t> ord(n);
+        for (uint64_t i = 0; i < n; ++i) ord[i] = i;
+        std::sort(ord.begin(), ord.end(), [&](uint64_t a, uint64_t b) { return k[a] != k[b] ? k[a] < k[b] : v[a] < v[b]; });
+        std::vector<uint32_t> rk, rv(n);
+        std::vector<uint64_t> ro;
+        std::vector<uint8_t> rs(n);
+        for (uint64_t j = 0; j < n; ++j) {
+            const uint64_t i = ord[j];
+            if (j && k[i] == k[ord[j - 1]] && v[i] == v[ord[j - 1]])
+                return fail(GS_ERR_INVALID, "gs_bip_restore: vertex %lld twice in component %lld", (long long)v[i], (long long)k[i]);
+            if (!j || k[i] != k[ord[j - 1]]) {
+                rk.push_back((uint32_t)k[i]);
+                ro.push_back(j);
+            }
+            rv[j] = (uint32_t)v[i];
+            rs[j] = sg[i];
+        }
+        ro.push_back(n);
+        const lit::State& S = h->lit->S;
+        if (n > S.E || rk.size() > S.C)
+            return fail(GS_ERR_CAPACITY, "gs_bip_restore: %llu entries in %zu components, the summary holds %u / %u "
+                        "(gs_bip_create_ex entry_capacity)", (unsigned long long)n, rk.size(), S.E, S.C);
+        const size_t b_rk = (rk.size() * 4 + 255) & ~(size_t)255, b_ro = (ro.size() * 8 + 255) & ~(size_t)255,
+                     b_rv = ((size_t)n * 4 + 255) & ~(size_t)255;
+        GS_TRY(bensure(&h->tmp, &h->tmp_bytes, b_rk + b_ro + b_rv + n));
+        char* base = static_cast<char*>(h->tmp);
+        GS_HIP(hipMemcpy(base, rk.data(), rk.size() * 4, hipMemcpyHostToDevice));
+        GS_HIP(hipMemcpy(base + b_rk, ro.data(), ro.size() * 8, hipMemcpyHostToDevice));
+        GS_HIP(hipMemcpy(base + b_rk + b_ro, rv.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+        GS_HIP(hipMemcpy(base + b_rk + b_ro + b_rv, rs.data(), n, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(k_bipl_load, dim3(1), dim3(kLitThreads), 0, h->stream, h->lit->S, (const uint32_t*)base,
+                           (const uint64_t*)(base + b_rk), (uint32_t)rk.size(), (const uint32_t*)(base + b_rk + b_ro),
+                           (const uint8_t*)(base + b_rk + b_ro + b_rv));
+        GS_HIP(hipGetLastError());
+        return lsync(h, nullptr);
+    }
+    std::vector<int64_t> src, dst;
+    if (!bipartite) {
+        if (h->cap < 3) return fail(GS_ERR_INVALID, "gs_bip_restore: a failed snapshot needs vertex_capacity >= 3");
+        src = {0, 1, 2};
+        dst = {1, 2, 0};
+    } else {
+        std::unordered_map<int64_t, uint8_t> ksign;   // component key -> the key vertex's own sign
+        std::unordered_map<int64_t, int64_t> other;   // component key -> a vertex signed unlike the key
+        for (uint64_t i = 0; i < n; ++i)
+            if (v[i] == k[i]) ksign[k[i]] = sg[i];
+        for (uint64_t i = 0; i < n; ++i) {
+            auto ks = ksign.find(k[i]);
+            if (ks == ksign.end())
+                return fail(GS_ERR_INVALID, "gs_bip_restore: component key %lld is not among the vertices", (long long)k[i]);
+            if (sg[i] != ks->second) other.emplace(k[i], v[i]);
+        }
+        src.reserve(n);
+        dst.reserve(n);
+        for (uint64_t i = 0; i < n; ++i) {
+            src.push_back(v[i]);
+            if (sg[i] != ksign[k[i]]) dst.push_back(k[i]);
+            else if (v[i] != k[i]) {
+                auto o = other.find(k[i]);
+                if (o == other.end())
+                    return fail(GS_ERR_INVALID, "gs_bip_restore: component %lld has vertices on one side only", (long long)k[i]);
+                dst.push_back(o->second);
+            } else dst.push_back(v[i]);
+        }
+    }
+    if (!src.empty()) {
+        if (esz == 4) {
+            std::vector<uint32_t> a(src.begin(), src.end()), b(dst.begin(), dst.end());
+            GS_TRY(bfold(h, a.data(), b.data(), a.size(), false));
+            GS_HIP(hipStreamSynchronize(h->stream));   // (the staged copies read the host vectors)
+        } else {
+            GS_TRY(bfold(h, src.data(), dst.data(), src.size(), false));
+            GS_HIP(hipStreamSynchronize(h->stream));
+        }
+    }
+    GS_TRY(gs_bip_close_window(h));
+    return bsync(h, nullptr);
 }
 
 int gs_bip_sync(gs_bip_t* h) {

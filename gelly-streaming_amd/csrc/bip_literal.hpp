@@ -392,5 +392,26 @@ GS_HD inline void merge_summaries(X& x, State& S, Shared& sh, const State& F) {
     x.sync();
 }
 
+// restoreState (SummaryAggregation.java:121-135 for this summary): on a reset state, the snapshot's
+// components one after another — run r is component key rk[r] with the members (rv[i], rs[i]),
+// i in [ro[r], ro[r + 1]) (distinct vertices within a run; the host groups and checks them); the
+// memberships go in as the rule made them, so components may share vertices again
+template <class X>
+GS_HD inline void load_components(X& x, State& S, Shared& sh, const uint32_t* rk, const uint64_t* ro, uint32_t runs,
+                                  const uint32_t* rv, const uint8_t* rs) {
+    for (uint32_t r = 0; r < runs; ++r) {
+        if (stopped(x, S, sh)) return;
+        const uint64_t lo = ro[r], s = ro[r + 1] - ro[r];
+        if (x.tid() == 0) sh.cslot = new_comp(S, rk[r]);
+        if (stopped(x, S, sh)) return;
+        const uint32_t c = sh.cslot;
+        grow(x, S, sh, c, (uint32_t)s);
+        if (stopped(x, S, sh)) return;
+        for (uint64_t i = x.tid(); i < s; i += x.nt()) add_node(x, S, c, rv[lo + i], (uint32_t)rs[lo + i]);
+        x.sync();
+    }
+    x.sync();
+}
+
 }  // namespace lit
 }  // namespace gsgpu

@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = (
     "gs_cc_fold_text", "gs_cc_fold_file",
     "gs_bip_create", "gs_bip_destroy", "gs_bip_reset", "gs_bip_set_stream", "gs_bip_sync", "gs_bip_fold",
     "gs_bip_fold_pairs", "gs_bip_merge", "gs_bip_close_window", "gs_bip_status", "gs_bip_checksum",
-    "gs_bip_emit_pairs", "gs_bip_create_ex",
+    "gs_bip_emit_pairs", "gs_bip_create_ex", "gs_bip_restore",
     "gs_comm_unique_id", "gs_comm_create", "gs_comm_create_local", "gs_comm_destroy", "gs_comm_info",
     "gs_cc_merge_window", "gs_cc_fold_windows",
     "gs_last_error", "gs_version",
@@ -158,6 +158,7 @@ def lib() -> ctypes.CDLL:
         "gs_bip_status": [vp, P(i32), P(u64), P(u64)],
         "gs_bip_checksum": [vp, P(u64), P(i32), P(u64), P(u64)],
         "gs_bip_emit_pairs": [vp, vp, vp, vp, u64, P(u64)],
+        "gs_bip_restore": [vp, i32, vp, vp, vp, u64],
         "gs_comm_unique_id": [vp, u64],
         "gs_comm_create": [P(vp), vp, i32, i32, i32],
         "gs_comm_create_local": [P(vp), i32, i32],

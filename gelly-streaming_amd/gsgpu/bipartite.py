@@ -133,51 +133,31 @@ class Candidates:
         return True, v, k, s
 
     def restore(self, success, vertices, keys, signs) -> None:
-        """This summary becomes the snapshotted one: reset, then one parity edge per vertex,
-        relative to its component key's own sign (reversed merges can leave a key signed false,
-        Candidates.java:155-182): a vertex signed differently from its key gets the edge
-        (v, key); a vertex signed like its key (other than the key) gets an edge to a vertex of
-        its component signed the other way (a connected bipartite component of several vertices
-        has one); a lone key gets its self-loop (edgeToCandidate(v, v) adds it). A failed snapshot
-        is restored as failed (Candidates.fail(): empty map) by an odd cycle on ids 0..2."""
-        if self.literal:
-            raise _abi.GsError(_abi.GS_ERR_UNSUPPORTED, "Candidates.restore",
-                               "a reference-literal summary (overlapping components) is not rebuilt from a snapshot")
-        self.reset()
-        if not success:
-            if self.capacity < 3:
-                raise ValueError("restoring a failed Candidates needs vertex_capacity >= 3")
-            self.fold(np.array([0, 1, 2]), np.array([1, 2, 0]))
-            return
+        """This summary becomes the snapshotted one (gs_bip_restore). A reference-literal summary
+        loads the entries as they are (its components may share vertices); an intended one is
+        rebuilt from one parity edge per vertex, relative to its component key's own sign
+        (reversed merges can leave a key signed false, Candidates.java:155-182): a vertex signed
+        differently from its key gets the edge (v, key); a vertex signed like its key (other than
+        the key) gets an edge to a vertex of its component signed the other way (a connected
+        bipartite component of several vertices has one); a lone key gets its self-loop
+        (edgeToCandidate(v, v) adds it). A failed snapshot is restored as failed
+        (Candidates.fail(): empty map; intended summaries: an odd cycle on ids 0..2)."""
+        dt = np.uint32 if self.id_bits == 32 else np.int64
         v = np.asarray(vertices, dtype=np.int64)
         k = np.asarray(keys, dtype=np.int64)
         s = np.asarray(signs, dtype=bool)
         if not (v.shape == k.shape == s.shape):
             raise ValueError("restore: vertices, keys and signs differ in length")
-        if v.size == 0:
-            return
-        ksign = {}                                 # component key -> the key vertex's own sign
-        for a, b, c in zip(v.tolist(), k.tolist(), s.tolist()):
-            if a == b:
-                ksign[b] = c
-        other = {}                                 # component key -> one vertex signed unlike the key
-        for a, b, c in zip(v.tolist(), k.tolist(), s.tolist()):
-            if b not in ksign:
-                raise ValueError("restore: component key %d is not among the vertices" % b)
-            if c != ksign[b]:
-                other.setdefault(b, a)
-        src, dst = [], []
-        for a, b, c in zip(v.tolist(), k.tolist(), s.tolist()):
-            if c != ksign[b]:
-                src.append(a); dst.append(b)
-            elif a != b:
-                if b not in other:
-                    raise ValueError("restore: component %d has vertices on one side only" % b)
-                src.append(a); dst.append(other[b])
-            else:
-                src.append(a); dst.append(a)
-        self.fold(np.array(src, dtype=np.int64), np.array(dst, dtype=np.int64))
-        self.close_window()
+        if not success:
+            v = k = np.empty(0, dtype=np.int64)
+            s = np.empty(0, dtype=bool)
+        if v.size and (v.min() < 0 or k.min() < 0):
+            raise ValueError("restore: negative vertex id")
+        va = np.ascontiguousarray(v.astype(dt))
+        ka = np.ascontiguousarray(k.astype(dt))
+        sa = np.ascontiguousarray(s.astype(np.uint8))
+        call("gs_bip_restore", self.handle, 1 if success else 0, va.ctypes.data_as(ctypes.c_void_p),
+             ka.ctypes.data_as(ctypes.c_void_p), sa.ctypes.data_as(ctypes.c_void_p), int(va.size))
 
     def toString(self) -> str:
         """Tuple2<Boolean, TreeMap<Long, TreeMap<Long, SignedVertex>>>.toString."""

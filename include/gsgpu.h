@@ -302,6 +302,9 @@ int gs_cc_fold_file(gs_cc_t* h, const char* path, uint64_t window_edges, uint64_
  *   gs_bip_status / _checksum  getSuccess() (Candidates.java:40-42), sizes, and
  *                              sum over v of splitmix64(v ^ splitmix64(((key << 1) | sign) ^ 0xD1B54A32D192ED03))
  *   gs_bip_emit_pairs          (vertex, key, sign) ordered by vertex      (Candidates.getMap(), :44-46)
+ *   gs_bip_restore             restoreState: the summary becomes a snapshot's — getSuccess() and
+ *                              the n entries gs_bip_emit_pairs wrote (any order; host or device
+ *                              arrays of the handle's id width)           (SummaryAggregation.java:121-135)
  * GS_BIP_REFERENCE_LITERAL (gs_bip_create_ex): the reference's Candidates rule as written
  * (Candidates.java:77-192) instead of its intended semantics, for callers that need the reference's
  * emissions on multi-window / multi-partition streams: a merge writes an input component under
@@ -313,7 +316,10 @@ int gs_cc_fold_file(gs_cc_t* h, const char* path, uint64_t window_edges, uint64_
  * vertex_capacity; GS_ERR_CAPACITY past it). Such summaries merge only with each other;
  * gs_bip_status / _checksum count (component, vertex) entries; gs_bip_emit_pairs writes every
  * entry ordered by vertex, then key; close_window is a no-op; a place where the reference's
- * merge would throw (an empty mergeBy list, :156) fails the call with GS_ERR_INVALID. */
+ * merge would throw (an empty mergeBy list, :156) fails the call with GS_ERR_INVALID; gs_bip_restore
+ * loads the entries as they are (components sharing vertices included). An intended-semantics
+ * summary is restored from one parity edge per vertex (GS_ERR_INVALID for entries no bipartite
+ * summary emits: a key outside its component, a component of one side only). */
 typedef struct gs_bip gs_bip_t;
 enum { GS_BIP_REFERENCE_LITERAL = 1 };
 int gs_bip_create(gs_bip_t** out, uint64_t vertex_capacity, uint32_t id_bits, int device);
@@ -330,6 +336,7 @@ int gs_bip_close_window(gs_bip_t* h);
 int gs_bip_status(gs_bip_t* h, int* bipartite, uint64_t* n_vertices, uint64_t* n_components);
 int gs_bip_checksum(gs_bip_t* h, uint64_t* checksum, int* bipartite, uint64_t* n_vertices, uint64_t* n_components);
 int gs_bip_emit_pairs(gs_bip_t* h, void* vertices, void* keys, uint8_t* signs, uint64_t cap, uint64_t* n_out);
+int gs_bip_restore(gs_bip_t* h, int bipartite, const void* vertices, const void* keys, const uint8_t* signs, uint64_t n);
 
 const char* gs_last_error(void);
 int gs_version(void);

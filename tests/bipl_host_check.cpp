@@ -5,6 +5,9 @@
 //
 // stdin:  cap W P n, then n lines "u v"
 // stdout: one emission per window, Tuple2.toString of the Merger's summary (literal_run's format)
+// argv[1] == "restore": after every window the Merger's summary is snapshotted (its live entries)
+// and restored into another summary (load_components, gs_bip_restore's engine), which the next
+// window continues from
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -78,7 +81,38 @@ struct HostCand {
     }
 };
 
-int main() {
+// restoreState: the live (key, vertex, sign) entries of `from`, grouped by key, loaded into `to`
+static bool restore_into(HostX& x, Shared& sh, const HostCand& from, HostCand& to) {
+    to.reset();
+    if (!from.ctl.ok) {
+        to.ctl.ok = 0;
+        return true;
+    }
+    std::vector<uint32_t> rk, rv;
+    std::vector<uint64_t> ro;
+    std::vector<uint8_t> rs;
+    for (uint32_t k = 0; k < from.cap; ++k) {
+        if (from.kslot[k] == kNone || !from.comp_alive[from.kslot[k]]) continue;
+        const uint32_t c = (uint32_t)from.kslot[k];
+        std::map<uint32_t, uint32_t> m;
+        for (uint32_t i = 0; i < from.comp_size[c]; ++i) {
+            const int32_t nd = from.arena[from.comp_base[c] + i];
+            m[from.node_v[nd]] = sign_of(from.node_cs[nd]);
+        }
+        rk.push_back(k);
+        ro.push_back(rv.size());
+        for (auto& kv : m) {
+            rv.push_back(kv.first);
+            rs.push_back((uint8_t)kv.second);
+        }
+    }
+    ro.push_back(rv.size());
+    load_components(x, to.S, sh, rk.data(), ro.data(), (uint32_t)rk.size(), rv.data(), rs.data());
+    return to.ctl.err == 0;
+}
+
+int main(int argc, char** argv) {
+    const bool restore = argc > 1 && std::string(argv[1]) == "restore";
     unsigned long long cap, W, P, n;
     if (scanf("%llu %llu %llu %llu", &cap, &W, &P, &n) != 4) return 1;
     std::vector<uint32_t> s(n), d(n);
@@ -117,6 +151,20 @@ int main() {
             return 2;
         }
         printf("%s\n", summary->str().c_str());
+        if (restore) {
+            HostCand* r = nullptr;
+            for (auto* c : pool)
+                if (c != summary) r = c;
+            if (!restore_into(x, sh, *summary, *r)) {
+                printf("ERR restore %u\n", r->ctl.err);
+                return 3;
+            }
+            if (r->str() != summary->str()) {
+                printf("ERR restore mismatch\n");
+                return 4;
+            }
+            summary = r;
+        }
     }
     for (auto* c : pool) delete c;
     return 0;

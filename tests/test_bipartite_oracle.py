@@ -153,7 +153,8 @@ def test_literal_engine_on_the_host_equals_literal_oracle(tmp_path):
     """csrc/bip_literal.hpp (the engine libgsgpu.so runs as one HIP workgroup) run serially on the
     host under ASan/UBSan (tests/bipl_host_check.cpp) = oracle/bipartite.py literal_run, every
     window's emission, on 240 random streams: windows of 0-39 edges, 1-3 partitions, failures,
-    components sharing vertices and keys signed false among them."""
+    components sharing vertices and keys signed false among them; on half of them again with the
+    Merger's summary snapshotted and restored (load_components) after every window."""
     import shutil
     import subprocess
     here = os.path.dirname(os.path.abspath(__file__))
@@ -171,6 +172,12 @@ def test_literal_engine_on_the_host_equals_literal_oracle(tmp_path):
         out = subprocess.run([exe], input=inp, capture_output=True, text=True, timeout=60)
         assert out.returncode == 0, (seed, out.stderr[-2000:])
         assert out.stdout.splitlines() == want, seed
+        if seed % 2 == 0:
+            # restoreState after every window (gs_bip_restore's engine, load_components): the stream
+            # continues from the restored summary with the same emissions
+            out = subprocess.run([exe, "restore"], input=inp, capture_output=True, text=True, timeout=60)
+            assert out.returncode == 0, (seed, out.stdout[-500:], out.stderr[-2000:])
+            assert out.stdout.splitlines() == want, seed
         failed += want[-1] == "(false,{})"
         false_key += any("={%d=(%d,false)" % (k, k) in want[-1] for k in range(nv))
         import re

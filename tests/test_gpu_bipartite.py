@@ -232,7 +232,71 @@ def test_literal_errors():
         a.sync()
     assert ei.value.code == _abi.GS_ERR_RANGE
     assert a.toString() == "(true,{1={1=(1,true), 2=(2,false), 5=(5,true)}})"
-    with pytest.raises(GsError):
-        a.restore(*a.snapshot())                       # (not rebuilt from a snapshot)
+    a.restore(*a.snapshot())                           # loaded as it is (gs_bip_restore)
+    assert a.toString() == "(true,{1={1=(1,true), 2=(2,false), 5=(5,true)}})"
+    # a snapshot larger than the entry capacity
+    c = Candidates(16, literal=True, entry_capacity=3)
+    with pytest.raises(GsError) as ei:
+        c.restore(True, np.array([1, 2, 3, 4]), np.array([1, 1, 3, 3]), np.array([True, False, True, False]))
+    assert ei.value.code == _abi.GS_ERR_CAPACITY
+    # an entry twice in one component
+    with pytest.raises(GsError) as ei:
+        a.restore(True, np.array([1, 1]), np.array([1, 1]), np.array([True, True]))
+    assert ei.value.code == _abi.GS_ERR_INVALID
     a.close()
     b.close()
+    c.close()
+
+
+def test_literal_restore_overlapping_components_then_fold():
+    """gs_bip_restore of a literal snapshot whose components share a vertex (key 1 = {1, 2}, key 2 =
+    {2, 3}, 2 signed false in one and true in the other) and a key signed false, then more edges:
+    every emission equals the literal oracle started from the same map (Candidates.add, :55-67)."""
+    from bipartite import LiteralCandidates, edge_to_candidate
+    comps = {1: {1: True, 2: False}, 2: {2: True, 3: False}, 5: {5: False, 6: True}}
+    v, k, sg = [], [], []
+    for key, m in comps.items():
+        for vert, sign in m.items():
+            v.append(vert); k.append(key); sg.append(sign)
+    for id_bits in (32, 64):
+        c = Candidates(32, id_bits=id_bits, literal=True)
+        c.restore(True, np.array(v), np.array(k), np.array(sg))
+        o = LiteralCandidates(True)
+        for key in sorted(comps):
+            o.add_component(key, dict(comps[key]))
+        assert c.toString() == o.to_string()
+        for a_, b_ in [(3, 7), (6, 8), (2, 9), (1, 3), (7, 5), (4, 4)]:
+            c.fold(np.array([a_]), np.array([b_]))
+            o = o.merge(edge_to_candidate(a_, b_))
+            assert c.toString() == o.to_string(), (id_bits, a_, b_)
+        c.restore(False, np.array([], dtype=np.int64), np.array([], dtype=np.int64), np.array([], dtype=bool))
+        assert c.toString() == "(false,{})"
+        c.fold(np.array([1]), np.array([2]))
+        assert c.toString() == "(false,{})"               # Candidates.fail() is sticky
+        c.close()
+
+
+def test_literal_checkpoint_resume():
+    """snapshotState after k windows, restoreState into a NEW literal operator, run the rest: every
+    later emission equals the literal oracle's uninterrupted run (ListCheckpointed Merger,
+    SummaryAggregation.java:121-135), on random multi-window streams with components that share
+    vertices, keys signed false and failures."""
+    tried = shared = 0
+    for seed, s, d, W, P in _random_literal_cases(40, 3000):
+        if W == 0 or len(s) < 3 * W:
+            continue
+        want = literal_run(s, d, W, partitions=P)
+        k = len(want) // 2
+        op = BipartitenessCheck(1000, window_edges=W, mode="literal", parallelism=P, vertex_capacity=128)
+        state = None
+        for w, c in enumerate(SimpleEdgeStream(s[:k * W], d[:k * W]).aggregate(op)):
+            assert c.toString() == want[w], (seed, w)
+            if w == k - 1:
+                state = op.snapshotState(1, 0)
+        op2 = BipartitenessCheck(1000, window_edges=W, mode="literal", parallelism=P, vertex_capacity=128)
+        op2.restoreState(state)
+        got = [c.toString() for c in SimpleEdgeStream(s[k * W:], d[k * W:]).aggregate(op2)]
+        assert got == want[k:], seed
+        tried += 1
+        shared += any(want[k - 1].count("=(%d," % v) > 1 for v in range(128))
+    assert tried >= 10 and shared >= 2, (tried, shared)
