@@ -26,3 +26,22 @@ def test_rccl_rank_processes_every_mode_vs_oracle(world):
     assert r["ok"] and out.returncode == 0, r
     for mode, m in r["modes"].items():
         assert m["peers_exchanged"], (mode, m)
+
+
+@pytest.mark.parametrize("merge", ["prefilter", "allgather", "gather", "tree"])
+def test_bench_rank_processes_over_rccl(merge):
+    """The driver's N > 1 bench path (bench.py under torch.distributed, RCCL for torch's process group
+    and for the C-ABI exchange), two rank processes on this GPU (tools/bench_ranks_one_gpu.py):
+    both exit 0 and rank 0's final labels equal an independent torch CC of the whole stream."""
+    root = os.path.dirname(HERE)
+    cmd = [sys.executable, "-u", os.path.join(root, "tools", "bench_ranks_one_gpu.py"), "--ranks", "2", "--timeout", "300",
+           "--", "--scale", "20", "--window-log2", "18", "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
+           "--verify", "--merge", merge]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=360)
+    lines = [line for line in out.stdout.splitlines() if line.startswith("{")]
+    assert lines, (out.returncode, out.stdout[-3000:], out.stderr[-3000:])
+    r = json.loads(lines[-1])
+    assert r["ok"] and out.returncode == 0, r
+    b = r["bench_line"]
+    assert b["n_gpus"] == 2 and b["exchange"]["merge"] == merge, b
+    assert b["verify"]["equals_torch_cc"], b["verify"]

@@ -41,6 +41,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--ranks", type=int, default=2)
     ap.add_argument("--timeout", type=float, default=600.0)
+    ap.add_argument("--log-dir", default="", help="write every rank's stderr there (rank<r>.err)")
     a = ap.parse_args(argv)
     port = free_port()
     procs = []
@@ -66,6 +67,11 @@ def main() -> int:
             o, e = p.communicate()
             rcs.append("timeout")
         outs.append((o, e))
+    if a.log_dir:
+        os.makedirs(a.log_dir, exist_ok=True)
+        for r, (_, e) in enumerate(outs):
+            with open(os.path.join(a.log_dir, "rank%d.err" % r), "w") as f:
+                f.write(e)
     line = None
     for ln in outs[0][0].splitlines():
         if ln.startswith("{"):
