@@ -15,8 +15,10 @@ timings of this transport mean nothing; the emissions must be exact.
 Checks, one JSON line from the launcher: in every mode, the checked ranks' emission checksum after
 EVERY window equals the C oracle's (tests only: the oracle is the checker), and their final dense
 labels equal the oracle's (allgather: every rank is a replica of the Merger; gather / tree /
-prefilter: rank 0). Reference: SummaryBulkAggregation.java:76-83 (partitions -> windowAll ->
-Merger), SummaryTreeReduce.java:95-123 (the tree), SummaryAggregation.java:106-119 (emission).
+prefilter: rank 0); then allgather / gather / tree once more with sparse int64 ids (negative ids,
+INT64_MIN / MAX: the reference's Long keys), whose exchange carries 16-B (id, root id) pairs.
+Reference: SummaryBulkAggregation.java:76-83 (partitions -> windowAll -> Merger),
+SummaryTreeReduce.java:95-123 (the tree), SummaryAggregation.java:106-119 (emission).
 """
 from __future__ import annotations
 
@@ -34,6 +36,7 @@ for p in (HERE, ROOT, os.path.join(ROOT, "gelly-streaming_amd"), os.path.join(RO
         sys.path.insert(0, p)
 
 MODES = ("allgather", "gather", "tree", "prefilter")
+SPARSE_MODES = ("allgather", "gather", "tree")      # (prefilter: dense ids only)
 
 
 def _wait_file(path: str, timeout: float = 120.0) -> bytes:
@@ -91,6 +94,24 @@ def rank_main(a) -> int:
         ds.close()
         comm.close()
         out["modes"][mode] = rec
+    # sparse int64 ids (any Long key): the exchange carries (id, root id) 16-B pairs
+    ss = torch.from_numpy(np.load(os.path.join(a.dir, "ssrc.npy"))).cuda()
+    sd = torch.from_numpy(np.load(os.path.join(a.dir, "sdst.npy"))).cuda()
+    for mode in SPARSE_MODES:
+        uid_path = os.path.join(a.dir, "uid_sparse_%s.bin" % mode)
+        if r == 0:
+            _put_file(uid_path, unique_id())
+        comm = Comm.create(_wait_file(uid_path), r, P, 0)
+        ds = gsgpu.DisjointSet(a.sparse_cap, id_bits=64, track_marks=True, sparse=True)
+        sums = []
+        for lo, hi in rank_slices(ss.numel(), a.sparse_window, P)[r]:
+            ds.fold(ss[lo:hi], sd[lo:hi])
+            ds.merge_window(comm, mode)
+            if r == 0 or mode == "allgather":
+                sums.append([int(x) for x in ds.checksum()])
+        ds.close()
+        out["modes"]["sparse_" + mode] = {"checksums": sums, "seconds": 0.0, "info": list(comm.info())}
+        comm.close()
     with open(os.path.join(a.dir, "rank%d.json" % r), "w") as f:
         json.dump(out, f)
     return 0
@@ -105,12 +126,23 @@ def launch_main(a) -> int:
     want = oracle.run(s, d, a.window, partitions=a.world, threads=4, emit=EMIT_CHECKSUM, label_cap=cap,
                       want_final=True)
     ws = [int(x) for x in want["checksums"]]
+    ss, sd = oracle.gen_rmat(0, a.sparse_edges, 14, a.seed + 1)
+    mul = np.uint64(0x9E3779B97F4A7C15)                   # odd: an injective map over the int64 range
+    with np.errstate(over="ignore"):
+        ss = (ss.astype(np.uint64) * mul).view(np.int64)
+        sd = (sd.astype(np.uint64) * mul).view(np.int64)
+    ss[:3] = [np.iinfo(np.int64).min, np.iinfo(np.int64).max, -1]
+    sd[:3] = [-1, 5, np.iinfo(np.int64).min]
+    swant = oracle.run(ss, sd, a.sparse_window, partitions=a.world, emit=EMIT_CHECKSUM)
+    sexp = [[int(c), int(v), int(k)] for c, (v, k) in zip(swant["checksums"], swant["counts"])]
     t0 = time.time()
     res = {"world": a.world, "scale": a.scale, "edges": a.edges, "window": a.window, "windows": len(ws),
            "transport": "RCCL net (sockets over lo), one process per rank, distinct NCCL_HOSTID"}
     with tempfile.TemporaryDirectory(prefix="gs_rccl_") as tmp:
         np.save(os.path.join(tmp, "src.npy"), s)
         np.save(os.path.join(tmp, "dst.npy"), d)
+        np.save(os.path.join(tmp, "ssrc.npy"), ss)
+        np.save(os.path.join(tmp, "sdst.npy"), sd)
         procs = []
         for r in range(a.world):
             env = dict(os.environ)
@@ -118,7 +150,8 @@ def launch_main(a) -> int:
                         "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
             env.pop("GSGPU_LIB_EXP", None)
             cmd = [sys.executable, "-u", os.path.abspath(__file__), "--rank", str(r), "--world", str(a.world),
-                   "--dir", tmp, "--window", str(a.window), "--cap", str(cap), "--share0", str(a.share0)]
+                   "--dir", tmp, "--window", str(a.window), "--cap", str(cap), "--share0", str(a.share0),
+                   "--sparse-window", str(a.sparse_window), "--sparse-cap", str(a.sparse_cap)]
             procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
         rcs, logs = [], []
         deadline = time.time() + a.timeout
@@ -169,6 +202,19 @@ def launch_main(a) -> int:
             m["ok"] = all(v is None for v in first_bad.values()) and m["peers_exchanged"]
             ok &= m["ok"]
             modes[mode] = m
+        for mode in SPARSE_MODES:
+            checked = list(range(a.world)) if mode == "allgather" else [0]
+            recs = [ranks[r]["modes"]["sparse_" + mode] for r in range(a.world)]
+            first_bad = {}
+            for r in checked:
+                got = recs[r]["checksums"]
+                first_bad[r] = next((w for w in range(len(sexp)) if w >= len(got) or got[w] != sexp[w]), None)
+            m = {"checked_ranks": checked, "ids": "sparse int64 (16-B pairs)",
+                 "bytes_recv": [x["info"][3] for x in recs], "first_bad_window": first_bad,
+                 "peers_exchanged": sum(x["info"][3] for x in recs) > 0}
+            m["ok"] = all(v is None for v in first_bad.values()) and m["peers_exchanged"]
+            ok &= m["ok"]
+            modes["sparse_" + mode] = m
         res["modes"] = modes
     res["ok"] = bool(ok)
     res["seconds"] = round(time.time() - t0, 1)
@@ -188,6 +234,9 @@ def main() -> int:
     ap.add_argument("--cap", type=int, default=0)
     ap.add_argument("--share0", type=float, default=0.125)
     ap.add_argument("--seed", type=int, default=31)
+    ap.add_argument("--sparse-edges", type=int, default=120000)
+    ap.add_argument("--sparse-window", type=int, default=20000)
+    ap.add_argument("--sparse-cap", type=int, default=1 << 15)
     ap.add_argument("--timeout", type=float, default=240.0)
     a = ap.parse_args()
     return rank_main(a) if a.rank >= 0 else launch_main(a)
