@@ -148,7 +148,6 @@ def launch_main(a) -> int:
             env = dict(os.environ)
             env.update({"NCCL_HOSTID": "gsgpu-rccl-rank%d" % r, "NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1",
                         "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
-            env.pop("GSGPU_LIB_EXP", None)
             cmd = [sys.executable, "-u", os.path.abspath(__file__), "--rank", str(r), "--world", str(a.world),
                    "--dir", tmp, "--window", str(a.window), "--cap", str(cap), "--share0", str(a.share0),
                    "--sparse-window", str(a.sparse_window), "--sparse-cap", str(a.sparse_cap)]
