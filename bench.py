@@ -576,11 +576,15 @@ def steady_profile(a, kernel, edges_per_launch):
 
 
 def request_roofline(prof, avg_ms):
-    """What bounds the steady fold besides bytes: L2 requests. Per launch, the PMC passes give its TCC
-    requests and its HBM bytes; tools/request_lab.hip measured what this chip sustains:
-    random 4-B loads over an L2-resident table (the request rate of L2 channels) and a streaming
-    read. Bound = max(requests / L2 request rate, HBM bytes / stream rate): the two are served by
-    different units and overlap."""
+    """What bounds the steady fold besides bytes: memory requests. Per launch, the PMC passes give
+    its TCC requests, their L2 hit rate and its HBM bytes; tools/request_lab.hip measured what this
+    chip sustains: random 4-B loads over an L2-resident table (1 MiB: the request rate of the L2
+    channels), over a table far larger than an L2 (64 MiB: the rate of requests that MISS the L2 and
+    go to the fabric / Infinity Cache / HBM), and a streaming read. Bound = max(requests / L2 rate,
+    L2 misses / miss rate, HBM bytes / stream rate): the three are served by different units and
+    overlap. The miss term is the tight one for the ring fold (round 6): its ~9 M misses per launch
+    are the gbits lines of cold ids (8 MiB bitmap against a 4 MiB L2 that also holds the 2 MiB warm
+    set), the survivors' parent[] lines and the edge stream."""
     lab_path = os.path.join(ROOT, "profiles", "r03_request_lab.json")
     if not os.path.exists(lab_path):
         return None
@@ -588,16 +592,23 @@ def request_roofline(prof, avg_ms):
         lab = json.load(open(lab_path))
         req, hbm = prof["tcc_requests_per_launch"], prof["hbm_bytes_per_launch"]
         req_gps, stream_tbps = lab["rand4B_1MiB_32w_Gps"], lab["stream_read_TBps"]
+        miss_gps = lab["rand4B_64MiB_32w_Gps"]
+        hit = prof.get("l2_hit_rate")
+        misses = req * (1.0 - hit) if hit is not None else None
         t_req = req / (req_gps * 1e3)                                     # us
+        t_miss = misses / (miss_gps * 1e3) if misses is not None else 0.0
         t_bytes = hbm / (stream_tbps * 1e6)
-        bound_us = max(t_req, t_bytes)
-        return {"bound": "l2-requests" if t_req >= t_bytes else "hbm-bytes", "tcc_requests_per_launch": req,
-                "hbm_bytes_per_launch": hbm, "request_peak_Gps": req_gps, "stream_peak_TBps": stream_tbps,
-                "requests_us": t_req, "bytes_us": t_bytes, "bound_us": bound_us, "avg_launch_us": avg_ms * 1e3,
-                "frac": bound_us / (avg_ms * 1e3),
-                "definition": "max(TCC requests / L2 random-request rate, PMC HBM bytes / streaming-read rate) per "
-                              "launch (counts: profiles/fold_traffic.json; rates: tools/request_lab.hip, "
-                              "profiles/r03_request_lab.json) / the launch's average duration"}
+        bound_us = max(t_req, t_miss, t_bytes)
+        bound = "l2-misses" if bound_us == t_miss else ("l2-requests" if bound_us == t_req else "hbm-bytes")
+        return {"bound": bound, "tcc_requests_per_launch": req, "l2_hit_rate": hit, "l2_misses_per_launch": misses,
+                "hbm_bytes_per_launch": hbm, "request_peak_Gps": req_gps, "miss_peak_Gps": miss_gps,
+                "stream_peak_TBps": stream_tbps, "requests_us": t_req, "misses_us": t_miss, "bytes_us": t_bytes,
+                "bound_us": bound_us, "avg_launch_us": avg_ms * 1e3, "frac": bound_us / (avg_ms * 1e3),
+                "frac_requests_only": t_req / (avg_ms * 1e3),
+                "definition": "max(TCC requests / L2 random-request rate, L2 misses / random-miss rate, PMC HBM "
+                              "bytes / streaming-read rate) per launch (counts: profiles/fold_traffic.json; rates: "
+                              "tools/request_lab.hip, profiles/r03_request_lab.json: 1 MiB / 64 MiB random 4-B "
+                              "loads, streaming read) / the launch's average duration"}
     except Exception:
         return None
 

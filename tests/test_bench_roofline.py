@@ -81,3 +81,19 @@ def test_request_roofline_definition():
     assert r["bound"] == ("l2-requests" if t_req >= t_b else "hbm-bytes")
     # the lab's ordering: L2-resident > Infinity Cache >= HBM for random 4-B loads
     assert lab["rand4B_1MiB_32w_Gps"] > lab["rand4B_8MiB_32w_Gps"] > lab["rand4B_64MiB_32w_Gps"] >= lab["rand4B_2GiB_32w_Gps"]
+
+
+def test_request_roofline_miss_term():
+    """With the L2 hit rate in the profile, the misses go to the fabric at the lab's random-miss rate
+    (64 MiB table); the bound is the largest of the three terms."""
+    bench, a = _bench()
+    lab = json.load(open(os.path.join(ROOT, "profiles", "r03_request_lab.json")))
+    prof = {"tcc_requests_per_launch": 34.85e6, "hbm_bytes_per_launch": 636e6, "l2_hit_rate": 0.74}
+    r = bench.request_roofline(prof, 0.22)
+    t_req = 34.85e6 / (lab["rand4B_1MiB_32w_Gps"] * 1e3)
+    t_miss = 34.85e6 * 0.26 / (lab["rand4B_64MiB_32w_Gps"] * 1e3)
+    t_b = 636e6 / (lab["stream_read_TBps"] * 1e6)
+    assert abs(r["l2_misses_per_launch"] - 34.85e6 * 0.26) < 1.0
+    assert abs(r["bound_us"] - max(t_req, t_miss, t_b)) < 1e-9
+    assert r["bound"] == "l2-misses" and t_miss > t_req
+    assert abs(r["frac"] - r["bound_us"] / 220.0) < 1e-9
