@@ -309,6 +309,7 @@ constexpr int kSmallEpt = 1;
 //   GSGPU_FOLD_MODE=plain|ring|auto   force the steady fold variant (parity tests of each variant)
 //   GSGPU_RING_MIN_BITS=B    ring fold + warm set from ids >= 2^B instead of 2^25 (tests at small sizes)
 //   GSGPU_YOUNG_SPLIT=S      young split after S edges (default: none; tests and A/B)
+//   GSGPU_PAIR_COMBINE=0     pair / survivor folds without wave-combined hooks (A/B)
 enum FoldMode { kFoldPlain = 0, kFoldRing = 1, kFoldAuto = 2 };
 struct DebugEnv {
     bool fold_stats = false;
@@ -321,6 +322,8 @@ struct DebugEnv {
     uint64_t young_first_min = kYoungFirstMinWg;    // GSGPU_YOUNG_FIRST_MIN: workgroup floor of the first young launch
     bool list_close = true;                         // GSGPU_LIST_CLOSE=0: no list-mode closes (A/B)
     bool small_claim = true;                        // GSGPU_SMALL_CLAIM=0: small k_fold launches without claims (A/B)
+    bool pair_combine = true;                       // GSGPU_PAIR_COMBINE=0: pair folds without combined hooks (A/B)
+    uint32_t pair_halve = 1;                        // GSGPU_PAIR_HALVE=0: pair folds walk read-only (A/B)
     DebugEnv() {
         const char* e = getenv("GSGPU_FOLD_STATS");
         fold_stats = e && atoi(e) != 0;
@@ -343,6 +346,10 @@ struct DebugEnv {
         if (e && *e) list_close = atoi(e) != 0;
         e = getenv("GSGPU_SMALL_CLAIM");
         if (e && *e) small_claim = atoi(e) != 0;
+        e = getenv("GSGPU_PAIR_COMBINE");
+        if (e && *e) pair_combine = atoi(e) != 0;
+        e = getenv("GSGPU_PAIR_HALVE");
+        if (e && *e) pair_halve = atoi(e) != 0 ? 1u : 0u;
 
     }
 };
@@ -383,6 +390,8 @@ void launch_fold(gs_cc_t* h, const void* a, const void* b, uint64_t n, bool youn
     ensure_stats(h);
     FoldArgs f{n, h->parent, h->mark, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, h->dstats};
     f.mark_len = h->mark_ctr;
+    f.combine = (AOS && dbg().pair_combine) ? 1u : 0u;   // pair / survivor folds (combine_hooks)
+    if (AOS) f.halve = dbg().pair_halve;
     // hooked roots marked (while no giant exists, k_fold) by mature SoA launches only: in the young
     // forest the marks would cost an atomic per hook for a close whose grandparent reads hit L2
     // anyway (an RMAT window 1's non-roots hang under a few hub roots)
@@ -952,6 +961,8 @@ int cc_fold_slots(gs_cc_t* h, const uint32_t* slots, uint64_t slot_words, int ns
     h->compressed = false;
     h->minkey_valid = false;
     FoldArgs f{0, h->parent, nullptr, h->sbits, h->gbits, giant_state(h), RangeCheck{h->cap, h->derr}, nullptr};
+    f.combine = dbg().pair_combine ? 1u : 0u;        // (combine_hooks)
+    f.halve = dbg().pair_halve;
     KTimer t(h, GS_K_MERGE);
     h->hkbits_ok = false;
     h->ilist_ok = false;

@@ -301,6 +301,7 @@ struct FoldArgs {
     // wave 0; in the kernel, tlog is the wave's own slot and tcnt its entry count in LDS
     uint32_t* tlog = nullptr;
     uint32_t* tcnt = nullptr;
+    uint32_t combine = 0;        // pair / survivor folds: wave-combined hooks of one root word (combine_hooks)
 };
 
 // A wave's first touches (t[k] != kInvalid) appended to its touch-log slot: ballots over the active
@@ -623,6 +624,64 @@ __device__ __forceinline__ void filter_group(const FoldArgs& f, const uint32_t (
 }
 
 // Parent gathers and unions of the edges with ok[k] (all issued before any dependent step).
+// Pair folds (f.combine: a received partial summary's (v, R) pairs, the Merger's survivors): the
+// pairs of one sender component all name its root R, and while R's component is not yet joined to
+// the receiver's every lane whose v has the smaller root CASes the same word (R's root) — one
+// succeeds, the rest fail and re-walk, serialised at the memory-side atomic unit (the all-gather's
+// window-1 merge at ~2.3 G pairs/s, window 5's at 0.6: profiles/r05_allgather_sim_p8.txt). Within a
+// wave the lanes whose unions hook the same root H are combined first: the lane holding the
+// smallest other root Lmin keeps union(H, Lmin); a lane whose other root is Lmin too has nothing
+// left (the same union); any other lane's union(H, lo) becomes union(lo, Lmin) — the same
+// components joined, over distinct words. One CAS on H per wave instead of one per lane.
+// Every lane of a live union leaves here holding its two ROOTS (fresh = its parent word kInvalid),
+// so union_edge does not walk again. Ballots and shuffles read only active lanes' values except in
+// the min reduction, whose result is checked against the lanes (no owner: nothing combined).
+__device__ __forceinline__ void combine_hooks(uint32_t* __restrict__ parent, bool halve, bool live, uint32_t& u,
+                                              uint32_t& v, uint32_t& pu, uint32_t& pv, bool& skip) {
+    skip = false;
+    const bool fu = pu == kInvalid, fv = pv == kInvalid;
+    if (live && (u == v || (!fu && !fv && pu == pv))) live = false;    // self-loop / common parent: union_edge's
+    uint32_t ru = 0, rv = 0;
+    if (live) {
+        ru = fu ? u : find_root(parent, u, pu, halve);
+        rv = fv ? v : find_root(parent, v, pv, halve);
+        if (ru == rv) {                                                 // one component already
+            live = false;
+            skip = true;
+        }
+    }
+    const uint32_t hi = ru > rv ? ru : rv, lo = ru > rv ? rv : ru;
+    const bool fhi = ru > rv ? fu : fv, flo = ru > rv ? fv : fu;       // fresh: the root is the vertex
+    if (live) {
+        u = hi;
+        pu = fhi ? kInvalid : hi;
+        v = lo;
+        pv = flo ? kInvalid : lo;
+    }
+    const uint64_t lm = __ballot(live);
+    if (!lm) return;                                                    // uniform
+    const uint32_t H = __shfl(hi, __ffsll((long long)lm) - 1, 64);
+    const bool same = live && hi == H;
+    if (__popcll(__ballot(same)) < 2) return;                           // uniform
+    uint32_t x = same ? lo : 0xFFFFFFFFu;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x = min(x, (uint32_t)__shfl_xor(x, off, 64));
+    const uint64_t om = __ballot(same && lo == x);
+    if (!om || !same) return;                                           // (om == 0: an inactive lane's value)
+    if ((int)__lane_id() == __ffsll((long long)om) - 1) return;         // the owner: union(H, Lmin)
+    if (lo == x) {                                                      // the owner's union
+        skip = true;
+        return;
+    }
+    // union(lo, Lmin): Lmin is a root, or fresh and initialised by the owner's union (H > Lmin); a
+    // hook of lo under a not yet initialised Lmin is the transient union_edge already tolerates (a
+    // walk stops at a kInvalid word; a CAS expecting Lmin there retries from kInvalid)
+    u = lo;
+    pu = flo ? kInvalid : lo;
+    v = x;
+    pv = x;
+}
+
 template <bool MARK, bool STATS, int EPT>
 __device__ __forceinline__ void union_group(const FoldArgs& f, const uint32_t (&u)[EPT], const uint32_t (&v)[EPT],
                                             const bool (&ok)[EPT], FoldStats& st) {
@@ -647,6 +706,16 @@ __device__ __forceinline__ void union_group(const FoldArgs& f, const uint32_t (&
             t[2 * k + 1] = nl[k].b;
         }
         slot_append<2 * EPT>(f.tlog, f.tcnt, t);
+    } else if (f.combine) {                          // pair folds: combined hooks (combine_hooks)
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const bool halve = f.halve == 1 || (f.halve > 1 && ((u[k] * 0x9E3779B1u) >> 29) == 0);
+            uint32_t cu = u[k], cv = v[k];
+            bool skip;
+            combine_hooks(f.parent, halve, ok[k], cu, cv, pu[k], pv[k], skip);
+            m[k] = (ok[k] && !skip) ? union_edge<MARK, STATS>(f.parent, f.sbits, cu, cv, pu[k], pv[k], &st, halve, f.hbits)
+                                    : kInvalid;
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < EPT; ++k)
@@ -756,6 +825,16 @@ __device__ __forceinline__ void union_group_gl(const FoldArgs& f, const uint32_t
             t[2 * k + 1] = nl[k].b;
         }
         slot_append<2 * EPT>(f.tlog, f.tcnt, t);
+    } else if (f.combine) {                          // pair folds: combined hooks (combine_hooks)
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            uint32_t cu = u[k], cv = v[k];
+            bool skip;
+            combine_hooks(f.parent, f.halve != 0, ok[k] && !claimed[k], cu, cv, pu[k], pv[k], skip);
+            if (claimed[k]) m[k] = MARK ? ((gflag[k] == 2u) ? u[k] : v[k]) : kInvalid;
+            else m[k] = (ok[k] && !skip) ? union_edge<MARK, STATS>(f.parent, f.sbits, cu, cv, pu[k], pv[k], &st, f.halve != 0, f.hbits)
+                                         : kInvalid;
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < EPT; ++k) {
